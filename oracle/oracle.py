@@ -1,0 +1,192 @@
+"""ctypes view of the CPU oracle (oracle/libntt_oracle.so).
+
+TEST INFRASTRUCTURE ONLY.  This module is imported by tests/, by
+``__graft_entry__.smoke()`` and by ``bench.py``'s ``cpu_baseline`` leg — as the
+*checker* and the CPU baseline, never as the thing measured or shipped.  The
+product package (``tfhe-rs-main_modified_amd/``) never imports it.
+
+Every function restates the reference named in ``ntt_oracle.h`` /
+``pbs_oracle.h`` (file:line citations live next to each C function).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libntt_oracle.so")
+
+SOLINAS_P = 0xFFFFFFFF00000001
+
+_u64 = ctypes.c_uint64
+_sz = ctypes.c_size_t
+_p64 = ctypes.POINTER(ctypes.c_uint64)
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc only; no reference sources are used)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        sigs = {
+            "ora_mul_mod": (_u64, [_u64, _u64, _u64]),
+            "ora_exp_mod": (_u64, [_u64, _u64, _u64]),
+            "ora_is_prime64": (ctypes.c_int, [_u64]),
+            "ora_largest_prime_in_ap": (ctypes.c_int, [_u64, _u64, _u64, _u64, _p64]),
+            "ora_find_primitive_root64": (ctypes.c_int, [_u64, _u64, _p64]),
+            "ora_find_root_solinas64": (ctypes.c_int, [_u64, _p64]),
+            "ora_plan_init": (ctypes.c_int, [_sz, _u64, _p64, _p64, _p64]),
+            "ora_fwd": (None, [_sz, _u64, _p64, _p64]),
+            "ora_inv": (None, [_sz, _u64, _p64, _p64]),
+            "ora_fwd_batch": (None, [_sz, _u64, _p64, _p64, _sz, _sz, ctypes.c_int]),
+            "ora_inv_batch": (None, [_sz, _u64, _p64, _p64, _sz, _sz, ctypes.c_int]),
+            "ora_mul_accumulate": (None, [_sz, _u64, _p64, _p64, _p64]),
+            "ora_normalize": (None, [_sz, _u64, _u64, _p64]),
+            "ora_mul_assign_normalize": (None, [_sz, _u64, _u64, _p64, _p64]),
+            "ora_negacyclic_convolution": (None, [_sz, _u64, _p64, _p64, _p64]),
+            "ora_have_avx512": (ctypes.c_int, []),
+            "ora_fwd_batch_avx512": (ctypes.c_int, [_sz, _p64, _p64, _sz, _sz, ctypes.c_int]),
+            "ora_inv_batch_avx512": (ctypes.c_int, [_sz, _p64, _p64, _sz, _sz, ctypes.c_int]),
+            "ora_fill_uniform": (None, [_u64, _u64, _p64, _sz]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_p64)
+
+
+def _opt(fn, *args):
+    out = _u64(0)
+    ok = fn(*args, ctypes.byref(out))
+    return int(out.value) if ok else None
+
+
+# ---- number theory -------------------------------------------------------
+def mul_mod(a, b, p):
+    return int(lib().ora_mul_mod(a, b, p))
+
+
+def exp_mod(base, pow_, p):
+    return int(lib().ora_exp_mod(base, pow_, p))
+
+
+def is_prime64(n):
+    return bool(lib().ora_is_prime64(n))
+
+
+def largest_prime_in_arithmetic_progression64(factor, offset, lo, hi):
+    return _opt(lib().ora_largest_prime_in_ap, factor, offset, lo, hi)
+
+
+def find_primitive_root64(p, degree):
+    return _opt(lib().ora_find_primitive_root64, p, degree)
+
+
+def find_root_solinas_64(degree):
+    return _opt(lib().ora_find_root_solinas64, degree)
+
+
+# ---- Plan ------------------------------------------------------------------
+class Plan:
+    """Oracle twin of ``tfhe_ntt::prime64::Plan`` (prime64.rs:245-1222)."""
+
+    def __init__(self, n, p, twid, inv_twid, n_inv):
+        self.n, self.p, self.twid, self.inv_twid, self.n_inv = n, p, twid, inv_twid, n_inv
+
+    @staticmethod
+    def try_new(n: int, p: int):
+        twid = np.zeros(max(n, 1), np.uint64)
+        inv = np.zeros(max(n, 1), np.uint64)
+        n_inv = _u64(0)
+        ok = lib().ora_plan_init(n, p, _ptr(twid), _ptr(inv), ctypes.byref(n_inv))
+        return Plan(n, p, twid, inv, int(n_inv.value)) if ok else None
+
+    def ntt_size(self):
+        return self.n
+
+    def modulus(self):
+        return self.p
+
+    def _batch(self, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.uint64)
+        assert buf.size % self.n == 0, "buffer length must be a multiple of the NTT size"
+        return buf
+
+    def fwd(self, buf: np.ndarray, threads: int = 1) -> np.ndarray:
+        out = self._batch(buf).copy()
+        lib().ora_fwd_batch(self.n, self.p, _ptr(self.twid), _ptr(out), out.size // self.n, self.n, threads)
+        return out.reshape(np.shape(buf))
+
+    def inv(self, buf: np.ndarray, threads: int = 1) -> np.ndarray:
+        out = self._batch(buf).copy()
+        lib().ora_inv_batch(self.n, self.p, _ptr(self.inv_twid), _ptr(out), out.size // self.n, self.n, threads)
+        return out.reshape(np.shape(buf))
+
+    def normalize(self, x):
+        out = self._batch(x).copy()
+        lib().ora_normalize(out.size, self.p, self.n_inv, _ptr(out))
+        return out.reshape(np.shape(x))
+
+    def mul_assign_normalize(self, lhs, rhs):
+        out = self._batch(lhs).copy()
+        r = np.ascontiguousarray(rhs, dtype=np.uint64).reshape(-1)
+        lib().ora_mul_assign_normalize(out.size, self.p, self.n_inv, _ptr(out), _ptr(r))
+        return out.reshape(np.shape(lhs))
+
+    def mul_accumulate(self, acc, lhs, rhs):
+        out = self._batch(acc).copy()
+        l = np.ascontiguousarray(lhs, dtype=np.uint64).reshape(-1)
+        r = np.ascontiguousarray(rhs, dtype=np.uint64).reshape(-1)
+        lib().ora_mul_accumulate(out.size, self.p, _ptr(out), _ptr(l), _ptr(r))
+        return out.reshape(np.shape(acc))
+
+    # CPU baseline (restated AVX-512 fast path, Solinas only)
+    def fwd_avx512_inplace(self, buf: np.ndarray, threads: int) -> bool:
+        assert self.p == SOLINAS_P
+        return bool(lib().ora_fwd_batch_avx512(self.n, _ptr(self.twid), _ptr(buf), buf.size // self.n, self.n, threads))
+
+    def inv_avx512_inplace(self, buf: np.ndarray, threads: int) -> bool:
+        assert self.p == SOLINAS_P
+        return bool(lib().ora_inv_batch_avx512(self.n, _ptr(self.inv_twid), _ptr(buf), buf.size // self.n, self.n, threads))
+
+    def fwd_scalar_inplace(self, buf: np.ndarray, threads: int) -> None:
+        lib().ora_fwd_batch(self.n, self.p, _ptr(self.twid), _ptr(buf), buf.size // self.n, self.n, threads)
+
+    def inv_scalar_inplace(self, buf: np.ndarray, threads: int) -> None:
+        lib().ora_inv_batch(self.n, self.p, _ptr(self.inv_twid), _ptr(buf), buf.size // self.n, self.n, threads)
+
+
+def have_avx512() -> bool:
+    return bool(lib().ora_have_avx512())
+
+
+def negacyclic_convolution(n, p, lhs, rhs):
+    out = np.zeros(n, np.uint64)
+    l = np.ascontiguousarray(lhs, dtype=np.uint64)
+    r = np.ascontiguousarray(rhs, dtype=np.uint64)
+    lib().ora_negacyclic_convolution(n, p, _ptr(l), _ptr(r), _ptr(out))
+    return out
+
+
+def fill_uniform(seed: int, p: int, count: int) -> np.ndarray:
+    out = np.zeros(count, np.uint64)
+    lib().ora_fill_uniform(seed & 0xFFFFFFFFFFFFFFFF, p, _ptr(out), count)
+    return out

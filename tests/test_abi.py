@@ -1,0 +1,66 @@
+"""The C-ABI library loads and exports every symbol the public header declares; argument
+validation paths that need no device behave like the reference's `Plan::try_new` (no GPU)."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def test_library_exports_header_symbols(engine):
+    from tfhe_ntt_amd import _lib
+
+    L = _lib.lib()
+    syms = _lib.declared_symbols()
+    assert "mi_ntt64_fwd_batch" in syms and "mi_ntt64_plan_create" in syms
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    # and nm agrees that they are real exported (T) text symbols of the .so
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(syms) <= exported
+
+
+def test_library_is_gfx950_code_object(engine):
+    from tfhe_ntt_amd import _lib
+
+    out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+@pytest.mark.parametrize("n,p,status", [
+    (8, 0xFFFFFFFF00000001, 1),      # N < 16 -> None (prime64.rs:769)
+    (48, 0xFFFFFFFF00000001, 1),     # not a power of two
+    (0, 0xFFFFFFFF00000001, 1),
+    (2048, 1024, 2),                 # not prime (prime64.rs:1988-1990 test_plan_crash_github_11)
+    (2048, 2**61 - 1, 3),            # prime without a 4096-th root of unity
+])
+def test_plan_create_rejects_like_reference(engine, n, p, status):
+    from tfhe_ntt_amd import _lib
+
+    h = ctypes.c_void_p()
+    st = _lib.lib().mi_ntt64_plan_create(n, p, 0, ctypes.byref(h))
+    assert st == status and not h.value
+    assert engine.Plan.try_new(n, p) is None
+    assert _lib.lib().mi_status_string(st)
+
+
+def test_null_arguments_are_errors_not_crashes(engine):
+    from tfhe_ntt_amd import _lib
+
+    L = _lib.lib()
+    assert L.mi_ntt64_plan_create(2048, 0xFFFFFFFF00000001, 0, None) == _lib.MI_ERR_INVALID_ARG
+    assert L.mi_ntt64_fwd_batch(None, None, 1, 2048, None) == _lib.MI_ERR_INVALID_ARG
+    assert L.mi_ntt64_plan_info(None, None, None, None) == _lib.MI_ERR_INVALID_ARG
+    assert L.mi_ntt64_plan_destroy(None) == _lib.MI_OK
+    assert b"NULL" in L.mi_last_error_message()
+
+
+def test_header_compiles_as_c(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "tfhe_ntt_amd.h"\nint main(void){ return (int)sizeof(&mi_ntt64_fwd_batch) == 0; }\n')
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c",
+                        str(src), "-o", str(tmp_path / "t.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

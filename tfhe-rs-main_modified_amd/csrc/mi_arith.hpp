@@ -1,0 +1,101 @@
+// mi_arith.hpp — device-side modular arithmetic for the MI355X NTT engine (gfx950).
+//
+// Two modulus policies with the same interface (add / sub / mul, canonical in [0,p)):
+//
+//  * Goldilocks  p = 2^64 - 2^32 + 1.  The reference reduces a 128-bit product with the
+//    Solinas identity 2^64 = 2^32 - 1, 2^96 = -1 (tfhe-ntt/src/prime64/generic_solinas.rs:102-128).
+//    gfx950 has no 64x64 multiply: the product is four v_mad_u64_u32 on 32-bit limbs, the
+//    reduction is pure 32/64-bit VALU.  Multiplication by a power of two (the "friendly"
+//    twiddles of prime64.rs:162-177, F6 in SURVEY.md) is a shift + the same reduction.
+//
+//  * Montgomery  any odd p < 2^64 (the generic prime64 path, prime64.rs:957-966): twiddles are
+//    pre-scaled by R = 2^64 on the host, so a*w_mont*R^-1 = a*w (mod p), canonical out.
+//
+// Every op takes canonical inputs (< p) and returns the canonical residue, so any factorisation
+// of the transform reproduces the reference bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mi {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+static constexpr u64 GL_P = 0xFFFFFFFF00000001ull;
+static constexpr u64 GL_EPS = 0xFFFFFFFFull;  // 2^64 mod p = 2^32 - 1
+
+__device__ __forceinline__ u32 lo32(u64 x) { return (u32)x; }
+__device__ __forceinline__ u32 hi32(u64 x) { return (u32)(x >> 32); }
+
+// 64x64 -> 128 with four 32x32+64 multiply-adds (v_mad_u64_u32).
+__device__ __forceinline__ void mul64x64(u64 a, u64 b, u64 &lo, u64 &hi) {
+  const u32 a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
+  const u64 p00 = (u64)a0 * b0;
+  const u64 p10 = (u64)a1 * b0 + (p00 >> 32);
+  const u64 p01 = (u64)a0 * b1 + (u64)lo32(p10);
+  const u64 p11 = (u64)a1 * b1 + (p10 >> 32) + (p01 >> 32);
+  lo = (u64)lo32(p00) | ((u64)lo32(p01) << 32);
+  hi = p11;
+}
+
+struct Goldilocks {
+  static constexpr u64 P = GL_P;
+
+  // a + b mod p.  If the 64-bit add carries, s + (2^32-1) is already canonical; otherwise
+  // subtract p (= add 2^32-1 mod 2^64) when s >= p.
+  __device__ __forceinline__ static u64 add(u64 a, u64 b) {
+    const u64 s = a + b;
+    const bool c = s < a;
+    return (c || s >= P) ? s + GL_EPS : s;
+  }
+  // a - b mod p.  On borrow, d + p = d - (2^32-1) (mod 2^64) and cannot underflow.
+  __device__ __forceinline__ static u64 sub(u64 a, u64 b) {
+    const u64 d = a - b;
+    return (a < b) ? d - GL_EPS : d;
+  }
+  // (hi:lo) mod p for any 128-bit value: hi = hh*2^32 + hl, 2^96 = -1, 2^64 = 2^32 - 1.
+  __device__ __forceinline__ static u64 reduce128(u64 lo, u64 hi) {
+    const u32 hh = hi32(hi), hl = lo32(hi);
+    u64 t0 = lo - (u64)hh;
+    t0 = (lo < (u64)hh) ? t0 - GL_EPS : t0;
+    const u64 t1 = ((u64)hl << 32) - (u64)hl;
+    const u64 r = t0 + t1;
+    const bool c = r < t1;
+    return (c || r >= P) ? r + GL_EPS : r;
+  }
+  __device__ __forceinline__ static u64 mul(u64 a, u64 b) {
+    u64 lo, hi;
+    mul64x64(a, b, lo, hi);
+    return reduce128(lo, hi);
+  }
+};
+
+// Generic odd modulus p < 2^64 in Montgomery form (R = 2^64).  `pinv` = -p^{-1} mod 2^64.
+struct Montgomery {
+  u64 p, pinv, r2;  // r2 = R^2 mod p (to enter Montgomery form on device)
+  __device__ __forceinline__ u64 add(u64 a, u64 b) const {
+    const u64 neg_b = p - b;
+    return a >= neg_b ? a - neg_b : a + b;
+  }
+  __device__ __forceinline__ u64 sub(u64 a, u64 b) const {
+    return a >= b ? a - b : a + (p - b);
+  }
+  // REDC(a*b): a < p, b < p  ->  a*b*R^-1 mod p, canonical.
+  __device__ __forceinline__ u64 mul(u64 a, u64 b) const {
+    u64 tlo, thi;
+    mul64x64(a, b, tlo, thi);
+    const u64 m = tlo * pinv;
+    u64 mlo, mhi;
+    mul64x64(m, p, mlo, mhi);
+    // tlo + mlo == 0 mod 2^64; carry out iff tlo != 0
+    const u64 c = (tlo != 0) ? 1 : 0;
+    const u64 s = thi + mhi;
+    const bool ov1 = s < thi;
+    const u64 t = s + c;
+    const bool ov = ov1 || (t < s);
+    return (ov || t >= p) ? t - p : t;
+  }
+};
+
+}  // namespace mi

@@ -1,0 +1,281 @@
+// ntt64_kernels.hip — batched negacyclic NTT over u64 primes for MI355X (gfx950).
+//
+// Reference semantics (paths relative to /root/reference/tfhe-ntt/src):
+//   forward  = prime64.rs:897-968 -> generic_solinas.rs:449-481/931-1032 (radix-2 Cooley-Tukey,
+//              twiddle twid[m + i] for block i at stage m, natural order in, bit-reversed out)
+//   inverse  = prime64.rs:975-1046 -> generic_solinas.rs:483-561/1036 (Gentleman-Sande with
+//              inv_twid[m + i], bit-reversed in, natural order out, unnormalised)
+//
+// MI355X design (not a translation of the CPU schedule):
+//   * one workgroup owns PPW whole polynomials; each lane keeps E = 2^LOGE coefficients in
+//     VGPRs and runs LOGE radix-2 stages on them with no data movement ("register window");
+//   * between windows the polynomial is transposed through LDS (padded layout), so the N-point
+//     transform costs ceil(LOGN / LOGE) - 1 LDS round trips and exactly one HBM read + write;
+//   * twiddles come from a plan-owned device table (16 KiB at N = 2048, L2/L1 resident);
+//   * Goldilocks arithmetic is 32-bit-limb VALU (no MFMA: integer modular arithmetic).
+// Bit-exactness follows from canonical arithmetic: any schedule of the same
+// butterflies with the same twiddles returns the same residues.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mi_arith.hpp"
+#include "ntt64_launch.hpp"
+
+namespace mi {
+
+template <int LOGN_, int LOGE_>
+struct Geo {
+  static constexpr int LOGN = LOGN_;
+  static constexpr int LOGE = LOGE_;
+  static constexpr int N = 1 << LOGN;
+  static constexpr int E = 1 << LOGE;
+  static constexpr int LOGT = LOGN - LOGE;  // lanes per polynomial = 2^LOGT
+  static constexpr int T = 1 << LOGT;
+  static constexpr int PPW = T >= 64 ? 1 : 64 / T;  // polynomials per workgroup
+  static constexpr int THREADS = T * PPW;
+  static constexpr int NFULL = LOGN / LOGE;
+  static constexpr int REM = LOGN % LOGE;
+  static constexpr int NWIN = NFULL + (REM ? 1 : 0);
+  // LDS image: 4 u64 of padding per 32 (keeps the strided window reads off shared banks)
+  static constexpr int PADDED = N + (N >> 3);
+  static_assert(LOGN >= LOGE, "window wider than the transform");
+  static_assert(THREADS <= 1024, "workgroup too large");
+};
+
+__device__ __forceinline__ int lds_addr(int e) { return e + ((e >> 5) << 2); }
+
+template <class G>
+__device__ __forceinline__ int elem(int t, int r, int lo) {
+  return ((t >> lo) << (lo + G::LOGE)) | (r << lo) | (t & ((1 << lo) - 1));
+}
+
+// window geometry: low bit of the register window and how many of its bits are new stages
+template <class G, bool FWD>
+__device__ __forceinline__ constexpr int win_lo(int w) {
+  if (FWD) return (w < G::NFULL) ? G::LOGN - G::LOGE * (w + 1) : 0;
+  return (w < G::NFULL) ? G::LOGE * w : G::LOGN - G::LOGE;
+}
+
+template <class G, bool FWD, class Mod>
+__device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w, const u64* __restrict__ tw,
+                                                   const Mod& mod) {
+  const int lo = win_lo<G, FWD>(w);
+  // r-bits of this window that still need a stage
+  int rb_first, rb_last;
+  if (w < G::NFULL) { rb_first = 0; rb_last = G::LOGE - 1; }
+  else if (FWD) { rb_first = 0; rb_last = G::REM - 1; }
+  else { rb_first = G::LOGE - G::REM; rb_last = G::LOGE - 1; }
+
+#pragma unroll
+  for (int s = 0; s < G::LOGE; ++s) {
+    const int rb = FWD ? (G::LOGE - 1 - s) : s;
+    if (rb < rb_first || rb > rb_last) continue;
+    const int b = lo + rb;                       // butterfly bit of the element index
+    const int m = 1 << (G::LOGN - 1 - b);        // reference's `m` for this stage
+    const int half = 1 << rb;
+    const int tpart = (t >> lo) << (G::LOGE - rb - 1);
+#pragma unroll
+    for (int r0 = 0; r0 < G::E; ++r0) {
+      if (r0 & half) continue;
+      const int r1 = r0 | half;
+      const u64 wv = tw[m + (tpart | (r0 >> (rb + 1)))];
+      if (FWD) {
+        const u64 z1w = mod.mul(x[r1], wv);
+        const u64 a = x[r0];
+        x[r0] = mod.add(a, z1w);
+        x[r1] = mod.sub(a, z1w);
+      } else {
+        const u64 a = x[r0], bb = x[r1];
+        x[r0] = mod.add(a, bb);
+        x[r1] = mod.mul(mod.sub(a, bb), wv);
+      }
+    }
+  }
+}
+
+template <class G, bool FWD, class Mod>
+__global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(u64* __restrict__ data, uint32_t batch, uint64_t stride,
+                                                                const u64* __restrict__ tw, Mod mod) {
+  __shared__ u64 lds[G::PPW * G::PADDED];
+  const int tid = threadIdx.x;
+  const int pw = tid >> G::LOGT;     // polynomial within the workgroup
+  const int t = tid & (G::T - 1);    // lane within the polynomial
+  const uint64_t poly = (uint64_t)blockIdx.x * G::PPW + pw;
+  const bool valid = poly < batch;
+  u64* __restrict__ src = data + poly * stride;
+  u64* sh = lds + pw * G::PADDED;
+
+  u64 x[G::E];
+  {
+    const int lo = win_lo<G, FWD>(0);
+#pragma unroll
+    for (int r = 0; r < G::E; ++r) x[r] = valid ? src[elem<G>(t, r, lo)] : 0;
+  }
+#pragma unroll
+  for (int w = 0; w < G::NWIN; ++w) {
+    if (w > 0) {
+      const int lo_prev = win_lo<G, FWD>(w - 1), lo = win_lo<G, FWD>(w);
+#pragma unroll
+      for (int r = 0; r < G::E; ++r) sh[lds_addr(elem<G>(t, r, lo_prev))] = x[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < G::E; ++r) x[r] = sh[lds_addr(elem<G>(t, r, lo))];
+      __syncthreads();
+    }
+    window_butterflies<G, FWD>(x, t, w, tw, mod);
+  }
+  if (valid) {
+    const int lo = win_lo<G, FWD>(G::NWIN - 1);
+#pragma unroll
+    for (int r = 0; r < G::E; ++r) src[elem<G>(t, r, lo)] = x[r];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launch dispatch
+
+template <int LOGN, int LOGE, bool FWD, class Mod>
+static hipError_t launch_window(u64* data, size_t batch, size_t stride, const u64* tw, const Mod& mod,
+                                hipStream_t stream) {
+  using G = Geo<LOGN, LOGE>;
+  const unsigned grid = (unsigned)((batch + G::PPW - 1) / G::PPW);
+  hipLaunchKernelGGL((ntt_window_kernel<G, FWD, Mod>), dim3(grid), dim3(G::THREADS), 0, stream, data,
+                     (uint32_t)batch, (uint64_t)stride, tw, mod);
+  return hipGetLastError();
+}
+
+template <bool FWD, class Mod>
+static hipError_t dispatch(int logn, int variant, u64* data, size_t batch, size_t stride, const u64* tw,
+                           const Mod& mod, hipStream_t s) {
+  switch (logn) {
+    case 4: return launch_window<4, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 5: return launch_window<5, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 6: return launch_window<6, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 7: return launch_window<7, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 8: return launch_window<8, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 9: return launch_window<9, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 10: return launch_window<10, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 11:
+      if (variant == 1) return launch_window<11, 4, FWD>(data, batch, stride, tw, mod, s);
+      return launch_window<11, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 12: return launch_window<12, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 13: return launch_window<13, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 14: return launch_window<14, 4, FWD>(data, batch, stride, tw, mod, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, u64* data,
+                      size_t batch, size_t stride, const u64* tw, hipStream_t s) {
+  if (goldilocks) {
+    Goldilocks g;
+    return fwd ? dispatch<true>(logn, variant, data, batch, stride, tw, g, s)
+               : dispatch<false>(logn, variant, data, batch, stride, tw, g, s);
+  }
+  Montgomery m{mp.p, mp.pinv, mp.r2};
+  return fwd ? dispatch<true>(logn, variant, data, batch, stride, tw, m, s)
+             : dispatch<false>(logn, variant, data, batch, stride, tw, m, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pointwise ops (prime64.rs:1050-1222), 2 u64 per lane per iteration, grid-stride
+
+enum PwOp { PW_NORMALIZE = 0, PW_MUL_ASSIGN_NORMALIZE = 1, PW_MUL_ACCUMULATE = 2 };
+
+template <int OP, class Mod>
+__device__ __forceinline__ u64 pw_one(u64 o, u64 a, u64 b, u64 c, const Mod& mod) {
+  if (OP == PW_NORMALIZE) return mod.mul(o, c);
+  if (OP == PW_MUL_ASSIGN_NORMALIZE) return mod.mul(mod.mul(o, b), c);
+  u64 prod = mod.mul(a, b);
+  if (c != 0) prod = mod.mul(prod, c);  // Montgomery: c = R^2 mod p restores the plain product
+  return mod.add(o, prod);
+}
+
+// VW = values per lane per iteration (2 -> 16-byte accesses, needs even stride + 16-B alignment)
+template <int OP, int VW, class Mod>
+__global__ __launch_bounds__(256) void pointwise_kernel(u64* __restrict__ out, const u64* __restrict__ a,
+                                                        const u64* __restrict__ b, uint32_t n, uint32_t batch,
+                                                        uint64_t stride, u64 c, Mod mod) {
+  const uint64_t per_poly = n / VW;
+  const uint64_t total = per_poly * batch;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t poly = i / per_poly;
+    const uint64_t off = poly * stride + VW * (i - poly * per_poly);
+    if (VW == 2) {
+      const ulonglong2 ov = *reinterpret_cast<const ulonglong2*>(out + off);
+      ulonglong2 av = make_ulonglong2(0, 0), bv = make_ulonglong2(0, 0);
+      if (OP == PW_MUL_ACCUMULATE) av = *reinterpret_cast<const ulonglong2*>(a + off);
+      if (OP != PW_NORMALIZE) bv = *reinterpret_cast<const ulonglong2*>(b + off);
+      *reinterpret_cast<ulonglong2*>(out + off) =
+          make_ulonglong2(pw_one<OP>(ov.x, av.x, bv.x, c, mod), pw_one<OP>(ov.y, av.y, bv.y, c, mod));
+    } else {
+      const u64 av = (OP == PW_MUL_ACCUMULATE) ? a[off] : 0;
+      const u64 bv = (OP != PW_NORMALIZE) ? b[off] : 0;
+      out[off] = pw_one<OP>(out[off], av, bv, c, mod);
+    }
+  }
+}
+
+template <int OP, class Mod>
+static hipError_t launch_pw(u64* out, const u64* a, const u64* b, size_t n, size_t batch, size_t stride, u64 c,
+                            const Mod& mod, hipStream_t s) {
+  const bool vec = (stride % 2 == 0) && ((uintptr_t)out % 16 == 0) && ((uintptr_t)a % 16 == 0) &&
+                   ((uintptr_t)b % 16 == 0);
+  const uint64_t total = (uint64_t)(vec ? n / 2 : n) * batch;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  if (vec)
+    hipLaunchKernelGGL((pointwise_kernel<OP, 2, Mod>), dim3((unsigned)blocks), dim3(256), 0, s, out, a, b,
+                       (uint32_t)n, (uint32_t)batch, (uint64_t)stride, c, mod);
+  else
+    hipLaunchKernelGGL((pointwise_kernel<OP, 1, Mod>), dim3((unsigned)blocks), dim3(256), 0, s, out, a, b,
+                       (uint32_t)n, (uint32_t)batch, (uint64_t)stride, c, mod);
+  return hipGetLastError();
+}
+
+hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, u64* out, const u64* a, const u64* b,
+                            size_t n, size_t batch, size_t stride, u64 c, hipStream_t s) {
+  if (goldilocks) {
+    Goldilocks g;
+    if (op == PW_NORMALIZE) return launch_pw<PW_NORMALIZE>(out, a, b, n, batch, stride, c, g, s);
+    if (op == PW_MUL_ASSIGN_NORMALIZE) return launch_pw<PW_MUL_ASSIGN_NORMALIZE>(out, a, b, n, batch, stride, c, g, s);
+    return launch_pw<PW_MUL_ACCUMULATE>(out, a, b, n, batch, stride, c, g, s);
+  }
+  Montgomery m{mp.p, mp.pinv, mp.r2};
+  if (op == PW_NORMALIZE) return launch_pw<PW_NORMALIZE>(out, a, b, n, batch, stride, c, m, s);
+  if (op == PW_MUL_ASSIGN_NORMALIZE) return launch_pw<PW_MUL_ASSIGN_NORMALIZE>(out, a, b, n, batch, stride, c, m, s);
+  return launch_pw<PW_MUL_ACCUMULATE>(out, a, b, n, batch, stride, c, m, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// synthetic input, identical stream to oracle/ntt_oracle.c:ora_fill_uniform
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_uniform_kernel(u64* __restrict__ out, uint64_t count, u64 seed, u64 p) {
+  const int shift = p ? __builtin_clzll(p) : 0;  // keep bitlen(p) bits, then reject >= p
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+    u64 v, k = 0;
+    do {
+      v = mix64(seed + (i + 1) * 0x9E3779B97F4A7C15ull + k * 0xD1B54A32D192ED03ull) >> shift;
+      ++k;
+    } while (p != 0 && v >= p);
+    out[i] = v;
+  }
+}
+
+hipError_t launch_fill_uniform(u64* out, size_t count, u64 seed, u64 p, hipStream_t s) {
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, (uint64_t)count, seed, p);
+  return hipGetLastError();
+}
+
+}  // namespace mi

@@ -1,0 +1,25 @@
+// ntt64_launch.hpp — host-side launchers exported by ntt64_kernels.hip to the C ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mi {
+
+// Montgomery parameters for a generic odd prime (R = 2^64).
+struct MontParams {
+  uint64_t p = 0, pinv = 0, r2 = 0;
+};
+
+// Transform kernels.  `variant` selects an alternative register-window width where one is
+// compiled (0 = default).  `tw` points at the plan's device table (forward or inverse).
+hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, uint64_t* data,
+                      size_t batch, size_t stride, const uint64_t* tw, hipStream_t s);
+
+// op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
+hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,
+                            const uint64_t* b, size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
+
+hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint64_t p, hipStream_t s);
+
+}  // namespace mi

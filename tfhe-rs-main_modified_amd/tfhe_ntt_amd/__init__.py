@@ -1,0 +1,12 @@
+"""MI355X-native negacyclic NTT engine for TFHE (host-side mirror of tfhe-ntt / core_crypto Ntt64).
+
+The compute path is ``libtfhe_ntt_amd.so`` (HIP kernels for gfx950 behind the C ABI in
+``include/tfhe_ntt_amd.h``); this package only binds it.  Importing it without the built library
+raises ``ImportError`` — there is no CPU fallback.
+"""
+from ._lib import MiError, lib as _load_lib
+from .prime64 import SOLINAS_P, Plan, fill_uniform
+
+_load_lib()
+
+__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform"]

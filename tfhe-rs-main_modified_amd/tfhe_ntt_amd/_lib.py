@@ -1,0 +1,87 @@
+"""ctypes binding of ``libtfhe_ntt_amd.so`` (the C ABI in ``include/tfhe_ntt_amd.h``).
+
+The library is built in-tree by ``make -C tfhe-rs-main_modified_amd`` (``__graft_entry__.build()``).
+There is deliberately no CPU fallback: if the shared object is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libtfhe_ntt_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include", "tfhe_ntt_amd.h")
+
+MI_OK = 0
+MI_ERR_INVALID_ARG = 1
+MI_ERR_NOT_PRIME = 2
+MI_ERR_NO_ROOT = 3
+MI_ERR_HIP = 4
+MI_ERR_OOM = 5
+MI_ERR_UNSUPPORTED = 6
+
+_u64 = ctypes.c_uint64
+_sz = ctypes.c_size_t
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_p64 = ctypes.POINTER(ctypes.c_uint64)
+
+
+class MiError(RuntimeError):
+    """A non-OK ``mi_status`` returned through the C ABI."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{message} (status {status})")
+        self.status = status
+
+
+_SIGS = {
+    "mi_status_string": (ctypes.c_char_p, [_int]),
+    "mi_last_error_message": (ctypes.c_char_p, []),
+    "mi_ntt64_plan_create": (_int, [_sz, _u64, _int, ctypes.POINTER(_vp)]),
+    "mi_ntt64_plan_destroy": (_int, [_vp]),
+    "mi_ntt64_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
+    "mi_ntt64_plan_twiddles": (_int, [_vp, _p64, _p64, _p64]),
+    "mi_ntt64_fwd_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_inv_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_normalize_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_mul_assign_normalize_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_mul_accumulate_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_fwd_host": (_int, [_vp, _p64, _sz]),
+    "mi_ntt64_inv_host": (_int, [_vp, _p64, _sz]),
+    "mi_fill_uniform": (_int, [_vp, _sz, _u64, _u64, _int, _vp]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C tfhe-rs-main_modified_amd` "
+                "(there is no CPU fallback for the HIP engine)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != MI_OK:
+        L = lib()
+        detail = (L.mi_last_error_message() or b"").decode()
+        text = (L.mi_status_string(status) or b"").decode()
+        raise MiError(status, f"{text}: {detail}" if detail else text)
+
+
+def declared_symbols(header: str = HEADER_PATH) -> list[str]:
+    """Every function the public header declares (used by the ABI export test)."""
+    src = open(header).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mi_[a-z0-9_]+)\s*\(", src)))
