@@ -190,3 +190,155 @@ def fill_uniform(seed: int, p: int, count: int) -> np.ndarray:
     out = np.zeros(count, np.uint64)
     lib().ora_fill_uniform(seed & 0xFFFFFFFFFFFFFFFF, p, _ptr(out), count)
     return out
+
+
+# ---- core_crypto consumers (pbs_oracle.h) ------------------------------------------------
+class _Tables(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("p", ctypes.c_uint64), ("twid", _p64), ("inv_twid", _p64),
+                ("n_inv", ctypes.c_uint64)]
+
+
+_PBS_SIGS = {
+    "ora_decomp_init_native": (_u64, [_u64, ctypes.c_int, ctypes.c_int]),
+    "ora_decompose_one_level": (_u64, [ctypes.c_int, _p64]),
+    "ora_modswitch_p2_to_prime": (_u64, [_u64, ctypes.c_uint, _u64]),
+    "ora_modswitch_prime_to_p2": (_u64, [_u64, ctypes.c_uint, _u64]),
+    "ora_modulus_switch": (_u64, [_u64, ctypes.c_uint]),
+    "ora_pbs_modulus_switch_non_native": (_u64, [_u64, _sz, _u64]),
+    "ora_poly_monomial_mul": (None, [_p64, _sz, _sz, _u64]),
+    "ora_poly_monomial_div": (None, [_p64, _sz, _sz, _u64]),
+    "ora_sample_extract": (None, [_p64, _p64, _sz, ctypes.c_int, _u64]),
+}
+_T = ctypes.POINTER(_Tables)
+for _name in ("ora_ext_product_bnf", "ora_ext_product_solinas"):
+    _PBS_SIGS[_name] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64])
+for _name in ("ora_cmux_bnf", "ora_cmux_solinas"):
+    _PBS_SIGS[_name] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64])
+_PBS_SIGS["ora_blind_rotate_bnf"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _u64, _p64, _sz])
+for _name in ("ora_pbs_bnf", "ora_pbs_solinas"):
+    _PBS_SIGS[_name] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz])
+_PBS_SIGS["ora_bsk_to_ntt"] = (None, [_T, _p64, _p64, _sz, ctypes.c_uint, ctypes.c_int])
+_PBS_SIGS["ora_pbs_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, _sz, ctypes.c_int])
+_PBS_SIGS["ora_ext_product_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz, ctypes.c_int])
+_pbs_ready = False
+
+
+def _plib():
+    global _pbs_ready
+    L = lib()
+    if not _pbs_ready:
+        for name, (res, args) in _PBS_SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _pbs_ready = True
+    return L
+
+
+def _u(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+class NttContext:
+    """Oracle twin of core_crypto's Ntt64 + the NTT PBS algorithms for one (N, p)."""
+
+    def __init__(self, n: int, p: int = SOLINAS_P):
+        self.plan = Plan.try_new(n, p)
+        assert self.plan is not None
+        self.n, self.p = n, p
+        self._t = _Tables(n, p, _ptr(self.plan.twid), _ptr(self.plan.inv_twid), self.plan.n_inv)
+
+    @property
+    def tables(self):
+        return ctypes.byref(self._t)
+
+    def ext_product(self, out, ggsw, glwe, k, base_log, level, bnf=True):
+        out = _u(out).copy()
+        fn = _plib().ora_ext_product_bnf if bnf else _plib().ora_ext_product_solinas
+        fn(self.tables, k, base_log, level, _ptr(out), _ptr(_u(ggsw)), _ptr(_u(glwe)))
+        return out
+
+    def ext_product_batch_bnf(self, out, ggsw, glwe, k, base_log, level, threads=8):
+        out = _u(out).copy()
+        batch = out.size // ((k + 1) * self.n)
+        _plib().ora_ext_product_bnf_batch(self.tables, k, base_log, level, _ptr(out), _ptr(_u(ggsw)),
+                                         _ptr(_u(glwe)), batch, threads)
+        return out
+
+    def cmux(self, ct0, ct1, ggsw, k, base_log, level, bnf=True):
+        ct0, ct1 = _u(ct0).copy(), _u(ct1).copy()
+        fn = _plib().ora_cmux_bnf if bnf else _plib().ora_cmux_solinas
+        fn(self.tables, k, base_log, level, _ptr(ct0), _ptr(ct1), _ptr(_u(ggsw)))
+        return ct0
+
+    def blind_rotate_bnf(self, acc, msed_mask, msed_body, bsk, k, base_log, level):
+        acc = _u(acc).copy()
+        m = _u(msed_mask)
+        _plib().ora_blind_rotate_bnf(self.tables, k, base_log, level, _ptr(acc), _ptr(m), int(msed_body),
+                                     _ptr(_u(bsk)), m.size)
+        return acc
+
+    def pbs(self, lwe_in, lut, bsk, k, base_log, level, bnf=True):
+        lwe_in = _u(lwe_in)
+        out = np.zeros(k * self.n + 1, np.uint64)
+        fn = _plib().ora_pbs_bnf if bnf else _plib().ora_pbs_solinas
+        fn(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)), _ptr(_u(bsk)), lwe_in.size - 1)
+        return out
+
+    def pbs_batch_bnf(self, lwe_in, lut, bsk, k, base_log, level, threads=8):
+        lwe_in = _u(lwe_in)
+        batch, n_lwe = lwe_in.shape[0], lwe_in.shape[1] - 1
+        out = np.zeros((batch, k * self.n + 1), np.uint64)
+        _plib().ora_pbs_bnf_batch(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
+                                  _ptr(_u(bsk)), n_lwe, batch, threads)
+        return out
+
+    def bsk_to_ntt(self, bsk_std, in_width=64, normalize=False):
+        src = _u(bsk_std)
+        dst = np.zeros_like(src)
+        _plib().ora_bsk_to_ntt(self.tables, _ptr(src), _ptr(dst), src.size // self.n, in_width, int(normalize))
+        return dst
+
+
+def decomp_init_native(x, base_log, level):
+    return int(_plib().ora_decomp_init_native(x, base_log, level))
+
+
+def decompose_one_level(base_log, state):
+    s = _u64(state)
+    t = _plib().ora_decompose_one_level(base_log, ctypes.byref(s))
+    return int(t), int(s.value)
+
+
+def modswitch_p2_to_prime(v, width, p=SOLINAS_P):
+    return int(_plib().ora_modswitch_p2_to_prime(v, width, p))
+
+
+def modswitch_prime_to_p2(v, width, p=SOLINAS_P):
+    return int(_plib().ora_modswitch_prime_to_p2(v, width, p))
+
+
+def modulus_switch(x, log_modulus):
+    return int(_plib().ora_modulus_switch(x, log_modulus))
+
+
+def pbs_modulus_switch_non_native(x, n, q):
+    return int(_plib().ora_pbs_modulus_switch_non_native(x, n, q))
+
+
+def poly_monomial_mul(poly, degree, q=0):
+    a = _u(poly).copy()
+    _plib().ora_poly_monomial_mul(_ptr(a), a.size, degree, q)
+    return a
+
+
+def poly_monomial_div(poly, degree, q=0):
+    a = _u(poly).copy()
+    _plib().ora_poly_monomial_div(_ptr(a), a.size, degree, q)
+    return a
+
+
+def sample_extract(glwe, n, k, q=0):
+    out = np.zeros(k * n + 1, np.uint64)
+    _plib().ora_sample_extract(_ptr(_u(glwe)), _ptr(out), n, k, q)
+    return out

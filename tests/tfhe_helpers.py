@@ -1,0 +1,165 @@
+"""Seeded TFHE key generation / encryption / decryption for the PBS tests (numpy, host only).
+
+Restates the *semantics* of the reference's encryption (reference paths relative to
+/root/reference/tfhe/src/core_crypto) so ciphertexts decrypt correctly through both the oracle
+and the GPU PBS; the random streams are our own (numpy PCG64), so only functional results and
+oracle-vs-engine parity on identical inputs are compared, never ciphertext bytes vs the reference.
+
+  * binary LWE / GLWE secret keys        (algorithms/lwe_secret_key_generation.rs, glwe_...)
+  * GLWE encryption  b = sum a_i * s_i + m + e  (negacyclic, mod 2^64)   (glwe_encryption.rs)
+  * GGSW encryption factor -m << (64 - j*B); rows r<k: s_r * factor, last row: -factor at X^0
+                                          (ggsw_encryption.rs:20-45, 318-375)
+  * PBS LUT                               (lwe_programmable_bootstrapping/mod.rs:24-75)
+"""
+import numpy as np
+
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def uniform_u64(g, shape):
+    return g.integers(0, 2**64, size=shape, dtype=np.uint64)
+
+
+def tuniform(g, shape, bound_log2):
+    """Small signed noise in [-2^b, 2^b] as wrapping u64 (TUniform-shaped support)."""
+    v = g.integers(-(1 << bound_log2), (1 << bound_log2) + 1, size=shape, dtype=np.int64)
+    return v.astype(np.uint64)
+
+
+def binary_key(g, size):
+    return g.integers(0, 2, size=size, dtype=np.uint64)
+
+
+def add_q(a, b, q=0):
+    """(a + b) mod q for canonical inputs; q = 0 means wrapping mod 2^64."""
+    with np.errstate(over="ignore"):
+        s = a + b
+        if not q:
+            return s
+        carry = s < a
+        return np.where(carry | (s >= np.uint64(q)), s - np.uint64(q), s)
+
+
+def sub_q(a, b, q=0):
+    with np.errstate(over="ignore"):
+        d = a - b
+        if not q:
+            return d
+        return np.where(a < b, d + np.uint64(q), d)
+
+
+def neg_q(a, q=0):
+    return sub_q(np.zeros_like(a), a, q)
+
+
+def negacyclic_mul_binary(a, s, q=0):
+    """(a * s) mod (X^N + 1), coefficients mod q (q = 0: mod 2^64), s a {0,1} polynomial."""
+    n = a.shape[-1]
+    out = np.zeros_like(a)
+    for j in np.nonzero(s)[0]:
+        j = int(j)
+        if j == 0:
+            out = add_q(out, a, q)
+        else:
+            out[..., j:] = add_q(out[..., j:], a[..., : n - j], q)
+            out[..., :j] = sub_q(out[..., :j], a[..., n - j:], q)
+    return out
+
+
+def uniform_q(g, shape, q=0):
+    return uniform_u64(g, shape) if not q else g.integers(0, q, size=shape, dtype=np.uint64)
+
+
+def noise_q(g, shape, noise_log2, q=0):
+    e = tuniform(g, shape, noise_log2)
+    if not q:
+        return e
+    neg = (e.astype(np.int64) < 0)
+    return np.where(neg, e + np.uint64(q), e)  # -x -> q - x
+
+
+def glwe_encrypt(g, plaintext, glwe_sk, noise_log2, q=0):
+    """plaintext (N,) -> GLWE (k+1, N) under glwe_sk (k, N): b = sum a_i s_i + m + e (mod q)."""
+    k, n = glwe_sk.shape
+    mask = uniform_q(g, (k, n), q)
+    body = plaintext.copy()
+    for i in range(k):
+        body = add_q(body, negacyclic_mul_binary(mask[i], glwe_sk[i], q), q)
+    body = add_q(body, noise_q(g, n, noise_log2, q), q)
+    return np.concatenate([mask, body[None, :]], axis=0)
+
+
+def glwe_decrypt(ct, glwe_sk, q=0):
+    k = glwe_sk.shape[0]
+    body = ct[k].copy()
+    for i in range(k):
+        body = sub_q(body, negacyclic_mul_binary(ct[i], glwe_sk[i], q), q)
+    return body
+
+
+def ggsw_encrypt(g, m, glwe_sk, base_log, level, noise_log2, q=0):
+    """GGSW(m) -> (level, k+1, k+1, N), highest level first (ntt_ggsw_ciphertext.rs:176-192).
+    factor = -m * 2^(64 - B*j) (mod q): ggsw_encryption.rs:20-45 (native and non-native summands)."""
+    k, n = glwe_sk.shape
+    mod = q if q else 2**64
+    out = np.zeros((level, k + 1, k + 1, n), np.uint64)
+    for li in range(level):
+        j = level - li  # DecompositionLevel(level_count - i)
+        factor = (-(int(m)) * (1 << (64 - base_log * j))) % mod
+        for r in range(k + 1):
+            if r < k:  # s_r * factor (slice_wrapping_scalar_mul_assign[_custom_mod])
+                pt = np.array([(int(v) * factor) % mod for v in glwe_sk[r]], dtype=np.uint64)
+            else:
+                pt = np.zeros(n, np.uint64)
+                pt[0] = np.uint64((-factor) % mod)
+            out[li, r] = glwe_encrypt(g, pt, glwe_sk, noise_log2, q)
+    return out
+
+
+def bsk_gen(g, lwe_sk, glwe_sk, base_log, level, noise_log2, q=0):
+    return np.stack([ggsw_encrypt(g, int(b), glwe_sk, base_log, level, noise_log2, q) for b in lwe_sk])
+
+
+def lwe_encrypt(g, pt, lwe_sk, noise_log2, q=0):
+    n = lwe_sk.size
+    mod = q if q else 2**64
+    a = uniform_q(g, n, q)
+    e = int(tuniform(g, 1, noise_log2)[0].astype(np.int64))
+    b = (sum(int(x) for x, s in zip(a, lwe_sk) if s) + int(pt) + e) % mod
+    return np.concatenate([a, np.array([b], np.uint64)])
+
+
+def lwe_decrypt(ct, lwe_sk, q=0):
+    mod = q if q else 2**64
+    return (int(ct[-1]) - sum(int(x) for x, s in zip(ct[:-1], lwe_sk) if s)) % mod
+
+
+def glwe_sk_as_lwe_sk(glwe_sk):
+    return glwe_sk.reshape(-1)
+
+
+def pbs_lut(n, k, msg_mod, delta, f, q=0):
+    """generate_programmable_bootstrap_glwe_lut (lwe_programmable_bootstrapping/mod.rs:24-75)."""
+    box = n // msg_mod
+    acc = np.zeros(n, np.uint64)
+    for i in range(msg_mod):
+        acc[i * box:(i + 1) * box] = np.uint64((f(i) * delta) % (q if q else 2**64))
+    half = box // 2
+    acc[:half] = neg_q(acc[:half], q)
+    acc = np.roll(acc, -half)
+    lut = np.zeros((k + 1, n), np.uint64)
+    lut[k] = acc
+    return lut
+
+
+def decode(pt, delta, msg_mod, q=0):
+    """divide_round(pt, delta) mod 2*msg_mod (padding bit kept); mod-q plaintexts are centred first."""
+    v = int(pt)
+    if q and v > q // 2:
+        v -= q
+    d = (v + delta // 2) // delta
+    return d % (2 * msg_mod)
