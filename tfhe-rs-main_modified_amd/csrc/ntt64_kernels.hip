@@ -168,6 +168,10 @@ static hipError_t dispatch(int logn, int variant, u64* data, size_t batch, size_
 hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, u64* data,
                       size_t batch, size_t stride, const u64* tw, hipStream_t s) {
   if (goldilocks) {
+    if (variant >= 2) {  // persistent software-pipelined path (ntt64_gl.hip)
+      const hipError_t e = launch_ntt_gl(fwd, logn, variant, data, batch, stride, tw, s);
+      if (e != hipErrorInvalidValue) return e;
+    }
     Goldilocks g;
     return fwd ? dispatch<true>(logn, variant, data, batch, stride, tw, g, s)
                : dispatch<false>(logn, variant, data, batch, stride, tw, g, s);
@@ -258,8 +262,9 @@ __device__ __forceinline__ u64 mix64(u64 z) {
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(256) void fill_uniform_kernel(u64* __restrict__ out, uint64_t count, u64 seed, u64 p) {
-  const int shift = p ? __builtin_clzll(p) : 0;  // keep bitlen(p) bits, then reject >= p
+// `shift` = clz(p) computed on the host (0 for p = 0): keep bitlen(p) bits, then reject >= p.
+__global__ __launch_bounds__(256) void fill_uniform_kernel(u64* __restrict__ out, uint64_t count, u64 seed, u64 p,
+                                                           uint32_t shift) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
     u64 v, k = 0;
     do {
@@ -274,7 +279,8 @@ hipError_t launch_fill_uniform(u64* out, size_t count, u64 seed, u64 p, hipStrea
   uint64_t blocks = (count + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, (uint64_t)count, seed, p);
+  const uint32_t shift = p ? (uint32_t)__builtin_clzll(p) : 0u;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, (uint64_t)count, seed, p, shift);
   return hipGetLastError();
 }
 

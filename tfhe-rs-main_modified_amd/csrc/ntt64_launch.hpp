@@ -16,6 +16,10 @@ struct MontParams {
 hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, uint64_t* data,
                       size_t batch, size_t stride, const uint64_t* tw, hipStream_t s);
 
+// Goldilocks persistent kernels (ntt64_gl.hip); hipErrorInvalidValue when the size is not covered.
+hipError_t launch_ntt_gl(bool fwd, int logn, int variant, uint64_t* data, size_t batch, size_t stride,
+                         const uint64_t* tw, hipStream_t s);
+
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
 hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,
                             const uint64_t* b, size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
