@@ -10,7 +10,12 @@ Multi-GPU: polynomials are independent, so each rank owns its o
 shard (weak scaling) and there is no data-path collective; torch.distributed (RCCL) is used only
 for the start/stop barriers and the max-over-ranks time.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+The second half of the metric, "PBS/sec @ shortint default params" (config 4), is measured in the
+same run and reported under "pbs": one step = a batch of 4096 programmable bootstraps per GPU at
+the PARAM_MESSAGE_2_CARRY_2 shape (n=918, k=1, N=2048, base 2^23, l=1, native 2^64 ciphertexts
+through the BNF NTT algorithm, ntt64_bnf_pbs.rs:469-540), one fused kernel launch.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-pbs]
 """
 import argparse
 import json
@@ -27,6 +32,8 @@ SOLINAS_P = 0xFFFFFFFF00000001
 SEED = 0x74666865 + 2  # 0x74666865 + config id
 BYTES_PER_POLY_PASS = 2 * N * 8  # read 16 KiB + write 16 KiB per polynomial per transform
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
+PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
 
 
 def parse():
@@ -37,6 +44,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline leg")
+    ap.add_argument("--no-pbs", action="store_true", help="skip the config-4 PBS leg")
+    ap.add_argument("--pbs-batch", type=int, default=PBS_BATCH)
+    ap.add_argument("--pbs-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -82,6 +92,103 @@ def cpu_baseline(seconds: float):
                    f"{'AVX-512 restatement of generic_solinas.rs fwd/inv_depth_first_avx512' if avx else 'scalar restatement'}, "
                    f"OpenMP {threads} threads, {cpu_model}"),
     }
+
+
+def cpu_baseline_pbs(seconds: float):
+    """Oracle restatement of programmable_bootstrap_ntt64_bnf (transforms through the AVX-512
+    restatement, as the reference's runtime dispatch), one PBS per thread, OpenMP over the batch."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    ctx = O.NttContext(N)
+    n_lwe, k = PBS_N_LWE, 1
+    bsk = O.fill_uniform(SEED + 20, SOLINAS_P, n_lwe * PBS_LEVEL * 4 * N)
+    lut = O.fill_uniform(SEED + 21, 0, 2 * N)
+    sample = threads * 2
+    lwe = O.fill_uniform(SEED + 22, 0, sample * (n_lwe + 1)).reshape(sample, n_lwe + 1)
+    out = np.zeros((sample, k * N + 1), np.uint64)
+    O.pbs_set_fast_ntt(True)
+    try:
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ctx.pbs_batch_bnf(lwe, lut, bsk, k, PBS_BASE_LOG, PBS_LEVEL, threads=threads, out=out)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        O.pbs_set_fast_ntt(False)
+    return {
+        "value": reps * sample / el,
+        "unit": "PBS/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{reps} x {sample} BNF PBS (n=918, N=2048, l=1) in {el:.1f}s, restatement of "
+                   f"ntt64_bnf_pbs.rs with {'AVX-512' if O.have_avx512() else 'scalar'} transforms, "
+                   f"OpenMP {threads} threads"),
+    }
+
+
+def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
+    """Config 4: batched BNF PBS, key and inputs resident in HBM, one fused launch per step."""
+    M = eng.ntt64_pbs
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    n_lwe, batch = PBS_N_LWE, args.pbs_batch
+    # synthetic NTT-domain key (60 MB): per-step work does not depend on its values
+    bsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 10, SOLINAS_P)
+    key = M.NttBootstrapKey(plan, bsk, PBS_BASE_LOG, PBS_LEVEL, M.BNF)
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 11, 0)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 12 + rank * 0x1000, 0)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+    run = lambda: M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe, out, lut, key)
+    run()
+    torch.cuda.synchronize()
+    K = args.pbs_steps
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(K):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = e0.elapsed_time(e1) / K
+    res = {
+        "metric": "PBS/sec @ shortint default params",
+        "value": world * batch * K / elapsed,
+        "unit": "PBS/s",
+        "steps": K,
+        "ms_per_step": elapsed / K * 1e3,
+        "kernel_ms": kernel_ms,
+        "ntt_equivalents_per_s": world * batch * K / elapsed * 4 * n_lwe,
+        "config": {
+            "workload": "programmable_bootstrap_ntt64_bnf, PARAM_MESSAGE_2_CARRY_2 shape n=918 k=1 N=2048 "
+                        "base_log=23 level=1, standard modulus switch (config 4)",
+            "batch_per_gpu": batch,
+            "global_batch": batch * world,
+            "key": "synthetic random NTT-domain BSK (60,162,048 B), resident",
+        },
+        "roofline": {
+            "bound": "valu",
+            "note": "integer VALU-bound (3,672 NTTs + 11.3 M modmul-class ops per PBS); per-step HBM "
+                    "traffic is the L2-resident key plus 23.7 KB of LWE in/out per PBS",
+        },
+        "cpu_baseline": None,
+    }
+    del key
+    return res
 
 
 def load_traffic():
@@ -189,8 +296,12 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if not args.no_pbs:
+        out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if not args.no_pbs:
+            out["pbs"]["cpu_baseline"] = cpu_baseline_pbs(min(args.cpu_seconds, 10.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

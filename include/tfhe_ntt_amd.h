@@ -82,6 +82,62 @@ int mi_ntt64_inv_host(const mi_ntt64_plan *plan, uint64_t *buf, size_t batch);
  * the oracle's ora_fill_uniform, so GPU-generated batches can be checked on the host. */
 int mi_fill_uniform(uint64_t *buf, size_t count, uint64_t seed, uint64_t p, int device, void *stream);
 
+/* ---- External product / CMUX / PBS (core_crypto consumers of the plan) -------------------
+ * Reference paths below are relative to /root/reference/tfhe/src/core_crypto.  These run for the
+ * Solinas plan (p = 2^64 - 2^32 + 1) at N = 2048, GLWE dimension k = 1, 1 <= level <= 3; other
+ * shapes return MI_ERR_UNSUPPORTED.  Layouts are the reference's entity layouts, contiguous:
+ *   GLWE       : (k+1) polynomials of N u64 (mask then body)
+ *   GGSW (NTT) : level-major, highest level first; per level (k+1) rows x (k+1) columns of N u64,
+ *                each polynomial in the plan's forward (bit-reversed) NTT order
+ *   BSK  (NTT) : n_lwe GGSWs back to back ((k+1)^2 * level * N u64 each)
+ *   LWE        : mask (dimension u64) then body
+ * Variant MI_NTT64_SOLINAS works modulo p (algorithms/lwe_programmable_bootstrapping/ntt64_pbs.rs);
+ * MI_NTT64_BNF works on native 2^64 ciphertexts with the back-and-forth modulus switch
+ * (ntt64_bnf_pbs.rs). */
+typedef enum mi_ntt64_variant { MI_NTT64_SOLINAS = 0, MI_NTT64_BNF = 1 } mi_ntt64_variant;
+
+/* Modulus switch of the PBS input (BNF only): standard rounding (fft_impl/common.rs:10-23, as
+ * ntt64_bnf_pbs.rs:512) or the centered-binary variant the shortint parameters use
+ * (algorithms/modulus_switch.rs:35-104). */
+typedef enum mi_ms_mode { MI_MS_STANDARD = 0, MI_MS_CENTERED = 1 } mi_ms_mode;
+
+/* convert_standard_lwe_bootstrap_key_to_ntt64 (algorithms/lwe_bootstrap_key_conversion.rs:294-365)
+ * over `n_polys` polynomials (= n_lwe * (k+1)^2 * level): bsk_ntt = fwd(switch(bsk_std)) [* N^{-1}],
+ * where switch = forward_from_power_of_two_modulus (commons/math/ntt/ntt64.rs:166-178) from a
+ * 2^in_modulus_width modulus when in_modulus_width > 0, identity when 0 (Solinas-modulus keys).
+ * normalize != 0 is NttLweBootstrapKeyOption::Normalize.  Device pointers, may not alias. */
+int mi_bsk_to_ntt64(const mi_ntt64_plan *plan, const uint64_t *bsk_std, uint64_t *bsk_ntt, size_t n_polys,
+                    unsigned in_modulus_width, int normalize, void *stream);
+
+/* out_glwe[b] += GGSW (.) in_glwe[b] for b < batch, one shared NTT-domain GGSW:
+ * add_external_product_ntt64_assign (ntt64_pbs.rs:553-663) or, for MI_NTT64_BNF,
+ * add_external_product_ntt64_bnf_assign (ntt64_bnf_pbs.rs:541-681; GGSW converted Raw). */
+int mi_ext_product_ntt64_batch(const mi_ntt64_plan *plan, uint64_t *out_glwe, const uint64_t *in_glwe,
+                               const uint64_t *ggsw_ntt, int k, int base_log, int level, size_t batch, int variant,
+                               void *stream);
+
+/* CMUX, per item: ct1[b] -= ct0[b]; ct0[b] += GGSW (.) ct1[b] — cmux_ntt64_assign (ntt64_pbs.rs:669-680)
+ * / cmux_ntt64_bnf_assign (ntt64_bnf_pbs.rs:683-705); like the reference, ct1 is left holding ct1 - ct0. */
+int mi_cmux_ntt64_batch(const mi_ntt64_plan *plan, uint64_t *ct0, uint64_t *ct1, const uint64_t *ggsw_ntt, int k,
+                        int base_log, int level, size_t batch, int variant, void *stream);
+
+/* A bootstrap key made ready for mi_pbs_ntt64_batch on the plan's device.  MI_NTT64_BNF keys
+ * (converted Raw, as ntt64_bnf_pbs.rs tests do) are copied once with N^{-1} folded in — the
+ * reference normalises each product at run time (ntt64_bnf_pbs.rs:670); in exact mod-p arithmetic
+ * both orders give identical values.  MI_NTT64_SOLINAS keys are referenced, not copied (the caller
+ * keeps `bsk_ntt` alive).  Replaces the reference's PodStack scratch (ntt64_pbs.rs:705-751). */
+typedef struct mi_pbs_ntt64_key mi_pbs_ntt64_key;
+int mi_pbs_ntt64_key_create(const mi_ntt64_plan *plan, const uint64_t *bsk_ntt, size_t n_lwe, int k, int base_log,
+                            int level, int variant, mi_pbs_ntt64_key **out_key);
+int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key *key);
+
+/* Batched programmable bootstrap: lwe_out[b] = SampleExtract_0(BlindRotate(lut, lwe_in[b])).
+ * programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized (ntt64_bnf_pbs.rs:469-540) or
+ * programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized (ntt64_pbs.rs:482-538).
+ * lwe_in: batch x (n_lwe + 1) u64; lut: one GLWE shared by the batch; lwe_out: batch x (k*N + 1). */
+int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
+                       size_t batch, int ms_mode, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,8 @@ void ora_negacyclic_convolution(size_t n, uint64_t p, const uint64_t *lhs, const
 int ora_have_avx512(void);
 int ora_fwd_batch_avx512(size_t n, const uint64_t *twid, uint64_t *data, size_t batch, size_t stride, int threads);
 int ora_inv_batch_avx512(size_t n, const uint64_t *inv_twid, uint64_t *data, size_t batch, size_t stride, int threads);
+int ora_fwd_avx512(size_t n, const uint64_t *twid, uint64_t *data);
+int ora_inv_avx512(size_t n, const uint64_t *inv_twid, uint64_t *data);
 
 /* deterministic input generator shared with the GPU tests/bench (splitmix64 -> uniform in [0,p) by rejection) */
 void ora_fill_uniform(uint64_t seed, uint64_t p, uint64_t *out, size_t count);

@@ -250,3 +250,16 @@ int ora_inv_batch_avx512(size_t n, const uint64_t *inv_twid, uint64_t *data, siz
     for (b = 0; b < (long long)batch; ++b) inv_depth_first(data + (size_t)b * stride, n, inv_twid, 0, 0);
     return 1;
 }
+
+/* single polynomial, no threading (used inside the batched PBS restatement) */
+int ora_fwd_avx512(size_t n, const uint64_t *twid, uint64_t *data) {
+    if (!ora_have_avx512() || n < 16) return 0;
+    fwd_depth_first(data, n, twid, 0, 0);
+    return 1;
+}
+
+int ora_inv_avx512(size_t n, const uint64_t *inv_twid, uint64_t *data) {
+    if (!ora_have_avx512() || n < 16) return 0;
+    inv_depth_first(data, n, inv_twid, 0, 0);
+    return 1;
+}

@@ -218,7 +218,11 @@ _PBS_SIGS["ora_blind_rotate_bnf"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctyp
 for _name in ("ora_pbs_bnf", "ora_pbs_solinas"):
     _PBS_SIGS[_name] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz])
 _PBS_SIGS["ora_bsk_to_ntt"] = (None, [_T, _p64, _p64, _sz, ctypes.c_uint, ctypes.c_int])
-_PBS_SIGS["ora_pbs_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, _sz, ctypes.c_int])
+_PBS_SIGS["ora_pbs_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, _sz,
+                                         ctypes.c_int, ctypes.c_int])
+_PBS_SIGS["ora_pbs_bnf_ms"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, ctypes.c_int])
+_PBS_SIGS["ora_centered_ms_body_correction"] = (_u64, [_p64, _sz, ctypes.c_uint])
+_PBS_SIGS["ora_pbs_set_fast_ntt"] = (None, [ctypes.c_int])
 _PBS_SIGS["ora_ext_product_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz, ctypes.c_int])
 _pbs_ready = False
 
@@ -278,19 +282,25 @@ class NttContext:
                                      _ptr(_u(bsk)), m.size)
         return acc
 
-    def pbs(self, lwe_in, lut, bsk, k, base_log, level, bnf=True):
+    def pbs(self, lwe_in, lut, bsk, k, base_log, level, bnf=True, centered=False):
         lwe_in = _u(lwe_in)
         out = np.zeros(k * self.n + 1, np.uint64)
-        fn = _plib().ora_pbs_bnf if bnf else _plib().ora_pbs_solinas
-        fn(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)), _ptr(_u(bsk)), lwe_in.size - 1)
+        if bnf:
+            _plib().ora_pbs_bnf_ms(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
+                                   _ptr(_u(bsk)), lwe_in.size - 1, int(centered))
+        else:
+            assert not centered
+            _plib().ora_pbs_solinas(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
+                                    _ptr(_u(bsk)), lwe_in.size - 1)
         return out
 
-    def pbs_batch_bnf(self, lwe_in, lut, bsk, k, base_log, level, threads=8):
+    def pbs_batch_bnf(self, lwe_in, lut, bsk, k, base_log, level, threads=8, centered=False, out=None):
         lwe_in = _u(lwe_in)
         batch, n_lwe = lwe_in.shape[0], lwe_in.shape[1] - 1
-        out = np.zeros((batch, k * self.n + 1), np.uint64)
+        if out is None:
+            out = np.zeros((batch, k * self.n + 1), np.uint64)
         _plib().ora_pbs_bnf_batch(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
-                                  _ptr(_u(bsk)), n_lwe, batch, threads)
+                                  _ptr(_u(bsk)), n_lwe, batch, int(centered), threads)
         return out
 
     def bsk_to_ntt(self, bsk_std, in_width=64, normalize=False):
@@ -298,6 +308,16 @@ class NttContext:
         dst = np.zeros_like(src)
         _plib().ora_bsk_to_ntt(self.tables, _ptr(src), _ptr(dst), src.size // self.n, in_width, int(normalize))
         return dst
+
+
+def pbs_set_fast_ntt(on: bool) -> None:
+    """Route the PBS restatement's transforms through the AVX-512 restatement (CPU baseline only)."""
+    _plib().ora_pbs_set_fast_ntt(int(on))
+
+
+def centered_ms_body_correction(mask, log_modulus):
+    m = _u(mask)
+    return int(_plib().ora_centered_ms_body_correction(_ptr(m), m.size, log_modulus))
 
 
 def decomp_init_native(x, base_log, level):

@@ -76,8 +76,19 @@ uint64_t ora_modswitch_prime_to_p2(uint64_t v, unsigned width, uint64_t p) {
     return ((uint64_t)x) << (64u - width);
 }
 
-static void fwd_poly(const ora_ntt_tables *t, uint64_t *poly) { ora_fwd(t->n, t->p, t->twid, poly); }
-static void inv_poly(const ora_ntt_tables *t, uint64_t *poly) { ora_inv(t->n, t->p, t->inv_twid, poly); }
+/* Plan::fwd / Plan::inv dispatch (prime64.rs:897-1046): the AVX-512 restatement when enabled and
+ * available for the Solinas prime (as the reference's runtime dispatch), else the scalar restatement.
+ * Both are bit-identical (tests/test_oracle.py); the fast one only serves the CPU baseline. */
+static int g_fast_ntt = 0;
+void ora_pbs_set_fast_ntt(int on) { g_fast_ntt = on; }
+static void fwd_poly(const ora_ntt_tables *t, uint64_t *poly) {
+    if (g_fast_ntt && t->p == 0xFFFFFFFF00000001ull && ora_fwd_avx512(t->n, t->twid, poly)) return;
+    ora_fwd(t->n, t->p, t->twid, poly);
+}
+static void inv_poly(const ora_ntt_tables *t, uint64_t *poly) {
+    if (g_fast_ntt && t->p == 0xFFFFFFFF00000001ull && ora_inv_avx512(t->n, t->inv_twid, poly)) return;
+    ora_inv(t->n, t->p, t->inv_twid, poly);
+}
 
 /* ntt64_bnf_pbs.rs:541-681 add_external_product_ntt64_bnf_assign */
 void ora_ext_product_bnf(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
@@ -230,15 +241,37 @@ void ora_sample_extract(const uint64_t *glwe, uint64_t *lwe_out, size_t n, int k
     lwe_out[(size_t)k * n] = glwe[(size_t)k * n];
 }
 
+/* algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add */
+uint64_t ora_centered_ms_body_correction(const uint64_t *mask, size_t n_lwe, unsigned log_modulus) {
+    uint64_t sum_half = 0;
+    int64_t sum_halving_doubled = 0;
+    for (size_t i = 0; i < n_lwe; ++i) {
+        const uint64_t rounded = ora_modulus_switch(mask[i], log_modulus) << (64u - log_modulus);
+        const int64_t err = (int64_t)(rounded - mask[i]);
+        const int64_t half = err / 2; /* truncating signed division, as Rust */
+        sum_halving_doubled += 2 * half - err;
+        sum_half += (uint64_t)half;
+    }
+    const uint64_t sum_halving = (uint64_t)(sum_halving_doubled / 2);
+    const uint64_t half_case = 1ull << (64u - log_modulus - 1u);
+    return sum_half - sum_halving - half_case;
+}
+
 void ora_pbs_bnf(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                  const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe) {
+    ora_pbs_bnf_ms(t, k, base_log, level, lwe_out, lwe_in, lut, bsk, n_lwe, 0);
+}
+
+void ora_pbs_bnf_ms(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
+                    const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe, int centered) {
     const size_t n = t->n, gs = (size_t)k + 1;
     const unsigned log_mod = (unsigned)__builtin_ctzll(n) + 1u; /* to_blind_rotation_input_modulus_log */
     uint64_t *acc = (uint64_t *)malloc(gs * n * sizeof(uint64_t));
     uint64_t *ms = (uint64_t *)malloc((n_lwe + 1) * sizeof(uint64_t));
     memcpy(acc, lut, gs * n * sizeof(uint64_t));
     for (size_t i = 0; i < n_lwe; ++i) ms[i] = ora_modulus_switch(lwe_in[i], log_mod);
-    const uint64_t body = ora_modulus_switch(lwe_in[n_lwe], log_mod);
+    const uint64_t corr = centered ? ora_centered_ms_body_correction(lwe_in, n_lwe, log_mod) : 0;
+    const uint64_t body = ora_modulus_switch(lwe_in[n_lwe] + corr, log_mod); /* modulus_switched_lwe_ciphertext.rs:155-162 */
     ora_blind_rotate_bnf(t, k, base_log, level, acc, ms, body, bsk, n_lwe);
     ora_sample_extract(acc, lwe_out, n, k, 0);
     free(acc); free(ms);
@@ -278,12 +311,13 @@ void ora_bsk_to_ntt(const ora_ntt_tables *t, const uint64_t *bsk_std, uint64_t *
 
 void ora_pbs_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                        const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe,
-                       size_t batch, int threads) {
+                       size_t batch, int centered, int threads) {
     const size_t out_len = (size_t)k * t->n + 1, in_len = n_lwe + 1;
     long long b;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
     for (b = 0; b < (long long)batch; ++b)
-        ora_pbs_bnf(t, k, base_log, level, lwe_out + (size_t)b * out_len, lwe_in + (size_t)b * in_len, lut, bsk, n_lwe);
+        ora_pbs_bnf_ms(t, k, base_log, level, lwe_out + (size_t)b * out_len, lwe_in + (size_t)b * in_len, lut, bsk,
+                       n_lwe, centered);
 }
 
 void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,

@@ -76,6 +76,14 @@ void ora_sample_extract(const uint64_t *glwe, uint64_t *lwe_out, size_t n, int k
 /* ntt64_bnf_pbs.rs:469-540: PBS of native ciphertexts (standard modulus switch, bsk Raw) */
 void ora_pbs_bnf(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                  const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe);
+/* same with the centered-binary modulus switch of the body when centered != 0
+ * (algorithms/modulus_switch.rs:35-104) */
+void ora_pbs_bnf_ms(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
+                    const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe, int centered);
+uint64_t ora_centered_ms_body_correction(const uint64_t *mask, size_t n_lwe, unsigned log_modulus);
+/* route the PBS restatement's transforms through the AVX-512 restatement (CPU baseline) */
+void ora_pbs_set_fast_ntt(int on);
+
 /* ntt64_pbs.rs:213-286 + 482-538: PBS of ciphertexts mod p (bsk pre-normalised) */
 void ora_pbs_solinas(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                      const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe);
@@ -89,7 +97,7 @@ void ora_bsk_to_ntt(const ora_ntt_tables *t, const uint64_t *bsk_std, uint64_t *
 /* batched wrappers (OpenMP over independent items) */
 void ora_pbs_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                        const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe,
-                       size_t batch, int threads);
+                       size_t batch, int centered, int threads);
 void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
                                const uint64_t *ggsw, const uint64_t *glwe, size_t batch, int threads);
 

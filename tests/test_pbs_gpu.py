@@ -1,0 +1,201 @@
+"""GPU parity of the fused external-product / CMUX / PBS kernels against the CPU oracle (`-m gpu`).
+
+Bar: bit-exact on identical inputs.  Random NTT-domain keys exercise every arithmetic path (parity
+does not need the key to be an encryption); seeded real keys check the functional property the
+reference's own tests assert, decrypt(PBS(Enc(m))) == f(m)
+(algorithms/test/lwe_programmable_bootstrapping.rs:708-865 Solinas, :1002-1163 BNF).
+"""
+import numpy as np
+import pytest
+
+import tfhe_helpers as H
+
+pytestmark = pytest.mark.gpu
+
+P = 0xFFFFFFFF00000001
+N = 2048
+K = 1
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def rand_q(g, shape, q):
+    return H.uniform_u64(g, shape) if not q else g.integers(0, q, size=shape, dtype=np.uint64)
+
+
+@pytest.fixture(scope="module")
+def plan(engine):
+    return engine.Plan.try_new(N, P)
+
+
+@pytest.fixture(scope="module")
+def ctx(oracle):
+    return oracle.NttContext(N)
+
+
+@pytest.mark.parametrize("width,normalize", [(64, False), (64, True), (0, True), (0, False), (40, False)])
+def test_bsk_conversion(engine, plan, ctx, width, normalize):
+    g = H.rng(100 + width + normalize)
+    polys = 3 * 4 * 2
+    src = rand_q(g, (polys, N), 0 if width else P)
+    if width and width < 64:  # a 2^w-modulus key lives in the top w bits (ntt64.rs:166-178)
+        src = (src >> np.uint64(64 - width)) << np.uint64(64 - width)
+    want = ctx.bsk_to_ntt(src.reshape(-1), width, normalize).reshape(polys, N)
+    s, d = dev(src), dev(np.zeros_like(src))
+    engine.ntt64_pbs.convert_standard_lwe_bootstrap_key_to_ntt64(plan, s, d, normalize, width or None)
+    assert np.array_equal(host(d), want)
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+@pytest.mark.parametrize("base_log,level", [(23, 1), (12, 2), (7, 3), (1, 1), (21, 3)])
+def test_external_product_parity(engine, plan, ctx, bnf, base_log, level):
+    q = 0 if bnf else P
+    g = H.rng(base_log * 10 + level + 1000 * bnf)
+    batch = 6
+    ggsw = rand_q(g, (level, K + 1, K + 1, N), P)
+    glwe = rand_q(g, (batch, K + 1, N), q)
+    glwe[0, 0, :8] = 0  # edge values the decomposition must carry exactly
+    glwe[0, 1, :4] = np.array([q - 1 if q else 2**64 - 1, 1, (q or 2**64) // 2, (q or 2**64) // 2 + 1], np.uint64)
+    out0 = rand_q(g, (batch, K + 1, N), q)
+    want = np.stack([ctx.ext_product(out0[b].reshape(-1), ggsw.reshape(-1), glwe[b].reshape(-1), K, base_log,
+                                     level, bnf=bnf).reshape(K + 1, N) for b in range(batch)])
+    out, tg, tk = dev(out0), dev(glwe), dev(ggsw)
+    fn = (engine.ntt64_pbs.add_external_product_ntt64_bnf_assign if bnf
+          else engine.ntt64_pbs.add_external_product_ntt64_assign)
+    fn(plan, out, tk, tg, base_log, level)
+    assert np.array_equal(host(out), want)
+    assert np.array_equal(host(tg), glwe)  # input untouched
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+def test_cmux_parity(engine, plan, ctx, bnf):
+    q = 0 if bnf else P
+    g = H.rng(7 + bnf)
+    batch, base_log, level = 5, 23, 1
+    ggsw = rand_q(g, (level, K + 1, K + 1, N), P)
+    ct0, ct1 = rand_q(g, (batch, K + 1, N), q), rand_q(g, (batch, K + 1, N), q)
+    want0 = np.stack([ctx.cmux(ct0[b].reshape(-1), ct1[b].reshape(-1), ggsw.reshape(-1), K, base_log, level,
+                               bnf=bnf).reshape(K + 1, N) for b in range(batch)])
+    want1 = H.sub_q(ct1, ct0, q)
+    t0, t1 = dev(ct0), dev(ct1)
+    fn = engine.ntt64_pbs.cmux_ntt64_bnf_assign if bnf else engine.ntt64_pbs.cmux_ntt64_assign
+    fn(plan, t0, t1, dev(ggsw), base_log, level)
+    assert np.array_equal(host(t0), want0)
+    assert np.array_equal(host(t1), want1)
+
+
+def _pbs_inputs(g, batch, n_lwe, q):
+    lwe = rand_q(g, (batch, n_lwe + 1), q)
+    # mask entries the blind rotation must skip (BNF: modulus-switch to 0; Solinas: raw 0)
+    lwe[:, ::7] = 0
+    if not q:
+        lwe[:, 3::11] = g.integers(0, 1 << 50, size=lwe[:, 3::11].shape, dtype=np.uint64)
+        lwe[:, 5::13] = np.uint64(2**64 - (1 << 50))
+    lwe[0, -1] = 0
+    return lwe
+
+
+@pytest.mark.parametrize("bnf,centered", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("level,base_log", [(1, 23), (2, 15)])
+def test_pbs_parity_random_key(engine, plan, ctx, oracle, bnf, centered, level, base_log):
+    q = 0 if bnf else P
+    g = H.rng(31 + 2 * bnf + centered + 10 * level)
+    n_lwe, batch = 40, 7
+    bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)
+    lut = rand_q(g, (K + 1, N), q)
+    lwe = _pbs_inputs(g, batch, n_lwe, q)
+    want = np.stack([ctx.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, bnf=bnf,
+                             centered=centered) for b in range(batch)])
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(plan, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    if bnf:
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(
+            dev(lwe), out, dev(lut), key, M.MS_CENTERED if centered else M.MS_STANDARD)
+    else:
+        M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    assert np.array_equal(host(out), want)
+
+
+def test_pbs_parity_config4_shape(engine, plan, ctx):
+    """PARAM_MESSAGE_2_CARRY_2 shape (n = 918, beta = 2^23, l = 1, BNF) on a random key, vs the
+    multi-threaded oracle."""
+    g = H.rng(918)
+    n_lwe, batch, base_log, level = 918, 48, 23, 1
+    bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)
+    lut = H.uniform_u64(g, (K + 1, N))
+    lwe = _pbs_inputs(g, batch, n_lwe, 0)
+    want = ctx.pbs_batch_bnf(lwe, lut.reshape(-1), bsk.reshape(-1), K, base_log, level, threads=16)
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(plan, dev(bsk), base_log, level, M.BNF)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    assert np.array_equal(host(out), want)
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+def test_pbs_functional_real_keys(engine, plan, ctx, bnf):
+    """Seeded real keys: GPU PBS == oracle PBS bit for bit, and decrypts to f(m) for every m."""
+    n_lwe, base_log, level = 64, 23, 1
+    q = 0 if bnf else P
+    msg_mod = 4
+    mod = q if q else 2**64
+    delta = (1 << 63) // msg_mod
+    g = H.rng(500 + bnf)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (K, N))
+    bsk = H.bsk_gen(g, lwe_sk, glwe_sk, base_log, level, 17 if bnf else 12, q)
+    nbsk = ctx.bsk_to_ntt(bsk.reshape(-1), 64 if bnf else 0, normalize=not bnf).reshape(n_lwe, level, K + 1, K + 1, N)
+    f = lambda x: (3 * x + 1) % msg_mod
+    lut = H.pbs_lut(N, K, msg_mod, delta, f, q)
+    msgs = list(range(msg_mod)) * 2
+    lwe = np.stack([H.lwe_encrypt(g, (m * delta) % mod, lwe_sk, 30 if bnf else 20, q) for m in msgs])
+    M = engine.ntt64_pbs
+    # the key conversion itself runs on the GPU too
+    gkey = dev(np.zeros_like(bsk))
+    M.convert_standard_lwe_bootstrap_key_to_ntt64(plan, dev(bsk), gkey, normalize=not bnf,
+                                                  input_modulus_width=64 if bnf else None)
+    assert np.array_equal(host(gkey), nbsk)
+    key = M.NttBootstrapKey(plan, gkey, base_log, level, M.BNF if bnf else M.SOLINAS)
+    out = dev(np.zeros((len(msgs), K * N + 1), np.uint64))
+    if bnf:
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    else:
+        M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    out_sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    for i, m in enumerate(msgs):
+        assert np.array_equal(got[i], ctx.pbs(lwe[i], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, bnf=bnf))
+        assert H.decode(H.lwe_decrypt(got[i], out_sk, q), delta, msg_mod, q) == f(m)
+
+
+def test_pbs_errors(engine, plan):
+    import torch
+    M = engine.ntt64_pbs
+    small = engine.Plan.try_new(1024, P)
+    bsk = torch.zeros((4, 1, 2, 2, 1024), dtype=torch.int64, device="cuda")
+    with pytest.raises(engine.MiError) as e:
+        M.NttBootstrapKey(small, bsk, 23, 1, M.BNF)
+    assert e.value.status == 6  # MI_ERR_UNSUPPORTED (N != 2048)
+    with pytest.raises(engine.MiError) as e:
+        M.NttBootstrapKey(plan, torch.zeros((2, 4, 2, 2, N), dtype=torch.int64, device="cuda"), 10, 4, M.BNF)
+    assert e.value.status == 6  # level > 3
+    bsk = torch.zeros((4, 1, 2, 2, N), dtype=torch.int64, device="cuda")
+    with pytest.raises(ValueError):
+        M.NttBootstrapKey(plan, bsk, 23, 2, M.BNF)  # shape / level mismatch
+    key = M.NttBootstrapKey(plan, bsk, 23, 1, M.SOLINAS)
+    lwe = torch.zeros((2, 5), dtype=torch.int64, device="cuda")
+    out = torch.zeros((2, N + 1), dtype=torch.int64, device="cuda")
+    lut = torch.zeros((2, N), dtype=torch.int64, device="cuda")
+    with pytest.raises(ValueError):  # variant mismatch
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe, out, lut, key)
+    M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe[:0], out[:0], lut, key)  # empty batch
+    with pytest.raises(ValueError):
+        M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe[:, :4], out, lut, key)

@@ -277,4 +277,131 @@ int mi_fill_uniform(uint64_t* buf, size_t count, uint64_t seed, uint64_t p, int 
   return e == hipSuccess ? MI_OK : hip_fail(e, "fill launch");
 }
 
+// ---- external product / PBS ------------------------------------------------------------------
+
+struct mi_pbs_ntt64_key {
+  const mi_ntt64_plan* plan = nullptr;
+  size_t n_lwe = 0;
+  int k = 1, base_log = 0, level = 0, variant = 0;
+  const u64* bsk = nullptr;  // what the kernel reads
+  u64* owned = nullptr;      // BNF: private copy with N^{-1} folded in
+};
+
+static int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (variant != MI_NTT64_SOLINAS && variant != MI_NTT64_BNF) return fail(MI_ERR_INVALID_ARG, "unknown variant");
+  if (level < 1 || base_log < 1 || base_log * level > 63)
+    return fail(MI_ERR_INVALID_ARG, "decomposition must satisfy level >= 1, base_log >= 1, base_log*level < 64");
+  if (!plan->goldilocks || plan->n != 2048 || k != 1)
+    return fail(MI_ERR_UNSUPPORTED, "external product / PBS run for the Solinas plan at N = 2048, k = 1");
+  if (level > 3) return fail(MI_ERR_UNSUPPORTED, "decomposition level > 3");
+  return MI_OK;
+}
+
+int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
+                    unsigned in_modulus_width, int normalize, void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (n_polys == 0) return MI_OK;
+  if (!bsk_std || !bsk_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (in_modulus_width > 64) return fail(MI_ERR_INVALID_ARG, "in_modulus_width > 64");
+  if (!plan->goldilocks || plan->n != 2048) return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N = 2048");
+  if (n_polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "too many polynomials");
+  DeviceGuard g(plan->device);
+  hipError_t e = mi::launch_bsk_to_ntt(bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0, plan->n_inv,
+                                       plan->d_twid, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
+}
+
+int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
+                               const uint64_t* ggsw_ntt, int k, int base_log, int level, size_t batch, int variant,
+                               void* stream) {
+  int st = check_pbs_shape(plan, k, base_log, level, variant);
+  if (st != MI_OK) return st;
+  if (batch == 0) return MI_OK;
+  if (!out_glwe || !in_glwe || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
+                                        ggsw_ntt, batch, base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv,
+                                        (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
+}
+
+int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1, const uint64_t* ggsw_ntt, int k,
+                        int base_log, int level, size_t batch, int variant, void* stream) {
+  int st = check_pbs_shape(plan, k, base_log, level, variant);
+  if (st != MI_OK) return st;
+  if (batch == 0) return MI_OK;
+  if (!ct0 || !ct1 || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
+                                        plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
+}
+
+int mi_pbs_ntt64_key_create(const mi_ntt64_plan* plan, const uint64_t* bsk_ntt, size_t n_lwe, int k, int base_log,
+                            int level, int variant, mi_pbs_ntt64_key** out_key) {
+  if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
+  *out_key = nullptr;
+  int st = check_pbs_shape(plan, k, base_log, level, variant);
+  if (st != MI_OK) return st;
+  if (n_lwe == 0 || n_lwe > 0xFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "n_lwe out of range");
+  if (!bsk_ntt) return fail(MI_ERR_INVALID_ARG, "bsk is NULL");
+  mi_pbs_ntt64_key* key = new (std::nothrow) mi_pbs_ntt64_key;
+  if (!key) return fail(MI_ERR_OOM, "host allocation failed");
+  key->plan = plan;
+  key->n_lwe = n_lwe;
+  key->k = k;
+  key->base_log = base_log;
+  key->level = level;
+  key->variant = variant;
+  key->bsk = bsk_ntt;
+  if (variant == MI_NTT64_BNF) {
+    const size_t count = n_lwe * (size_t)(k + 1) * (k + 1) * level * plan->n;
+    DeviceGuard g(plan->device);
+    if (hipMalloc(&key->owned, count * sizeof(u64)) != hipSuccess) {
+      delete key;
+      return fail(MI_ERR_OOM, "bootstrap key copy allocation failed");
+    }
+    hipError_t e = mi::launch_scale(key->owned, bsk_ntt, count, plan->n_inv, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
+      (void)hipFree(key->owned);
+      delete key;
+      return hip_fail(e, "bootstrap key normalisation");
+    }
+    key->bsk = key->owned;
+  }
+  *out_key = key;
+  return MI_OK;
+}
+
+int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key* key) {
+  if (!key) return MI_OK;
+  if (key->owned) {
+    DeviceGuard g(key->plan->device);
+    (void)hipFree(key->owned);
+  }
+  delete key;
+  return MI_OK;
+}
+
+int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
+                       size_t batch, int ms_mode, void* stream) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED) return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
+  if (ms_mode == MI_MS_CENTERED && key->variant != MI_NTT64_BNF)
+    return fail(MI_ERR_INVALID_ARG, "centered modulus switch applies to native-modulus (BNF) inputs");
+  if (batch == 0) return MI_OK;
+  if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  const mi_ntt64_plan* plan = key->plan;
+  DeviceGuard g(plan->device);
+  hipError_t e = mi::launch_pbs(key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe,
+                                batch, key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED,
+                                (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
+}
+
 }  // extern "C"

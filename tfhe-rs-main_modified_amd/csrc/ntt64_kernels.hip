@@ -20,78 +20,9 @@
 
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
+#include "ntt64_regs.hpp"
 
 namespace mi {
-
-template <int LOGN_, int LOGE_>
-struct Geo {
-  static constexpr int LOGN = LOGN_;
-  static constexpr int LOGE = LOGE_;
-  static constexpr int N = 1 << LOGN;
-  static constexpr int E = 1 << LOGE;
-  static constexpr int LOGT = LOGN - LOGE;  // lanes per polynomial = 2^LOGT
-  static constexpr int T = 1 << LOGT;
-  static constexpr int PPW = T >= 64 ? 1 : 64 / T;  // polynomials per workgroup
-  static constexpr int THREADS = T * PPW;
-  static constexpr int NFULL = LOGN / LOGE;
-  static constexpr int REM = LOGN % LOGE;
-  static constexpr int NWIN = NFULL + (REM ? 1 : 0);
-  // LDS image: 4 u64 of padding per 32 (keeps the strided window reads off shared banks)
-  static constexpr int PADDED = N + (N >> 3);
-  static_assert(LOGN >= LOGE, "window wider than the transform");
-  static_assert(THREADS <= 1024, "workgroup too large");
-};
-
-__device__ __forceinline__ int lds_addr(int e) { return e + ((e >> 5) << 2); }
-
-template <class G>
-__device__ __forceinline__ int elem(int t, int r, int lo) {
-  return ((t >> lo) << (lo + G::LOGE)) | (r << lo) | (t & ((1 << lo) - 1));
-}
-
-// window geometry: low bit of the register window and how many of its bits are new stages
-template <class G, bool FWD>
-__device__ __forceinline__ constexpr int win_lo(int w) {
-  if (FWD) return (w < G::NFULL) ? G::LOGN - G::LOGE * (w + 1) : 0;
-  return (w < G::NFULL) ? G::LOGE * w : G::LOGN - G::LOGE;
-}
-
-template <class G, bool FWD, class Mod>
-__device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w, const u64* __restrict__ tw,
-                                                   const Mod& mod) {
-  const int lo = win_lo<G, FWD>(w);
-  // r-bits of this window that still need a stage
-  int rb_first, rb_last;
-  if (w < G::NFULL) { rb_first = 0; rb_last = G::LOGE - 1; }
-  else if (FWD) { rb_first = 0; rb_last = G::REM - 1; }
-  else { rb_first = G::LOGE - G::REM; rb_last = G::LOGE - 1; }
-
-#pragma unroll
-  for (int s = 0; s < G::LOGE; ++s) {
-    const int rb = FWD ? (G::LOGE - 1 - s) : s;
-    if (rb < rb_first || rb > rb_last) continue;
-    const int b = lo + rb;                       // butterfly bit of the element index
-    const int m = 1 << (G::LOGN - 1 - b);        // reference's `m` for this stage
-    const int half = 1 << rb;
-    const int tpart = (t >> lo) << (G::LOGE - rb - 1);
-#pragma unroll
-    for (int r0 = 0; r0 < G::E; ++r0) {
-      if (r0 & half) continue;
-      const int r1 = r0 | half;
-      const u64 wv = tw[m + (tpart | (r0 >> (rb + 1)))];
-      if (FWD) {
-        const u64 z1w = mod.mul(x[r1], wv);
-        const u64 a = x[r0];
-        x[r0] = mod.add(a, z1w);
-        x[r1] = mod.sub(a, z1w);
-      } else {
-        const u64 a = x[r0], bb = x[r1];
-        x[r0] = mod.add(a, bb);
-        x[r1] = mod.mul(mod.sub(a, bb), wv);
-      }
-    }
-  }
-}
 
 template <class G, bool FWD, class Mod>
 __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(u64* __restrict__ data, uint32_t batch, uint64_t stride,

@@ -27,3 +27,19 @@ hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint6
 hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint64_t p, hipStream_t s);
 
 }  // namespace mi
+
+namespace mi {
+
+// pbs_kernels.hip — Goldilocks, N = 2048, k = 1 only (callers validate the shape).
+hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
+                             uint64_t n_inv, const uint64_t* tw, hipStream_t s);
+hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s);
+// cmux: glwe -= out first (written back), then out += GGSW (.) glwe
+hipError_t launch_ext_product(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
+                              size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
+                              hipStream_t s);
+hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+                      const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
+                      const uint64_t* itw, int centered, hipStream_t s);
+
+}  // namespace mi

@@ -1,0 +1,457 @@
+// pbs_kernels.hip — NTT-domain GGSW x GLWE external product, CMUX / blind rotation and programmable
+// bootstrap for MI355X, in both NTT flavours of tfhe core_crypto (reference paths relative to
+// /root/reference/tfhe/src/core_crypto):
+//   BNF     : native 2^64 ciphertexts, back-and-forth modulus switch to the Goldilocks prime
+//             (algorithms/lwe_programmable_bootstrapping/ntt64_bnf_pbs.rs:208-726)
+//   SOLINAS : ciphertexts modulo the prime (algorithms/lwe_programmable_bootstrapping/ntt64_pbs.rs:213-702)
+//
+// MI355X design: one workgroup (256 lanes) owns one ciphertext for the WHOLE blind rotation.  The
+// GLWE accumulator (k+1 = 2 polynomials of N = 2048) lives in VGPRs across all n CMUX steps, so the
+// only per-step global traffic is the step's NTT GGSW (64 KiB, shared by every workgroup of the
+// launch, hence L2/MALL-resident: all workgroups walk the key in the same order).  Each step
+// rotates through LDS, decomposes in registers, runs 2 forward + 2 inverse NTTs with the register
+// window engine of ntt64_regs.hpp, multiply-accumulates against the GGSW in the NTT domain and
+// switches the result back — the reference's ~10 host-side passes per CMUX fused into one loop body.
+//
+// Bit-exactness: every step restates the reference arithmetic exactly; the only reordering is the
+// BNF N^{-1} normalisation, which is folded into a private copy of the key (exact: Goldilocks
+// arithmetic is canonical, (sum a*g) * N^-1 == sum a*(g*N^-1) mod p).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mi_arith.hpp"
+#include "ntt64_launch.hpp"
+#include "ntt64_regs.hpp"
+
+namespace mi {
+namespace pbs {
+
+using G = Geo<11, 3>;  // N = 2048, 8 coefficients per lane, 256 lanes
+static constexpr int N = G::N;
+static constexpr int T = G::T;
+static constexpr int E = G::E;
+static constexpr u64 P = GL_P;
+static constexpr int LO_COL = G::LOGN - G::LOGE;          // column layout e = r * T + t
+static constexpr int LO_NTT = win_lo<G, true>(G::NWIN - 1);  // forward exit / inverse entry layout
+
+// ---- scalar helpers (each restates one reference function) ----------------------------------
+
+// commons/math/decomposition/decomposer.rs:156-185 (native u64)
+__device__ __forceinline__ u64 decomp_init_native(u64 input, int base_log, int level) {
+  const unsigned rep = base_log * level, non_rep = 64u - rep;
+  u64 res = input >> (non_rep - 1);
+  const u64 rounding_bit = res & 1u;
+  res += 1;
+  res >>= 1;
+  res &= (~0ull) >> (64u - rep);
+  const u64 need_balance = (((res - 1) | (rounding_bit << (rep - 1))) & res) >> (rep - 1);
+  return res - (need_balance << rep);
+}
+
+// commons/math/decomposition/iter.rs:131-151
+__device__ __forceinline__ u64 decompose_one_level(int base_log, u64& state) {
+  const u64 mask = (1ull << base_log) - 1;
+  const u64 res = state & mask;
+  state = (u64)((int64_t)state >> base_log);
+  const u64 carry = (((res - 1) | state) & res) >> (base_log - 1);
+  state += carry;
+  return res - (carry << base_log);
+}
+
+// decomposer.rs:25-49 native_closest_representable, then decomposer.rs:521-548 (q = p, 64 bits)
+__device__ __forceinline__ u64 closest_abs_nonnative(u64 abs_value, int base_log, int level) {
+  const unsigned shift = 64u - (unsigned)(level * base_log) - 1u;
+  u64 res = abs_value >> shift;
+  res += 1;
+  res &= ~1ull;
+  return res << shift;
+}
+
+// commons/math/ntt/ntt64.rs:184-197: ((v << 64) | (p >> 1)) / p for v < p, restated without a
+// 128-bit division: 2^64 = p + EPS, so q = v + floor((v*EPS + h) / p) with h = p >> 1.
+__device__ __forceinline__ u64 modswitch_prime_to_native(u64 v) {
+  const unsigned __int128 R = (unsigned __int128)v * GL_EPS + (P >> 1);
+  const u64 rh = (u64)(R >> 64), rl = (u64)R;
+  unsigned __int128 R2 = (unsigned __int128)rh * GL_EPS + rl;  // R = rh*p + R2, R2 < 2^65
+  u64 q = rh;
+  if (R2 >= P) { R2 -= P; ++q; }
+  if (R2 >= P) { ++q; }
+  return v + q;
+}
+
+// fft_impl/common.rs:10-23
+__device__ __forceinline__ u64 modulus_switch(u64 input, unsigned log_modulus) {
+  return (input + (1ull << (64u - log_modulus - 1u))) >> (64u - log_modulus);
+}
+
+// ntt64_pbs.rs:540-549 + algorithms/misc.rs:6-18 divide_round
+__device__ __forceinline__ u64 ms_non_native(u64 input) {
+  const unsigned __int128 num = ((unsigned __int128)input) << (G::LOGN + 1);
+  // num / p with the 2^64 = p + EPS split (num < 2^76)
+  const u64 nh = (u64)(num >> 64), nl = (u64)num;
+  unsigned __int128 r = (unsigned __int128)nh * GL_EPS + nl;  // num = nh*p + r
+  u64 q = nh;
+  while (r >= P) { r -= P; ++q; }
+  return q + (r >= (P >> 1) ? 1 : 0);
+}
+
+__device__ __forceinline__ u64 neg_custom(u64 a) { return a == 0 ? 0 : P - a; }
+__device__ __forceinline__ u64 sub_custom(u64 a, u64 b) { return a >= b ? a - b : a - b + P; }
+__device__ __forceinline__ u64 add_custom(u64 a, u64 b) { return sub_custom(a, neg_custom(b)); }
+
+template <bool BNF>
+__device__ __forceinline__ u64 neg_q(u64 a) { return BNF ? (u64)0 - a : neg_custom(a); }
+
+// ---- one external product on registers ------------------------------------------------------
+// in: ct1[2][E] (column layout, the GLWE to decompose); out: y[2][E] (column layout, the GLWE
+// contribution out += GGSW (.) ct1 in the ciphertext domain).  `ggsw` = LEVELS x 2 x 2 x N (NTT
+// domain, highest level first); BNF keys are expected pre-normalised unless `normalize`.
+template <bool BNF, int LEVELS>
+__device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[2][E], u64 (&y)[2][E], const u64* __restrict__ ggsw,
+                                                 int base_log, int t, u64* sh, const u64* __restrict__ tw,
+                                                 const u64* __restrict__ itw, bool normalize, u64 n_inv) {
+  const Goldilocks gl;
+  u64 state[2][E];
+  unsigned char sign[2][E];
+  (void)sign;
+  if (BNF) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) state[c][r] = decomp_init_native(ct1[c][r], base_log, LEVELS);
+  } else {
+    // iter.rs:623-670 TensorSignedDecompositionLendingIterNonNative::new (q = p: ceil_log2 = 64)
+    const unsigned shift = 64u - (unsigned)(base_log * LEVELS);
+    const u64 half = P / 2 + 1;  // div_ceil(2)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const u64 x = ct1[c][r];
+        const bool s = x >= half;
+        state[c][r] = closest_abs_nonnative(s ? P - x : x, base_log, LEVELS) >> shift;
+        sign[c][r] = s;
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) y[c][r] = 0;
+
+#pragma unroll
+  for (int li = 0; li < LEVELS; ++li) {
+    u64 x[2][E];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        u64 term = decompose_one_level(base_log, state[c][r]);
+        if (!BNF && sign[c][r]) term = (u64)0 - term;  // iter.rs:722-731
+        x[c][r] = ((int64_t)term < 0) ? term + P : term;  // ntt64.rs:231-238 / iter.rs:724-730
+      }
+    ntt_regs<G, true, 2>(x, t, sh, tw, gl);
+    const u64* mat = ggsw + (size_t)li * 4 * N;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int pos = elem<G>(t, r, LO_NTT);
+      const u64 g00 = mat[0 * N + pos], g01 = mat[1 * N + pos], g10 = mat[2 * N + pos], g11 = mat[3 * N + pos];
+      // update_with_fmadd (ntt64_pbs.rs:683-702 / ntt64_bnf_pbs.rs:707-726): row r' times column c
+      y[0][r] = gl.add(y[0][r], gl.add(gl.mul(x[0][r], g00), gl.mul(x[1][r], g10)));
+      y[1][r] = gl.add(y[1][r], gl.add(gl.mul(x[0][r], g01), gl.mul(x[1][r], g11)));
+    }
+  }
+  if (BNF && normalize) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) y[c][r] = gl.mul(y[c][r], n_inv);
+  }
+  ntt_regs<G, false, 2>(y, t, sh, itw, gl);
+  if (BNF) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) y[c][r] = modswitch_prime_to_native(y[c][r]);
+  }
+}
+
+// ---- external product / CMUX batch (config 3) ----------------------------------------------------
+// EXT : out[b] += GGSW (.) glwe[b]                          (add_external_product_ntt64[_bnf]_assign)
+// CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
+template <bool BNF, int LEVELS, bool CMUX>
+__global__ __launch_bounds__(256) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                          const u64* __restrict__ ggsw, uint32_t batch, int base_log,
+                                                          const u64* __restrict__ tw, const u64* __restrict__ itw,
+                                                          u64 n_inv) {
+  __shared__ u64 sh[2 * G::PADDED];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;  // uniform per workgroup
+  u64* in = glwe + (size_t)b * 2 * N;
+  u64* o = out + (size_t)b * 2 * N;
+  u64 ct[2][E], y[2][E], acc[2][E];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int e = c * N + elem<G>(t, r, LO_COL);
+      ct[c][r] = in[e];
+      acc[c][r] = o[e];
+      if (CMUX) {  // ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705: ct1 -= ct0
+        ct[c][r] = BNF ? ct[c][r] - acc[c][r] : sub_custom(ct[c][r], acc[c][r]);
+        in[e] = ct[c][r];
+      }
+    }
+  ext_product_regs<BNF, LEVELS>(ct, y, ggsw, base_log, t, sh, tw, itw, true, n_inv);
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int e = c * N + elem<G>(t, r, LO_COL);
+      o[e] = BNF ? acc[c][r] + y[c][r] : add_custom(acc[c][r], y[c][r]);  // ntt64.rs:110-137 / 244-266
+    }
+}
+
+// algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the
+// workgroup (uses sh[0 .. 2T) and leaves it free again).
+__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int t,
+                                        u64* sh) {
+  u64 sum_half = 0;
+  int64_t sum_hed = 0;
+  for (uint32_t i = t; i < n_lwe; i += T) {
+    const u64 a = lwe[i];
+    const int64_t err = (int64_t)((modulus_switch(a, log_mod) << (64u - log_mod)) - a);
+    const int64_t half = err / 2;  // truncating, as Rust's signed division
+    sum_half += (u64)half;
+    sum_hed += 2 * half - err;
+  }
+  sh[t] = sum_half;
+  sh[T + t] = (u64)sum_hed;
+  __syncthreads();
+  for (int s = T / 2; s > 0; s >>= 1) {
+    if (t < s) {
+      sh[t] += sh[t + s];
+      sh[T + t] = (u64)((int64_t)sh[T + t] + (int64_t)sh[T + t + s]);
+    }
+    __syncthreads();
+  }
+  const u64 total_half = sh[0];
+  const int64_t total_hed = (int64_t)sh[T];
+  __syncthreads();
+  const u64 sum_halving = (u64)(total_hed / 2);
+  const u64 half_case = 1ull << (64u - log_mod - 1u);
+  return total_half - sum_halving - half_case;
+}
+
+// ---- programmable bootstrap batch (configs 4/5) -----------------------------------------------
+// lwe_in: batch x (n+1); lut: 2 x N shared; bsk: n x LEVELS x 2 x 2 x N (BNF: pre-normalised copy);
+// lwe_out: batch x (N+1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
+template <bool BNF, int LEVELS>
+__global__ __launch_bounds__(256) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+                                                  const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                  uint32_t n_lwe, uint32_t batch, int base_log,
+                                                  const u64* __restrict__ tw, const u64* __restrict__ itw,
+                                                  int centered) {
+  __shared__ u64 sh[2 * G::PADDED];
+  const int t = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;
+  const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
+  const size_t ggsw_len = (size_t)LEVELS * 4 * N;
+  const unsigned log_mod = G::LOGN + 1;  // PolynomialSize::to_blind_rotation_input_modulus_log
+
+  u64 body_corr = 0;
+  if (BNF && centered) body_corr = centered_body_correction(lwe, n_lwe, log_mod, t, sh);
+
+  u64 acc[2][E];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) acc[c][r] = lut[c * N + elem<G>(t, r, LO_COL)];
+
+  if (!BNF) {  // ntt64_pbs.rs:237-249: rotate the LUT by -ms(b) first (custom modulus)
+    const u64 body = ms_non_native(lwe[n_lwe]);
+    const int full = (int)(body / N) & 1, rem = (int)(body % N);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const int m = elem<G>(t, r, LO_COL);  // div_assign: new[m] = old[(m + rem) % N], neg for m >= N - rem
+        u64 v = sh[c * N + ((m + rem) & (N - 1))];
+        if (full ^ (m >= N - rem)) v = neg_custom(v);
+        acc[c][r] = v;
+      }
+    __syncthreads();
+  }
+
+  for (uint32_t i = 0; i < n_lwe; ++i) {
+    const u64 a_raw = lwe[i];
+    u64 a;
+    if (BNF) {
+      a = modulus_switch(a_raw, log_mod);
+      if (a == 0) continue;  // ntt64_bnf_pbs.rs:241
+    } else {
+      if (a_raw == 0) continue;  // ntt64_pbs.rs:257
+      a = ms_non_native(a_raw);
+    }
+    const int full = (int)(a / N) & 1, rem = (int)(a % N);
+    // ct1 = acc * X^a (polynomial_wrapping_monic_monomial_mul_assign[_custom_mod]) ; ct1 -= acc
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+    __syncthreads();
+    u64 ct1[2][E], y[2][E];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const int e = elem<G>(t, r, LO_COL);  // mul_assign: new[e] = old[(e - rem) % N], neg for e < rem
+        u64 v = sh[c * N + ((e - rem) & (N - 1))];
+        if (full ^ (e < rem)) v = neg_q<BNF>(v);
+        ct1[c][r] = BNF ? v - acc[c][r] : sub_custom(v, acc[c][r]);  // cmux: ct1 - ct0
+      }
+    __syncthreads();
+    ext_product_regs<BNF, LEVELS>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, t, sh, tw, itw, false, 0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) acc[c][r] = BNF ? acc[c][r] + y[c][r] : add_custom(acc[c][r], y[c][r]);
+  }
+
+  // BNF: final rotation by -ms(b) (ntt64_bnf_pbs.rs:262-270); then sample extract (nth = 0)
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+  __syncthreads();
+  int full = 0, rem = 0;
+  if (BNF) {
+    const u64 body = modulus_switch(lwe[n_lwe] + body_corr, log_mod);
+    full = (int)(body / N) & 1;
+    rem = (int)(body % N);
+  }
+  // rotated[c][m] = sign * acc[c][(m + rem) % N]
+  u64* out = lwe_out + (size_t)b * (N + 1);
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int j = elem<G>(t, r, LO_COL);
+    // glwe_sample_extraction.rs:89-160: out[0] = A[0], out[j] = -A[N - j]
+    const int m = (j == 0) ? 0 : N - j;
+    u64 v = sh[(m + rem) & (N - 1)];
+    if (full ^ (m >= N - rem)) v = neg_q<BNF>(v);
+    out[j] = (j == 0) ? v : neg_q<BNF>(v);
+  }
+  if (t == 0) {
+    u64 v = sh[N + (rem & (N - 1))];
+    if (full ^ (0 >= N - rem)) v = neg_q<BNF>(v);
+    out[N] = v;
+  }
+}
+
+// ---- key conversion (lwe_bootstrap_key_conversion.rs:294-365) + normalisation ---------------------
+// bsk_ntt[pi] = fwd(modswitch_{2^w -> p}(bsk_std[pi])) [* N^-1]; also used to prepare the BNF copy.
+__global__ __launch_bounds__(256) void bsk_to_ntt_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
+                                                         uint64_t n_polys, unsigned in_width, int normalize,
+                                                         u64 n_inv, const u64* __restrict__ tw) {
+  __shared__ u64 sh[G::PADDED];
+  const Goldilocks gl;
+  const int t = threadIdx.x;
+  const uint64_t pi = blockIdx.x;
+  if (pi >= n_polys) return;
+  u64 x[1][E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    u64 v = src[pi * N + elem<G>(t, r, LO_COL)];
+    if (in_width) {  // ntt64.rs:166-178
+      const unsigned __int128 w = ((unsigned __int128)(v >> (64u - in_width))) * P + ((unsigned __int128)1 << (in_width - 1));
+      v = (u64)(w >> in_width);
+    }
+    x[0][r] = v;
+  }
+  ntt_regs<G, true, 1>(x, t, sh, tw, gl);
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    u64 v = x[0][r];
+    if (normalize) v = gl.mul(v, n_inv);
+    dst[pi * N + elem<G>(t, r, LO_NTT)] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(u64* __restrict__ dst, const u64* __restrict__ src, uint64_t count,
+                                                    u64 c) {
+  const Goldilocks gl;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = gl.mul(src[i], c);
+}
+
+}  // namespace pbs
+
+hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
+                             uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
+  if (n_polys == 0) return hipSuccess;
+  hipLaunchKernelGGL(pbs::bsk_to_ntt_kernel, dim3((unsigned)n_polys), dim3(256), 0, s, dst, src, (uint64_t)n_polys,
+                     in_width, normalize, n_inv, tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pbs::scale_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, (uint64_t)count, c);
+  return hipGetLastError();
+}
+
+template <bool BNF, bool CMUX>
+static hipError_t ext_dispatch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
+                               int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
+  const dim3 grid((unsigned)batch), block(256);
+  switch (level) {
+    case 1: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 1, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
+    case 2: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 2, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
+    case 3: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 3, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ext_product(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
+                              size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
+                              hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  if (cmux)
+    return bnf ? ext_dispatch<true, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
+               : ext_dispatch<false, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+  return bnf ? ext_dispatch<true, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
+             : ext_dispatch<false, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+}
+
+template <bool BNF>
+static hipError_t pbs_dispatch(int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+                               const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
+                               const uint64_t* itw, int centered, hipStream_t s) {
+  const dim3 grid((unsigned)batch), block(256);
+  switch (level) {
+    case 1: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 1>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
+    case 2: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 2>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
+    case 3: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 3>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+                      const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
+                      const uint64_t* itw, int centered, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  return bnf ? pbs_dispatch<true>(level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s)
+             : pbs_dispatch<false>(level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s);
+}
+
+}  // namespace mi

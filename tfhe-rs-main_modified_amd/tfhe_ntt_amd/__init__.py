@@ -9,4 +9,6 @@ from .prime64 import SOLINAS_P, Plan, fill_uniform
 
 _load_lib()
 
-__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform"]
+from . import ntt64_pbs  # noqa: E402  (core_crypto consumers: external product, CMUX, PBS)
+
+__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform", "ntt64_pbs"]

@@ -1,0 +1,173 @@
+"""Host-side mirror of the core_crypto NTT64 consumers (external product, CMUX, PBS) over the C ABI.
+
+Function names follow the reference (paths relative to /root/reference/tfhe/src/core_crypto):
+
+* ``convert_standard_lwe_bootstrap_key_to_ntt64``    algorithms/lwe_bootstrap_key_conversion.rs:294-365
+* ``add_external_product_ntt64_assign``              algorithms/lwe_programmable_bootstrapping/ntt64_pbs.rs:553-663
+* ``add_external_product_ntt64_bnf_assign``          .../ntt64_bnf_pbs.rs:541-681
+* ``cmux_ntt64_assign`` / ``cmux_ntt64_bnf_assign``   ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705
+* ``programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized``
+                                                     ntt64_pbs.rs:482-538 / ntt64_bnf_pbs.rs:469-540
+
+Every operand is a HIP device tensor (uint64 / int64).  The reference works on one ciphertext per
+call; here a leading batch dimension is allowed everywhere (the reference's rayon loop over
+ciphertexts, ``pbs_bench.rs:865-886``, becomes one launch).  Shape mismatches raise ``ValueError``
+(the reference panics on ``assert_eq!``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import MiError, check, lib
+
+SOLINAS = 0
+BNF = 1
+MS_STANDARD = 0
+MS_CENTERED = 1
+
+
+def _dev(t, name):
+    import torch
+
+    if not (type(t).__module__.startswith("torch") and t.is_cuda):
+        raise TypeError(f"{name} must be a HIP device tensor")
+    if t.dtype not in (torch.uint64, torch.int64):
+        raise TypeError(f"{name} must hold 64-bit integers, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _glwe_batch(t, k, n, name):
+    if t.dim() < 2 or tuple(t.shape[-2:]) != (k + 1, n):
+        raise ValueError(f"assertion failed: {name} shape {tuple(t.shape)} != (..., {k + 1}, {n})")
+    return t.numel() // ((k + 1) * n)
+
+
+def _ggsw_shape(plan, ggsw, level, k):
+    n = plan.ntt_size()
+    want = (level, k + 1, k + 1, n)
+    if tuple(ggsw.shape[-4:]) != want or ggsw.numel() != level * (k + 1) ** 2 * n:
+        raise ValueError(f"assertion failed: ggsw shape {tuple(ggsw.shape)} != {want}")
+
+
+def convert_standard_lwe_bootstrap_key_to_ntt64(plan, input_bsk, output_bsk, normalize: bool = False,
+                                                input_modulus_width: int | None = 64) -> None:
+    """output_bsk = fwd(switch(input_bsk)) [* N^-1] polynomial by polynomial.
+
+    ``input_modulus_width``: 64 for native-modulus keys (``Ntt64::modswitch_requirement``,
+    ntt64.rs:142-159), the power-of-two width for other 2^w moduli, ``None`` for keys already mod p.
+    ``normalize``: ``NttLweBootstrapKeyOption::Normalize`` (Solinas PBS) vs ``Raw`` (BNF PBS)."""
+    n = plan.ntt_size()
+    if input_bsk.shape != output_bsk.shape or input_bsk.numel() % n:
+        raise ValueError("assertion failed: input/output bootstrap key shapes differ")
+    check(lib().mi_bsk_to_ntt64(plan.handle, _dev(input_bsk, "input_bsk"), _dev(output_bsk, "output_bsk"),
+                                input_bsk.numel() // n, int(input_modulus_width or 0), int(bool(normalize)),
+                                _stream(output_bsk)))
+
+
+def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux):
+    n = plan.ntt_size()
+    k = 1
+    b = _glwe_batch(out, k, n, "out")
+    if glwe.shape != out.shape:
+        raise ValueError(f"assertion failed: glwe shape {tuple(glwe.shape)} != out shape {tuple(out.shape)}")
+    _ggsw_shape(plan, ggsw, level, k)
+    fn = lib().mi_cmux_ntt64_batch if cmux else lib().mi_ext_product_ntt64_batch
+    check(fn(plan.handle, _dev(out, "out"), _dev(glwe, "glwe"), _dev(ggsw, "ggsw"), k, base_log, level, b, variant,
+             _stream(out)))
+
+
+def add_external_product_ntt64_assign(plan, out, ggsw, glwe, base_log: int, level: int) -> None:
+    """out += ggsw (.) glwe modulo the Solinas prime; ``ggsw`` NTT-domain (converted Normalize)."""
+    _ext(plan, out, ggsw, glwe, base_log, level, SOLINAS, False)
+
+
+def add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, base_log: int, level: int) -> None:
+    """out += ggsw (.) glwe on native 2^64 ciphertexts; ``ggsw`` NTT-domain (converted Raw)."""
+    _ext(plan, out, ggsw, glwe, base_log, level, BNF, False)
+
+
+def cmux_ntt64_assign(plan, ct0, ct1, ggsw, base_log: int, level: int) -> None:
+    """ct0 = cmux(ggsw, ct0, ct1) mod p; like the reference, ct1 is left holding ct1 - ct0."""
+    _ext(plan, ct0, ggsw, ct1, base_log, level, SOLINAS, True)
+
+
+def cmux_ntt64_bnf_assign(plan, ct0, ct1, ggsw, base_log: int, level: int) -> None:
+    _ext(plan, ct0, ggsw, ct1, base_log, level, BNF, True)
+
+
+class NttBootstrapKey:
+    """An NTT-domain bootstrap key bound to a plan (``mi_pbs_ntt64_key``).
+
+    ``bsk`` is the device tensor (n_lwe, level, k+1, k+1, N) produced by
+    ``convert_standard_lwe_bootstrap_key_to_ntt64``: Raw for ``BNF`` (a private copy with N^-1
+    folded in is made once), Normalize for ``SOLINAS`` (referenced; keep the tensor alive)."""
+
+    def __init__(self, plan, bsk, base_log: int, level: int, variant: int = BNF):
+        n = plan.ntt_size()
+        k = 1
+        if bsk.dim() != 5 or tuple(bsk.shape[1:]) != (level, k + 1, k + 1, n):
+            raise ValueError(f"assertion failed: bsk shape {tuple(bsk.shape)} != (n_lwe, {level}, 2, 2, {n})")
+        self.plan, self.bsk, self.base_log, self.level, self.variant = plan, bsk, base_log, level, variant
+        self.input_lwe_dimension = bsk.shape[0]
+        self.glwe_dimension, self.polynomial_size = k, n
+        h = ctypes.c_void_p()
+        check(lib().mi_pbs_ntt64_key_create(plan.handle, _dev(bsk, "bsk"), self.input_lwe_dimension, k, base_log,
+                                            level, variant, ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().mi_pbs_ntt64_key_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def output_lwe_size(self) -> int:
+        return self.glwe_dimension * self.polynomial_size + 1
+
+
+def _pbs(key, lwe_in, lwe_out, accumulator, ms_mode):
+    n_in = key.input_lwe_dimension + 1
+    if lwe_in.shape[-1] != n_in:
+        raise ValueError(f"assertion failed: input lwe size {lwe_in.shape[-1]} != {n_in}")
+    batch = lwe_in.numel() // n_in
+    if lwe_out.shape[-1] != key.output_lwe_size() or lwe_out.numel() // key.output_lwe_size() != batch:
+        raise ValueError(f"assertion failed: output lwe shape {tuple(lwe_out.shape)}")
+    if tuple(accumulator.shape) != (key.glwe_dimension + 1, key.polynomial_size):
+        raise ValueError(f"assertion failed: accumulator shape {tuple(accumulator.shape)}")
+    check(lib().mi_pbs_ntt64_batch(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                   _dev(accumulator, "accumulator"), batch, ms_mode, _stream(lwe_out)))
+
+
+def programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key,
+                                                                  ms_mode: int = MS_STANDARD) -> None:
+    """Batched BNF PBS of native-modulus LWEs (ntt64_bnf_pbs.rs:469-540)."""
+    if key.variant != BNF:
+        raise ValueError("key was not prepared for the BNF variant")
+    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode)
+
+
+def programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key) -> None:
+    """Batched PBS of LWEs modulo the Solinas prime (ntt64_pbs.rs:482-538)."""
+    if key.variant != SOLINAS:
+        raise ValueError("key was not prepared for the Solinas variant")
+    _pbs(key, lwe_in, lwe_out, accumulator, MS_STANDARD)
+
+
+__all__ = [
+    "SOLINAS", "BNF", "MS_STANDARD", "MS_CENTERED", "MiError", "NttBootstrapKey",
+    "convert_standard_lwe_bootstrap_key_to_ntt64", "add_external_product_ntt64_assign",
+    "add_external_product_ntt64_bnf_assign", "cmux_ntt64_assign", "cmux_ntt64_bnf_assign",
+    "programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized",
+    "programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized",
+]
