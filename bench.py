@@ -161,9 +161,7 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = eng.multi_gpu.max_over_ranks(elapsed, dev)
     kernel_ms = e0.elapsed_time(e1) / K
     res = {
         "metric": "PBS/sec @ shortint default params",
@@ -250,9 +248,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = eng.multi_gpu.max_over_ranks(elapsed, dev)
 
     fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / K
     inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / K

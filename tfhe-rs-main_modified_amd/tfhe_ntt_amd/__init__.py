@@ -9,6 +9,6 @@ from .prime64 import SOLINAS_P, Plan, fill_uniform
 
 _load_lib()
 
-from . import ntt64_pbs  # noqa: E402  (core_crypto consumers: external product, CMUX, PBS)
+from . import multi_gpu, ntt64_pbs  # noqa: E402  (core_crypto consumers; batch sharding)
 
-__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform", "ntt64_pbs"]
+__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform", "ntt64_pbs", "multi_gpu"]
