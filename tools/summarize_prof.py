@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_session.sh output directory into the committed profile artefacts.
+
+  python tools/summarize_prof.py gpurun_out/prof_<tag> profiles/<tag>
+
+Writes <dst>/kernel_stats.csv (rocprofv3 --kernel-trace --stats summary, copied), <dst>/pmc_summary.json
+(per-kernel mean PMC values for the NTT transform kernels of the bench run, HBM bytes corrected as
+MI355X_MICROARCH.md prescribes: FETCH_SIZE is in KiB and reports half the bytes of a coalesced
+streaming read on gfx950 -> x1024 x2; WRITE_SIZE in KiB -> x1024) and refreshes
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ALG_BYTES = 8192 * 2048 * 8 * 2  # one N=2048 batch-8192 pass: read + write in place
+
+
+def counters(path):
+    vals = defaultdict(lambda: defaultdict(list))
+    grid = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            vals[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            grid[row["Kernel_Name"]] = int(row["Grid_Size"])
+    return vals, grid
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    merged = defaultdict(dict)
+    grids = {}
+    for sub in ("pmc_sq", "pmc_lds", "pmc_fetch", "pmc_write"):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        vals, grid = counters(p)
+        grids.update(grid)
+        for k, cs in vals.items():
+            for c, v in cs.items():
+                merged[k][c] = sum(v) / len(v)
+    summary = {}
+    for k, cs in merged.items():
+        if "ntt_window_kernel" not in k and "ntt_gl" not in k and "pbs_kernel" not in k:
+            continue
+        if "ntt" in k and grids.get(k, 0) < 8192 * 64:  # only the full-batch launches
+            continue
+        d = dict(cs)
+        if "FETCH_SIZE" in d:
+            d["hbm_read_bytes_corrected"] = d["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in d:
+            d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
+            if "ntt" in k:
+                d["algorithmic_bytes_per_launch"] = ALG_BYTES
+        if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
+            d["valu_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        summary[k] = d
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    ntt = {k: v for k, v in summary.items() if "ntt" in k and "hbm_bytes_per_launch" in v}
+    if ntt:
+        worst = max(ntt.items(), key=lambda kv: kv[1]["hbm_bytes_per_launch"])
+        traffic = {"source": os.path.join(dst, "pmc_summary.json"), "kernel": worst[0],
+                   "bytes_per_launch": worst[1]["hbm_bytes_per_launch"],
+                   "per_kernel": {k: v["hbm_bytes_per_launch"] for k, v in ntt.items()}}
+        root = os.path.dirname(os.path.abspath(dst.rstrip("/")))
+        with open(os.path.join(root, "pmc_traffic.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
+    for k, v in summary.items():
+        print(k[:90], {c: round(x, 1) for c, x in v.items() if c in ("valu_per_wave", "hbm_bytes_per_launch", "SQ_LDS_BANK_CONFLICT")})
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define ITERS 2048
 
@@ -18,7 +19,7 @@
     uint32_t b = s1 ^ threadIdx.x, c = s0 + 77;                                              \
     uint64_t m0, m1;                                                                         \
     asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 %1, 0" : "=s"(m0), "=s"(m1));              \
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");                                       \
+    asm volatile("v_cmp_gt_u32_e32 vcc, 17, %0\n\ts_nop 7\n\ts_nop 7" :: "v"(b) : "memory", "vcc");     \
     uint64_t t0 = __builtin_amdgcn_s_memtime();                                              \
     uint64_t r0 = __builtin_amdgcn_s_memrealtime();                                          \
     for (int i = 0; i < ITERS; ++i) { BODY8(INS) }                                           \
@@ -47,6 +48,25 @@
 #define I_CMP64(x, k) { uint64_t m; asm volatile("v_cmp_lt_u64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(a0)); }
 #define I_MOV64(x, k) asm volatile("v_mov_b64 %0, %0" : "+v"(x));
 #define I_MULHI(x, k) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x) : "v"(b));
+// VOP2 forms with VCC (e32)
+#define I_ADDCO32(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1" : "+v"(x) : "v"(b) : "vcc");
+#define I_CND32(x, k) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
+#define I_SUBB32(x, k) asm volatile("v_subb_co_u32_e32 %0, vcc, %0, %1, vcc" : "+v"(x) : "v"(b) : "vcc");
+#define I_CND32B(x, k) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
+#define I_CND64VCC(x, k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
+#define I_SUBU32(x, k) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define I_LSHR32(x, k) asm volatile("v_lshrrev_b32_e32 %0, 7, %0" : "+v"(x));
+#define I_LSHR64(x, k) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(x));
+#define I_NOT32(x, k) asm volatile("v_not_b32_e32 %0, %0" : "+v"(x));
+#define I_MUL24(x, k) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define I_MULHI24(x, k) asm volatile("v_mul_hi_u32_u24_e32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define I_MULLO(x, k) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(b));
+#define I_BFI(x, k) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c));
+#define I_PERM(x, k) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c));
+#define I_NOP0(x, k) asm volatile("s_nop 0");
+#define I_NOP1(x, k) asm volatile("s_nop 1");
+#define I_ADDPAIR(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n s_nop 1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
+#define I_ADDPAIR_NONOP(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
 
 KERNEL(k_add, uint32_t, I_ADD)
 KERNEL(k_xor, uint32_t, I_XOR)
@@ -64,10 +84,29 @@ KERNEL(k_lshladd64, uint64_t, I_LSHLADD64)
 KERNEL(k_cmp64, uint64_t, I_CMP64)
 KERNEL(k_mov64, uint64_t, I_MOV64)
 KERNEL(k_mulhi, uint32_t, I_MULHI)
+KERNEL(k_addco32, uint32_t, I_ADDCO32)
+KERNEL(k_cnd32, uint32_t, I_CND32)
+KERNEL(k_subb32, uint32_t, I_SUBB32)
+KERNEL(k_nop0, uint32_t, I_NOP0)
+KERNEL(k_cnd32b, uint32_t, I_CND32B)
+KERNEL(k_cnd64vcc, uint32_t, I_CND64VCC)
+KERNEL(k_subu32, uint32_t, I_SUBU32)
+KERNEL(k_lshr32, uint32_t, I_LSHR32)
+KERNEL(k_lshr64, uint64_t, I_LSHR64)
+KERNEL(k_not32, uint32_t, I_NOT32)
+KERNEL(k_mul24, uint32_t, I_MUL24)
+KERNEL(k_mulhi24, uint32_t, I_MULHI24)
+KERNEL(k_mullo, uint32_t, I_MULLO)
+KERNEL(k_bfi, uint32_t, I_BFI)
+KERNEL(k_perm, uint32_t, I_PERM)
+KERNEL(k_nop1, uint32_t, I_NOP1)
+KERNEL(k_addpair, uint32_t, I_ADDPAIR)
+KERNEL(k_addpair_nonop, uint32_t, I_ADDPAIR_NONOP)
 
 typedef void (*kfn)(uint64_t*, uint32_t, uint32_t, uint64_t*);
 
-int main() {
+int main(int argc, char** argv) {
+  setvbuf(stdout, NULL, _IONBF, 0);
   struct { const char* name; kfn f; } ks[] = {
       {"v_add_u32", k_add},          {"v_xor_b32", k_xor},           {"v_mov_b32", k_mov},
       {"v_add3_u32", k_add3},        {"v_alignbit_b32", k_align},    {"v_add_co_u32(e64)", k_addco3},
@@ -75,11 +114,16 @@ int main() {
       {"v_cndmask(0,-1,s)", k_cndk}, {"v_mad_u64_u32", k_mad},       {"v_mad_u64_u32(+0)", k_mad0},
       {"v_lshl_add_u64", k_lshladd64}, {"v_cmp_lt_u64", k_cmp64},    {"v_mov_b64", k_mov64},
       {"v_mul_hi_u32", k_mulhi},
+      {"v_add_co_u32_e32(vcc)", k_addco32}, {"v_cndmask_e32(vcc)", k_cnd32}, {"v_subb_co_e32 chain", k_subb32},
+      {"s_nop 0", k_nop0}, {"v_cndmask_e32(vcc valu-set)", k_cnd32b}, {"v_cndmask_e64(vcc)", k_cnd64vcc},
+      {"v_sub_u32_e32", k_subu32}, {"v_lshrrev_b32_e32", k_lshr32}, {"v_lshrrev_b64", k_lshr64}, {"v_not_b32", k_not32},
+      {"v_mul_u32_u24_e32", k_mul24}, {"v_mul_hi_u32_u24_e32", k_mulhi24}, {"v_mul_lo_u32", k_mullo}, {"v_bfi_b32", k_bfi},
+      {"v_perm_b32", k_perm}, {"s_nop 1", k_nop1}, {"addco+nop1+addc (3 ins)", k_addpair}, {"addco+addc no nop", k_addpair_nonop},
   };
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
   const int cus = prop.multiProcessorCount;
-  const int blocks = cus * 8;
+  const int blocks = cus * (argc > 1 ? atoi(argv[1]) : 8);
   uint64_t *out, *clk;
   (void)hipMalloc(&out, (size_t)blocks * 256 * 8);
   (void)hipMalloc(&clk, (size_t)blocks * 16);
