@@ -15,6 +15,7 @@
 #include "../../include/tfhe_ntt_amd.h"
 #include "host_math.hpp"
 #include "ntt64_launch.hpp"
+#include "ntt64_tw_tables.hpp"
 
 using mi::host::u128;
 using mi::host::u64;
@@ -32,6 +33,9 @@ struct mi_ntt64_plan {
   u64 c_normalize = 0, c_man = 0, c_macc = 0;  // device constants of the pointwise ops
   u64* d_twid = nullptr;
   u64* d_inv_twid = nullptr;
+  // twisted N = 2048 Solinas transform (ntt64_tw.hip): rho_i^j and rho_i^-j, 64 i + j
+  u64* d_twist_f = nullptr;
+  u64* d_twist_i = nullptr;
 };
 
 namespace {
@@ -104,7 +108,7 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   plan->p = p;
   plan->device = device;
   plan->goldilocks = (p == mi::host::SOLINAS_P);
-  plan->variant = env_variant();
+  plan->variant = env_variant();  // default 0; the Solinas N = 2048 plan maps 0 to the twisted kernel (4) below
 
   // prime64.rs:162-182: Solinas uses the hard-coded friendly root tower, other primes the
   // Tonelli-Shanks root.
@@ -164,6 +168,46 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
     delete plan;
     return hip_fail(e, "twiddle upload");
   }
+  if (plan->goldilocks && n == 2048) {
+    // The twisted factorisation needs the reference's first five stages to use power-of-two
+    // twiddles (the Solinas root tower, psi^64 = 8); check it against the tables it was built from.
+    bool tower_ok = true;
+    for (int st = 0; st < 5 && tower_ok; ++st)
+      for (int g = 0; g < (1 << st); ++g)
+        if (plan->twid[(1u << st) + g] != mi::host::exp_mod(2, (u64)mi::tw::G1_FWD[st][g], p)) tower_ok = false;
+    if (tower_ok) {
+      const u64 psi = plan->twid[mi::host::bit_rev(logn, 1)];
+      std::vector<u64> tf(n + 32), ti(n + 32);
+      for (int g = 0; g < 32; ++g) {  // twiddles of the lane-pair stage (ntt64_tw.hip)
+        tf[n + g] = mi::host::exp_mod(2, (u64)mi::tw::CYC_FWD[5][g], p);
+        ti[n + g] = mi::host::exp_mod(2, (u64)mi::tw::CYC_INV[5][g], p);
+      }
+      for (unsigned i = 0; i < 32; ++i) {
+        const u64 rho = mi::host::exp_mod(psi, 2 * (u64)mi::host::bit_rev(5, i) + 1, p);
+        const u64 rho_inv = mi::host::exp_mod(rho, p - 2, p);
+        u64 f = 1, b = 1;
+        for (unsigned j = 0; j < 64; ++j) {
+          tf[64 * i + j] = f;
+          ti[64 * i + j] = b;
+          f = mi::host::mul_mod(f, rho, p);
+          b = mi::host::mul_mod(b, rho_inv, p);
+        }
+      }
+      if (hipMalloc(&plan->d_twist_f, (n + 32) * sizeof(u64)) == hipSuccess &&
+          hipMalloc(&plan->d_twist_i, (n + 32) * sizeof(u64)) == hipSuccess &&
+          hipMemcpy(plan->d_twist_f, tf.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess &&
+          hipMemcpy(plan->d_twist_i, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess) {
+      } else {
+        if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);
+        if (plan->d_twist_i) (void)hipFree(plan->d_twist_i);
+        plan->d_twist_f = plan->d_twist_i = nullptr;
+        (void)hipFree(plan->d_twid);
+        (void)hipFree(plan->d_inv_twid);
+        delete plan;
+        return fail(MI_ERR_OOM, "twist table allocation failed");
+      }
+    }
+  }
   *out_plan = plan;
   return MI_OK;
 }
@@ -174,6 +218,8 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
     DeviceGuard g(plan->device);
     if (plan->d_twid) (void)hipFree(plan->d_twid);
     if (plan->d_inv_twid) (void)hipFree(plan->d_inv_twid);
+    if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);
+    if (plan->d_twist_i) (void)hipFree(plan->d_twist_i);
   }
   delete plan;
   return MI_OK;
@@ -204,12 +250,21 @@ static int check_batch(const mi_ntt64_plan* plan, const void* buf, size_t batch,
   return MI_OK;
 }
 
+// Variant routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan when its tables
+// exist (MI_NTT_VARIANT=4), else the register-window kernels.
+static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride,
+                                   hipStream_t s) {
+  if (plan->variant >= 4 && plan->variant <= 6 && plan->d_twist_f)
+    return mi::launch_ntt_tw(fwd, plan->variant, buf, batch, stride, fwd ? plan->d_twist_f : plan->d_twist_i, s);
+  return mi::launch_ntt(fwd, plan->logn, plan->variant >= 4 ? 0 : plan->variant, plan->goldilocks, plan->mp, buf,
+                        batch, stride, fwd ? plan->d_twid : plan->d_inv_twid, s);
+}
+
 static int run_ntt(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride, void* stream) {
   int st = check_batch(plan, buf, batch, stride);
   if (st != MI_OK || batch == 0) return st;
   DeviceGuard g(plan->device);
-  hipError_t e = mi::launch_ntt(fwd, plan->logn, plan->variant, plan->goldilocks, plan->mp, buf, batch, stride,
-                                fwd ? plan->d_twid : plan->d_inv_twid, (hipStream_t)stream);
+  hipError_t e = launch_transform(fwd, plan, buf, batch, stride, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, fwd ? "fwd launch" : "inv launch");
 }
 
@@ -256,9 +311,7 @@ static int run_host(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t b
   u64* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return fail(MI_ERR_OOM, "device buffer allocation failed");
   hipError_t e = hipMemcpy(d, buf, bytes, hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = mi::launch_ntt(fwd, plan->logn, plan->variant, plan->goldilocks, plan->mp, d, batch, plan->n,
-                       fwd ? plan->d_twid : plan->d_inv_twid, nullptr);
+  if (e == hipSuccess) e = launch_transform(fwd, plan, d, batch, plan->n, nullptr);
   if (e == hipSuccess) e = hipMemcpy(buf, d, bytes, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   (void)hipFree(d);

@@ -20,6 +20,11 @@ hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const Mo
 hipError_t launch_ntt_gl(bool fwd, int logn, int variant, uint64_t* data, size_t batch, size_t stride,
                          const uint64_t* tw, hipStream_t s);
 
+// Twisted shift-twiddle transform (ntt64_tw.hip): Solinas prime, N = 2048 only.  `twist` = the
+// plan's rho_i^j table (forward) or rho_i^-j table (inverse), 2048 u64 each.
+hipError_t launch_ntt_tw(bool fwd, int variant, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
+                         hipStream_t s);
+
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
 hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,
                             const uint64_t* b, size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);

@@ -1,0 +1,699 @@
+#!/usr/bin/env python3
+"""Generate tfhe-rs-main_modified_amd/csrc/ntt64_tw_body.hpp: the whole data path of the twisted
+N = 2048 Goldilocks transform (ntt64_tw.hip) as ONE hand-scheduled gfx950 asm body per direction.
+
+The compiler keeps no data registers: the body owns v8..v127 (64 of them hold the 32 coefficients
+of the lane, the rest are scratch) and s20..s99; C++ only passes addresses.  See ntt64_tw.hip for
+the factorisation and the layouts; tools/gen_tw_tables.py for the exponent tables.
+
+Data path (forward):
+  LOAD  W0 rows (512-B coalesced)          -> G1 stages (CT, shift twiddles, compile-time per register)
+  TWIST x *= rho_i^j (table, general multiply)
+  T1    W0 -> W1 through LDS (two 8 KiB halves split by j, row stride 34)
+  CYC   stages q = 0..4 (CT, shift twiddles)
+  LAST  regroup lane pairs (DPP) -> stage q = 5 with a per-lane twiddle -> canonical
+  T2    W1' -> W0 through LDS (halves split by i, row stride 66, column swizzle j ^ (j >> 5))
+  STORE W0 rows
+Inverse: LOAD, T1, regroup + first GS stage + regroup back, CYC_INV, T4 (W1 -> W0), UNTWIST, G1_INV,
+canonical, STORE.
+
+Usage: python tools/gen_tw_kernel.py > tfhe-rs-main_modified_amd/csrc/ntt64_tw_body.hpp
+"""
+import os
+import sys
+
+# ------------------------------------------------------------------------------------------------
+# register budget
+VLO, VHI = 8, 128            # v8..v127 owned by the body (v0..v7: compiler / address inputs)
+# SGPRs: s20:21 odd-lane mask, s22:23 saved exec, s24:25 junk carry, s36..s77 carry pairs (3 per slot,
+# up to 7 slots), s78..s93 row-group bases.  s32..s35 are left alone (stack/frame registers).
+SG0 = 36
+JUNK = "s[24:25]"
+SGPR_CLOBBER = list(range(20, 32)) + list(range(36, 94))
+
+
+def pv(b):
+    return f"v[{b}:{b + 1}]"
+
+
+class Op:
+    __slots__ = ("text", "reads", "writes", "kind", "cost", "preds", "succs", "prio", "idx")
+
+    def __init__(self, text, reads, writes, kind="valu"):
+        self.text, self.kind = text, kind
+        self.reads, self.writes = set(), set()
+        for r in reads:
+            self.reads.update(expand(r))
+        for w in writes:
+            self.writes.update(expand(w))
+        m = text.split()[0]
+        if kind == "salu":
+            self.cost = 0.0
+        elif m in ("v_mov_b32", "v_lshrrev_b32", "v_lshlrev_b32") or kind == "dpp":
+            self.cost = 2.3
+        else:
+            self.cost = 4.5
+        self.preds, self.succs = set(), set()
+        self.prio = 0.0
+
+
+def expand(r):
+    if r.startswith("v[") or r.startswith("s["):
+        a, b = r[2:-1].split(":")
+        return [f"{r[0]}{i}" for i in range(int(a), int(b) + 1)]
+    return [r]
+
+
+class Seg:
+    """A list of ops in sequential program order, list-scheduled with gfx950 hazard padding:
+    VALU write of an SGPR -> VALU read: 2 wait states; -> SALU read: 1; VALU write of a VGPR ->
+    DPP read of it: 2 wait states."""
+
+    def __init__(self):
+        self.ops = []
+
+    def add(self, text, reads=(), writes=(), kind="valu"):
+        self.ops.append(Op(text, reads, writes, kind))
+
+    def schedule(self):
+        ops = self.ops
+        last_w, readers = {}, {}
+        for op in ops:
+            for r in op.reads:
+                if r in last_w:
+                    op.preds.add(last_w[r])
+            for w in op.writes:
+                if w in ("s24", "s25"):
+                    continue
+                if w in last_w:
+                    op.preds.add(last_w[w])
+                for rd in readers.get(w, []):
+                    if rd is not op:
+                        op.preds.add(rd)
+            for r in op.reads:
+                readers.setdefault(r, []).append(op)
+            for w in op.writes:
+                if w in ("s24", "s25"):
+                    continue
+                last_w[w] = op
+                readers[w] = []
+        for op in ops:
+            for p in op.preds:
+                p.succs.add(op)
+        for op in reversed(ops):
+            op.prio = op.cost + max((s.prio for s in op.succs), default=0.0)
+        # producers of each read register (for hazards)
+        prod = {}
+        lw = {}
+        for op in ops:
+            for r in op.reads:
+                if r in lw:
+                    prod[(op, r)] = lw[r]
+            for w in op.writes:
+                lw[w] = op
+        done, out, issued = set(), [], {}
+        remaining = list(ops)
+        slot = 0
+        while remaining:
+            best = None
+            for op in remaining:
+                if not all(p in done for p in op.preds):
+                    continue
+                ok = True
+                for r in op.reads:
+                    p = prod.get((op, r))
+                    if p is None or p.kind == "salu":
+                        continue
+                    if r[0] == "s" or r == "vcc":
+                        need = 2 if op.kind == "salu" else 3
+                    elif op.kind == "dpp":
+                        need = 3
+                    else:
+                        continue
+                    if slot - issued[p] < need:
+                        ok = False
+                        break
+                if not ok:
+                    continue
+                key = (op.prio, -op.idx)
+                if best is None or key > bkey:
+                    best, bkey = op, key
+            if best is None:
+                out.append("s_nop 0")
+                slot += 1
+                continue
+            out.append(best.text)
+            issued[best] = slot
+            slot += 1
+            done.add(best)
+            remaining.remove(best)
+        return merge_nops(out)
+
+    def emit_in_order(self):
+        return [op.text for op in self.ops]
+
+
+def merge_nops(lines):
+    res, run = [], 0
+    for l in lines + ["<end>"]:
+        if l == "s_nop 0":
+            run += 1
+            continue
+        while run:
+            n = min(run, 8)
+            res.append(f"s_nop {n - 1}")
+            run -= n
+        if l != "<end>":
+            res.append(l)
+    return res
+
+
+# ------------------------------------------------------------------------------------------------
+class Slot:
+    """8 scratch VGPRs (4 pairs) + 3 SGPR carry pairs."""
+
+    def __init__(self, vbase, sbase):
+        self.v = [f"v{vbase + i}" for i in range(8)]
+        self.P = [pv(vbase + 2 * i) for i in range(4)]
+        self.c = [f"s[{sbase + 2 * i}:{sbase + 2 * i + 1}]" for i in range(3)]
+
+
+class MulSlot:
+    """12 scratch VGPRs for a general multiply + 2 SGPR carry pairs."""
+
+    def __init__(self, vbase, sbase):
+        self.v = [f"v{vbase + i}" for i in range(12)]
+        self.P = [pv(vbase + 2 * i) for i in range(6)]
+        self.c = [f"s[{sbase + 2 * i}:{sbase + 2 * i + 1}]" for i in range(2)]
+
+
+def X(dmap, r):
+    b = dmap[r]
+    return f"v{b}", f"v{b + 1}", pv(b)
+
+
+def tmul(sg, S, xlo, xhi, xp, sl, tlo, thi):
+    """canonical t (tlo:thi) with x * 2^S = (neg ? -t : t)."""
+    e = S % 96
+    neg = (S >= 96) != (e >= 64)
+    v, P, c = sl.v, sl.P, sl.c
+    if e == 0:
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {xp}", [xp], [P[0], c[1]])
+        sg.add(f"v_cndmask_b32_e64 {tlo}, {xlo}, {v[0]}, {c[1]}", [xlo, v[0], c[1]], [tlo])
+        sg.add(f"v_cndmask_b32_e64 {thi}, {xhi}, {v[1]}, {c[1]}", [xhi, v[1], c[1]], [thi])
+        return neg
+    if e < 64:
+        r = e if e <= 32 else e - 32
+        sg.add(f"v_lshlrev_b64 {P[0]}, {r}, {xp}", [xp], [P[0]])
+        if r == 32:
+            h = xhi
+        else:
+            h = v[4]
+            sg.add(f"v_lshrrev_b32 {h}, {32 - r}, {xhi}", [xhi], [h])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {h}, -1, {P[0]}", [h, P[0]], [P[1], c[0]])
+        if e > 32:
+            sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[0]}", [c[0]], [v[4]])
+            sg.add(f"v_mad_u64_u32 {P[0]}, {JUNK}, {v[4]}, 1, {P[1]}", [v[4], P[1]], [P[0], JUNK])
+            sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
+            sg.add(f"v_mov_b32 {v[7]}, {v[0]}", [v[0]], [v[7]])
+            sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[1]}, -1, {P[3]}", [v[1], P[3]], [P[1], c[0]])
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {P[1]}", [P[1]], [P[0], c[1]])
+        sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
+        sg.add(f"v_cndmask_b32_e64 {tlo}, {v[2]}, {v[0]}, {c[1]}", [v[2], v[0], c[1]], [tlo])
+        sg.add(f"v_cndmask_b32_e64 {thi}, {v[3]}, {v[1]}, {c[1]}", [v[3], v[1], c[1]], [thi])
+        return neg
+    K = 96 - e
+    sg.add(f"v_lshrrev_b64 {P[0]}, {K}, {xp}", [xp], [P[0]])
+    if K == 32:
+        u = xlo
+    else:
+        u = v[4]
+        sg.add(f"v_lshlrev_b32 {u}, {32 - K}, {xlo}", [xlo], [u])
+    sg.add(f"v_mad_u64_u32 {P[1]}, {JUNK}, {u}, 1, {P[0]}", [u, P[0]], [P[1], JUNK])
+    sg.add(f"v_sub_co_u32_e64 {v[3]}, {c[0]}, {v[3]}, {u}", [v[3], u], [v[3], c[0]])
+    sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -1, {c[0]}", [c[0]], [v[5]])
+    sg.add(f"v_addc_co_u32_e64 {tlo}, {c[1]}, {v[2]}, 0, {c[0]}", [v[2], c[0]], [tlo, c[1]])
+    sg.add(f"v_addc_co_u32_e64 {thi}, {JUNK}, {v[3]}, {v[5]}, {c[1]}", [v[3], v[5], c[1]], [thi, JUNK])
+    return neg
+
+
+def add_part1(sg, sl, alo, ahi, tlo, thi):
+    v, c = sl.v, sl.c
+    sg.add(f"v_add_co_u32_e64 {v[0]}, {c[2]}, {alo}, {tlo}", [alo, tlo], [v[0], c[2]])
+    sg.add(f"v_addc_co_u32_e64 {v[1]}, {c[2]}, {ahi}, {thi}, {c[2]}", [ahi, thi, c[2]], [v[1], c[2]])
+
+
+def add_part2(sg, sl, dp):
+    v, P, c = sl.v, sl.P, sl.c
+    sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -1, {c[2]}", [c[2]], [v[5]])
+    sg.add(f"v_mad_u64_u32 {dp}, {JUNK}, {v[5]}, 1, {P[0]}", [v[5], P[0]], [dp, JUNK])
+
+
+def sub_seq(sg, sl, dlo, dhi, alo, ahi, tlo, thi):
+    v, c = sl.v, sl.c
+    sg.add(f"v_sub_co_u32_e64 {dlo}, {c[0]}, {alo}, {tlo}", [alo, tlo], [dlo, c[0]])
+    sg.add(f"v_subb_co_u32_e64 {dhi}, {c[1]}, {ahi}, {thi}, {c[0]}", [ahi, thi, c[0]], [dhi, c[1]])
+    sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[1]}", [c[1]], [v[4]])
+    sg.add(f"v_addc_co_u32_e64 {dlo}, {c[0]}, {dlo}, 0, {c[1]}", [dlo, c[1]], [dlo, c[0]])
+    sg.add(f"v_addc_co_u32_e64 {dhi}, {JUNK}, {dhi}, {v[4]}, {c[0]}", [dhi, v[4], c[0]], [dhi, JUNK])
+
+
+def ct_core(sg, sl, a, b, neg):
+    """t in sl.v2:v3 (canonical); a, b = (lo, hi, pair)."""
+    alo, ahi, ap = a
+    blo, bhi, bp = b
+    tlo, thi = sl.v[2], sl.v[3]
+    add_part1(sg, sl, alo, ahi, tlo, thi)
+    if not neg:
+        sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
+        add_part2(sg, sl, ap)
+    else:
+        sub_seq(sg, sl, alo, ahi, alo, ahi, tlo, thi)
+        add_part2(sg, sl, bp)
+
+
+def ct(sg, sl, a, b, S):
+    neg = tmul(sg, S, b[0], b[1], b[2], sl, sl.v[2], sl.v[3])
+    ct_core(sg, sl, a, b, neg)
+
+
+def gs_core(sg, sl, a, b):
+    """a' = a + b, b <- a - b (both semi in, semi out); b canonicalised first."""
+    alo, ahi, ap = a
+    blo, bhi, bp = b
+    v, P, c = sl.v, sl.P, sl.c
+    sg.add(f"v_mad_u64_u32 {P[3]}, {c[1]}, -1, 1, {bp}", [bp], [P[3], c[1]])
+    sg.add(f"v_cndmask_b32_e64 {v[2]}, {blo}, {v[6]}, {c[1]}", [blo, v[6], c[1]], [v[2]])
+    sg.add(f"v_cndmask_b32_e64 {v[3]}, {bhi}, {v[7]}, {c[1]}", [bhi, v[7], c[1]], [v[3]])
+    add_part1(sg, sl, alo, ahi, v[2], v[3])
+    sub_seq(sg, sl, blo, bhi, alo, ahi, v[2], v[3])
+    add_part2(sg, sl, ap)
+
+
+def gs(sg, sl, a, b, S):
+    gs_core(sg, sl, a, b)
+    blo, bhi, bp = b
+    neg = tmul(sg, S, blo, bhi, bp, sl, blo, bhi)
+    if neg:
+        sg.add(f"v_sub_co_u32_e64 {blo}, {sl.c[2]}, 1, {blo}", [blo], [blo, sl.c[2]])
+        sg.add(f"v_subb_co_u32_e64 {bhi}, {JUNK}, -1, {bhi}, {sl.c[2]}", [bhi, sl.c[2]], [bhi, JUNK])
+
+
+def gmul(sg, ms, x, wlo, whi, olo, ohi):
+    """o = x * w canonical (x semi, w canonical), general 64x64 multiply (17 VALU)."""
+    xlo, xhi, _ = x
+    v, P, c = ms.v, ms.P, ms.c
+    PA, PB, PC, PD, Z1, Z2 = P
+    A0, A1, B0, B1, C0, C1, D0, D1, Z1l, Z1h, Z2l, Z2h = v
+    sg.add(f"v_mov_b32 {Z1h}, 0", [], [Z1h])
+    sg.add(f"v_mov_b32 {Z2h}, 0", [], [Z2h])
+    sg.add(f"v_mad_u64_u32 {PA}, {JUNK}, {xlo}, {wlo}, 0", [xlo, wlo], [PA, JUNK])
+    sg.add(f"v_mov_b32 {Z1l}, {A1}", [A1], [Z1l])
+    sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {xlo}, {whi}, {Z1}", [xlo, whi, Z1], [PB, JUNK])
+    sg.add(f"v_mov_b32 {Z2l}, {B0}", [B0], [Z2l])
+    sg.add(f"v_mov_b32 {Z1l}, {B1}", [B1], [Z1l])
+    sg.add(f"v_mad_u64_u32 {PC}, {JUNK}, {xhi}, {wlo}, {Z2}", [xhi, wlo, Z2], [PC, JUNK])
+    sg.add(f"v_mad_u64_u32 {PD}, {JUNK}, {xhi}, {whi}, {Z1}", [xhi, whi, Z1], [PD, JUNK])
+    sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {C1}, 1, {PD}", [C1, PD], [PB, JUNK])          # H = D + C.hi
+    sg.add(f"v_sub_co_u32_e64 {D0}, {c[0]}, {A0}, {B1}", [A0, B1], [D0, c[0]])          # T = L - H1
+    sg.add(f"v_subb_co_u32_e64 {D1}, {c[1]}, {C0}, 0, {c[0]}", [C0, c[0]], [D1, c[1]])
+    sg.add(f"v_cndmask_b32_e64 {Z2l}, 0, -1, {c[1]}", [c[1]], [Z2l])
+    sg.add(f"v_sub_co_u32_e64 {D0}, {c[0]}, {D0}, {Z2l}", [D0, Z2l], [D0, c[0]])
+    sg.add(f"v_subb_co_u32_e64 {D1}, {JUNK}, {D1}, 0, {c[0]}", [D1, c[0]], [D1, JUNK])
+    sg.add(f"v_mad_u64_u32 {PA}, {c[0]}, {B0}, -1, {PD}", [B0, PD], [PA, c[0]])         # R = T + H0 EPS
+    sg.add(f"v_mad_u64_u32 {PC}, {c[1]}, -1, 1, {PA}", [PA], [PC, c[1]])                # U = R + EPS
+    sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
+    sg.add(f"v_cndmask_b32_e64 {olo}, {A0}, {C0}, {c[1]}", [A0, C0, c[1]], [olo])
+    sg.add(f"v_cndmask_b32_e64 {ohi}, {A1}, {C1}, {c[1]}", [A1, C1, c[1]], [ohi])
+
+
+def canon(sg, sl, x):
+    xlo, xhi, xp = x
+    v, P, c = sl.v, sl.P, sl.c
+    sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {xp}", [xp], [P[0], c[1]])
+    sg.add(f"v_cndmask_b32_e64 {xlo}, {xlo}, {v[0]}, {c[1]}", [xlo, v[0], c[1]], [xlo])
+    sg.add(f"v_cndmask_b32_e64 {xhi}, {xhi}, {v[1]}, {c[1]}", [xhi, v[1], c[1]], [xhi])
+
+
+# ------------------------------------------------------------------------------------------------
+class Body:
+    def __init__(self, tabs):
+        self.tabs = tabs
+        self.lines = []
+        self.nvalu = 0
+
+    def out(self, lines):
+        self.lines += lines
+        self.nvalu += sum(1 for l in lines if l.startswith("v_"))
+
+    def raw(self, *lines):
+        self.out(list(lines))
+
+    # slots from a list of free 8-register blocks
+    @staticmethod
+    def slots(free_blocks, n=None):
+        sl = []
+        for i, b in enumerate(free_blocks[: n or len(free_blocks)]):
+            sl.append(Slot(b, SG0 + 6 * i))
+        return sl
+
+    def stage(self, kind, dist, exps, dmap, free_blocks):
+        sg = Seg()
+        slots = self.slots(free_blocks)
+        bf = 0
+        for r in range(32):
+            if r & dist:
+                continue
+            S = exps[r // (2 * dist)]
+            sl = slots[bf % len(slots)]
+            a, b = X(dmap, r), X(dmap, r + dist)
+            if kind == "ct":
+                ct(sg, sl, a, b, S)
+            else:
+                gs(sg, sl, a, b, S)
+            bf += 1
+        for i, op in enumerate(sg.ops):
+            op.idx = i
+        self.out(sg.schedule())
+
+    def mulrows(self, dmap, rows, wregs, mslots):
+        """x[r] = x[r] * w (general), w in wregs[k] (pair base)."""
+        sg = Seg()
+        for k, r in enumerate(rows):
+            ms = mslots[k % len(mslots)]
+            x = X(dmap, r)
+            wb = wregs[k]
+            gmul(sg, ms, x, f"v{wb}", f"v{wb + 1}", x[0], x[1])
+        for i, op in enumerate(sg.ops):
+            op.idx = i
+        self.out(sg.schedule())
+
+
+def load_tables():
+    here = os.path.dirname(os.path.abspath(__file__))
+    hdr = os.path.join(here, "..", "tfhe-rs-main_modified_amd", "csrc", "ntt64_tw_tables.hpp")
+    tabs, cur = {}, None
+    for line in open(hdr):
+        line = line.strip()
+        if line.startswith("constexpr int"):
+            cur = line.split()[2].split("[")[0]
+            tabs[cur] = []
+        elif cur and line.startswith("{"):
+            tabs[cur].append([int(t) for t in line.strip("{},").split(",")])
+        elif line.startswith("};"):
+            cur = None
+    return tabs
+
+
+# SGPR map (beyond the carry pairs s20..s75 of up to 7 slots)
+S_GB = 78    # s[78:85]: data row-group bases g + 4096 m, m = 0..3
+S_TB = 86    # s[86:93]: table bases
+S_PAR = 20   # s[20:21]: odd-lane mask
+S_EXE = 22   # s[22:23]: saved exec
+
+
+def bases(body, reg_g, dst):
+    for m in range(4):
+        body.raw(f"s_add_u32 s{dst + 2 * m}, {reg_g}[0], {4096 * m}")
+    # (replaced below by proper lo/hi handling)
+
+
+def gen_bases(src, dst):
+    """dst pairs = src + 4096 m; src is an asm operand name for an SGPR pair."""
+    lines = []
+    for m in range(4):
+        lines.append(f"s_add_u32 s{dst + 2 * m}, %[{src}_lo], {4096 * m}")
+        lines.append(f"s_addc_u32 s{dst + 2 * m + 1}, %[{src}_hi], 0")
+    return lines
+
+
+def load_rows(dmap, base, voff="%[l8]"):
+    out = []
+    for r in range(32):
+        out.append(f"global_load_dwordx2 {pv(dmap[r])}, {voff}, s[{base + 2 * (r // 8)}:{base + 2 * (r // 8) + 1}] "
+                   f"offset:{512 * (r % 8)}")
+    return out
+
+
+def store_rows(dmap, base):
+    out = []
+    for r in range(32):
+        out.append(f"global_store_dwordx2 %[l8], {pv(dmap[r])}, s[{base + 2 * (r // 8)}:{base + 2 * (r // 8) + 1}] "
+                   f"offset:{512 * (r % 8)}")
+    return out
+
+
+EXEC_LO = [f"s_mov_b32 exec_hi, 0"]          # lanes 0..31 (assumes exec was all ones)
+EXEC_HI = [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
+EXEC_ALL = [f"s_mov_b64 exec, s[{S_EXE}:{S_EXE + 1}]"]
+
+
+def t1(body, dmap, ybase, newhi):
+    """W0 -> W1 (split by j half).  Returns the new dmap (x[q] in y for q < 16, x[16+q] at newhi)."""
+    L = []
+    L += [f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"]
+    for r in range(32):
+        L.append(f"ds_write_b64 %[t1w], {pv(dmap[r])} offset:{r * 34 * 8}")
+    L += EXEC_ALL
+    for q in range(16):
+        L.append(f"ds_read_b64 {pv(ybase + 2 * q)}, %[t1r] offset:{2 * q * 8}")
+    L += [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
+    for r in range(32):
+        L.append(f"ds_write_b64 %[t1w], {pv(dmap[r])} offset:{r * 34 * 8}")
+    L += EXEC_ALL
+    L.append("s_waitcnt lgkmcnt(0)")
+    for q in range(16):
+        L.append(f"ds_read_b64 {pv(newhi + 2 * q)}, %[t1r] offset:{2 * q * 8}")
+    L.append("s_waitcnt lgkmcnt(0)")
+    body.raw(*L)
+    return [ybase + 2 * q for q in range(16)] + [newhi + 2 * q for q in range(16)]
+
+
+def t_iw0(body, dmap, pairs, ybase, newhi):
+    """W1 (pairs=False) or W1' (pairs=True) -> W0, halves split by i (row stride 66)."""
+    L = []
+    for h in range(2):
+        L += ([f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"] if h == 0 else
+              [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"])
+        for k in range(32):
+            if pairs:
+                if k < 16:
+                    L.append(f"ds_write_b64 %[t2wl], {pv(dmap[k])} offset:{2 * k * 8}")
+                else:
+                    L.append(f"ds_write_b64 %[t2wh], {pv(dmap[k])} offset:{2 * (k - 16) * 8}")
+            else:
+                L.append(f"ds_write_b64 %[t4w], {pv(dmap[k])} offset:{2 * k * 8}")
+        L += EXEC_ALL
+        if h == 1:
+            L.append("s_waitcnt lgkmcnt(0)")
+        dst = ybase if h == 0 else newhi
+        rb = "%[t2r]" if pairs else "%[t4r]"
+        for r in range(16):
+            L.append(f"ds_read_b64 {pv(dst + 2 * r)}, {rb} offset:{r * 66 * 8}")
+    L.append("s_waitcnt lgkmcnt(0)")
+    body.raw(*L)
+    return [ybase + 2 * r for r in range(16)] + [newhi + 2 * r for r in range(16)]
+
+
+def regroup(sg, dmap, k, tmp, to_pairs):
+    """W1 <-> W1' for register pair (k, k+16) of this lane and its partner (lane ^ 1).
+    to_pairs: even lane ends with (a_k, b_k), odd lane with (a_{k+16}, b_{k+16}).
+    back:     even lane ends with (a_k, a_{k+16}), odd lane with (b_k, b_{k+16})."""
+    lo0, hi0, p0 = X(dmap, k)
+    lo1, hi1, p1 = X(dmap, k + 16)
+    T0, T1, U0, U1 = tmp
+    par = f"s[{S_PAR}:{S_PAR + 1}]"
+    dpp = "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+    if to_pairs:
+        # T = partner x[k], U = partner x[k+16]; even: x[k+16] <- T ; odd: x[k] <- U
+        sg.add(f"v_mov_b32_dpp {T0}, {lo0} {dpp}", [lo0], [T0], "dpp")
+        sg.add(f"v_mov_b32_dpp {T1}, {hi0} {dpp}", [hi0], [T1], "dpp")
+        sg.add(f"v_mov_b32_dpp {U0}, {lo1} {dpp}", [lo1], [U0], "dpp")
+        sg.add(f"v_mov_b32_dpp {U1}, {hi1} {dpp}", [hi1], [U1], "dpp")
+        sg.add(f"v_cndmask_b32_e64 {lo0}, {lo0}, {U0}, {par}", [lo0, U0, par], [lo0])
+        sg.add(f"v_cndmask_b32_e64 {hi0}, {hi0}, {U1}, {par}", [hi0, U1, par], [hi0])
+        sg.add(f"v_cndmask_b32_e64 {lo1}, {T0}, {lo1}, {par}", [T0, lo1, par], [lo1])
+        sg.add(f"v_cndmask_b32_e64 {hi1}, {T1}, {hi1}, {par}", [T1, hi1, par], [hi1])
+    else:
+        # even holds (a_k, b_k) -> wants (a_k, a_{k+16}) ; odd holds (a_{k+16}, b_{k+16}) -> (b_k, b_{k+16})
+        sg.add(f"v_mov_b32_dpp {T0}, {lo0} {dpp}", [lo0], [T0], "dpp")   # partner's first
+        sg.add(f"v_mov_b32_dpp {T1}, {hi0} {dpp}", [hi0], [T1], "dpp")
+        sg.add(f"v_mov_b32_dpp {U0}, {lo1} {dpp}", [lo1], [U0], "dpp")   # partner's second
+        sg.add(f"v_mov_b32_dpp {U1}, {hi1} {dpp}", [hi1], [U1], "dpp")
+        # even: x[k+16] <- T (partner a_{k+16}) ; odd: x[k] <- U (partner b_k)
+        sg.add(f"v_cndmask_b32_e64 {lo1}, {T0}, {lo1}, {par}", [T0, lo1, par], [lo1])
+        sg.add(f"v_cndmask_b32_e64 {hi1}, {T1}, {hi1}, {par}", [T1, hi1, par], [hi1])
+        sg.add(f"v_cndmask_b32_e64 {lo0}, {lo0}, {U0}, {par}", [lo0, U0, par], [lo0])
+        sg.add(f"v_cndmask_b32_e64 {hi0}, {hi0}, {U1}, {par}", [hi0, U1, par], [hi0])
+
+
+def free_blocks_except(dmap, extra_busy=()):
+    busy = set()
+    for b in dmap:
+        busy.update((b, b + 1))
+    busy.update(extra_busy)
+    blocks = []
+    for b in range(VLO, VHI, 8):
+        if not any(x in busy for x in range(b, b + 8)):
+            blocks.append(b)
+    return blocks
+
+
+def slot_view(m, c23):
+    """CT/GS scratch view over a general-multiply slot (used after / around its multiply)."""
+    sl = Slot.__new__(Slot)
+    sl.v = m.v[0:8]
+    sl.P = [m.P[0], m.P[1], m.P[2], m.P[3]]
+    sl.c = [m.c[0], m.c[1], c23[0]]
+    return sl
+
+
+def pair_stage(B, dmap, fwd):
+    """Cyclic stage q = 5 on lane pairs: regroup W1 -> W1' (DPP), butterfly with the per-lane twiddle
+    w_g, g = k + 16 (lane & 1), from the 32-entry table; forward: CT then canonical outputs (layout
+    stays W1' for T2); inverse: GS then regroup back to W1."""
+    regs = []
+    for b in free_blocks_except(dmap):
+        regs += list(range(b, b + 8))
+    assert len(regs) >= 48, len(regs)
+    wb = regs[0:16]
+    tmps = [regs[16:20], regs[20:24]]
+    msl = [MulSlot(regs[24], SG0), MulSlot(regs[36], SG0 + 6)]
+    c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
+    for half in range(2):
+        ks = list(range(8 * half, 8 * half + 8))
+        B.raw(*[f"global_load_dwordx2 {pv(wb[2 * i])}, %[lwo], %[lw] offset:{8 * k}" for i, k in enumerate(ks)],
+              "s_waitcnt vmcnt(0)", "s_nop 1")
+        sg = Seg()
+        for i, k in enumerate(ks):
+            tmp = [f"v{r}" for r in tmps[i % 2]]
+            m = msl[i % 2]
+            sl = slot_view(m, c23[i % 2])
+            wlo, whi = f"v{wb[2 * i]}", f"v{wb[2 * i] + 1}"
+            regroup(sg, dmap, k, tmp, True)
+            a, b = X(dmap, k), X(dmap, k + 16)
+            if fwd:
+                # t = b * w into the slot's Z1 pair, then CT with t viewed as v2:v3
+                gmul(sg, m, b, wlo, whi, m.v[8], m.v[9])
+                ct_sl = Slot.__new__(Slot)
+                ct_sl.v = [m.v[0], m.v[1], m.v[8], m.v[9], m.v[4], m.v[5], m.v[6], m.v[7]]
+                ct_sl.P = [m.P[0], None, None, m.P[3]]
+                ct_sl.c = sl.c
+                ct_core(sg, ct_sl, a, b, False)
+                canon(sg, ct_sl, a)
+                canon(sg, ct_sl, b)
+            else:
+                gs_core(sg, sl, a, b)
+                gmul(sg, m, b, wlo, whi, b[0], b[1])
+                regroup(sg, dmap, k, tmp, False)
+        for j, op in enumerate(sg.ops):
+            op.idx = j
+        B.out(sg.schedule())
+
+
+def store_raw(dmap):
+    return store_rows(dmap, S_GB) + ["s_waitcnt vmcnt(0)"]
+
+
+def gen_fwd(tabs, stop=None):
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    fb = free_blocks_except(dmap)
+    for s in range(5):
+        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
+    if stop == "g1":
+        B.raw(*store_raw(dmap)); return B
+    # twist: 4 batches of 8 rows, table rows in v8..v23, 3 multiply slots in v24..v59
+    ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
+    for bt in range(4):
+        rows = list(range(8 * bt, 8 * bt + 8))
+        B.raw(*[f"global_load_dwordx2 {pv(8 + 2 * k)}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] offset:{512 * k}"
+                for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms)
+    if stop == "twist":
+        B.raw(*store_raw(dmap)); return B
+    dmap = t1(B, dmap, 8, 64)
+    if stop == "t1":
+        B.raw(*store_raw(dmap)); return B
+    fb = free_blocks_except(dmap)
+    for q in range(5):
+        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb)
+    if stop == "cyc":
+        B.raw(*store_raw(dmap)); return B
+    pair_stage(B, dmap, True)
+    if stop == "last":
+        B.raw(*store_raw(dmap)); return B
+    dmap = t_iw0(B, dmap, True, 96, 64)
+    B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    return B
+
+
+def gen_inv(tabs, stop=None):
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    dmap = t1(B, dmap, 8, 64)
+    pair_stage(B, dmap, False)
+    fb = free_blocks_except(dmap)
+    for q in range(4, -1, -1):
+        B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb)
+    dmap = t_iw0(B, dmap, False, 96, 64)
+    # untwist: table rows in v8..v23 are free? dmap now occupies v8..v39 (rows 0..15) and v64..v95
+    free = free_blocks_except(dmap)
+    regs = []
+    for b in free:
+        regs += list(range(b, b + 8))
+    ms = [MulSlot(regs[16 + 12 * i], SG0 + 6 * i) for i in range((len(regs) - 16) // 12)]
+    for bt in range(4):
+        rows = list(range(8 * bt, 8 * bt + 8))
+        B.raw(*[f"global_load_dwordx2 {pv(regs[2 * k])}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] "
+                f"offset:{512 * k}" for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms)
+    fb = free_blocks_except(dmap)
+    for s in range(4, -1, -1):
+        B.stage("gs", 16 >> s, tabs["G1_INV"][s], dmap, fb)
+    sg = Seg()
+    sls = B.slots(fb)
+    for r in range(32):
+        canon(sg, sls[r % len(sls)], X(dmap, r))
+    for j, op in enumerate(sg.ops):
+        op.idx = j
+    B.out(sg.schedule())
+    B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    return B
+
+
+def emit(name, body, ops_in):
+    clob = [f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
+    text = "\n".join(f'      "{l}\\n"' for l in body.lines)
+    return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
+            f"#define MI_TW_BODY_{name.upper()}(...) asm volatile(\\\n" +
+            "\\\n".join(f'      "{l}\\n"' for l in body.lines) +
+            f"\\\n      :: __VA_ARGS__ \\\n      : {', '.join(clob)})\n")
+
+
+def main():
+    tabs = load_tables()
+    if len(sys.argv) > 1 and sys.argv[1] == "debug":
+        print("#pragma once")
+        for st in ("g1", "twist", "t1", "cyc", "last"):
+            print(emit("fwd_" + st, gen_fwd(tabs, st), None))
+        return
+    f, i = gen_fwd(tabs), gen_inv(tabs)
+    print("// GENERATED by tools/gen_tw_kernel.py — do not edit.  Whole-data-path asm bodies of the twisted")
+    print("// N = 2048 Goldilocks transform (ntt64_tw.hip).  Owns v8..v127, s20..s31 + s36..s93, exec (restored).")
+    print("#pragma once")
+    print(emit("fwd", f, None))
+    print(emit("inv", i, None))
+    print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
