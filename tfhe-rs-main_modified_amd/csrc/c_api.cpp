@@ -66,9 +66,10 @@ struct DeviceGuard {
 
 u64 mont_form(u64 x, u64 p) { return (u64)(((u128)x << 64) % p); }
 
+// MI_NTT_VARIANT selects a kernel family for benchmarking (-1 / unset = the default choice).
 int env_variant() {
   const char* v = std::getenv("MI_NTT_VARIANT");
-  return v ? std::atoi(v) : 0;
+  return v ? std::atoi(v) : -1;
 }
 
 }  // namespace
@@ -108,7 +109,7 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   plan->p = p;
   plan->device = device;
   plan->goldilocks = (p == mi::host::SOLINAS_P);
-  plan->variant = env_variant();  // default 0; the Solinas N = 2048 plan maps 0 to the twisted kernel (4) below
+  plan->variant = env_variant();
 
   // prime64.rs:162-182: Solinas uses the hard-coded friendly root tower, other primes the
   // Tonelli-Shanks root.
@@ -208,6 +209,8 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
       }
     }
   }
+  // default kernel: the twisted shift-twiddle transform where it applies, else the window kernels
+  if (plan->variant < 0) plan->variant = plan->d_twist_f ? 4 : 0;
   *out_plan = plan;
   return MI_OK;
 }

@@ -258,11 +258,15 @@ def sub_seq(sg, sl, dlo, dhi, alo, ahi, tlo, thi):
     sg.add(f"v_addc_co_u32_e64 {dhi}, {JUNK}, {dhi}, {v[4]}, {c[0]}", [dhi, v[4], c[0]], [dhi, JUNK])
 
 
-def ct_core(sg, sl, a, b, neg):
-    """t in sl.v2:v3 (canonical); a, b = (lo, hi, pair)."""
+def ct_core(sg, sl, a, b, neg, tsrc=None):
+    """t in sl.v2:v3 (or tsrc) canonical; a, b = (lo, hi, pair)."""
     alo, ahi, ap = a
     blo, bhi, bp = b
-    tlo, thi = sl.v[2], sl.v[3]
+    tlo, thi = tsrc if tsrc else (sl.v[2], sl.v[3])
+    if tsrc:  # t aliases b, which the subtraction overwrites: keep a copy
+        sg.add(f"v_mov_b32 {sl.v[2]}, {tlo}", [tlo], [sl.v[2]])
+        sg.add(f"v_mov_b32 {sl.v[3]}, {thi}", [thi], [sl.v[3]])
+        tlo, thi = sl.v[2], sl.v[3]
     add_part1(sg, sl, alo, ahi, tlo, thi)
     if not neg:
         sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
@@ -290,13 +294,44 @@ def gs_core(sg, sl, a, b):
     add_part2(sg, sl, ap)
 
 
-def gs(sg, sl, a, b, S):
-    gs_core(sg, sl, a, b)
+def gs(sg, sl, a, b, S, ac=False, bc=False):
+    """GS butterfly; ac / bc: whether a / b are known canonical (skips the canonicalisation).
+    Returns whether the new b is canonical."""
+    alo, ahi, ap = a
     blo, bhi, bp = b
-    neg = tmul(sg, S, blo, bhi, bp, sl, blo, bhi)
+    v, P, c = sl.v, sl.P, sl.c
+    e = S % 96
+    neg = (S >= 96) != (e >= 64)
+    if bc or not ac:
+        if not bc:  # canonicalise b into v2:v3, then a' = a + cb, b <- a - cb
+            sg.add(f"v_mad_u64_u32 {P[3]}, {c[1]}, -1, 1, {bp}", [bp], [P[3], c[1]])
+            sg.add(f"v_cndmask_b32_e64 {v[2]}, {blo}, {v[6]}, {c[1]}", [blo, v[6], c[1]], [v[2]])
+            sg.add(f"v_cndmask_b32_e64 {v[3]}, {bhi}, {v[7]}, {c[1]}", [bhi, v[7], c[1]], [v[3]])
+            tlo, thi = v[2], v[3]
+        else:
+            tlo, thi = blo, bhi
+        if neg and ac:
+            # (a - b) w = (b - a) |w|: subtract the canonical a instead, no negation afterwards
+            add_part1(sg, sl, alo, ahi, tlo, thi)
+            sub_seq(sg, sl, blo, bhi, tlo, thi, alo, ahi) if bc else sub_seq(sg, sl, blo, bhi, v[2], v[3], alo, ahi)
+            add_part2(sg, sl, ap)
+            neg = False
+        else:
+            add_part1(sg, sl, alo, ahi, tlo, thi)
+            sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
+            add_part2(sg, sl, ap)
+    else:
+        # only a canonical: a' = b + a, b <- b - a, sign flips
+        add_part1(sg, sl, blo, bhi, alo, ahi)
+        sub_seq(sg, sl, blo, bhi, blo, bhi, alo, ahi)
+        add_part2(sg, sl, ap)
+        neg = not neg
+    tmul(sg, S, blo, bhi, bp, sl, blo, bhi)
     if neg:
         sg.add(f"v_sub_co_u32_e64 {blo}, {sl.c[2]}, 1, {blo}", [blo], [blo, sl.c[2]])
         sg.add(f"v_subb_co_u32_e64 {bhi}, {JUNK}, -1, {bhi}, {sl.c[2]}", [bhi, sl.c[2]], [bhi, JUNK])
+        return False
+    return True
 
 
 def gmul(sg, ms, x, wlo, whi, olo, ohi):
@@ -357,10 +392,13 @@ class Body:
             sl.append(Slot(b, SG0 + 6 * i))
         return sl
 
-    def stage(self, kind, dist, exps, dmap, free_blocks):
+    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None):
+        """canon: list of 32 flags (logical registers known canonical), updated in place."""
         sg = Seg()
         slots = self.slots(free_blocks)
         bf = 0
+        if canon is None:
+            canon = [False] * 32
         for r in range(32):
             if r & dist:
                 continue
@@ -368,9 +406,14 @@ class Body:
             sl = slots[bf % len(slots)]
             a, b = X(dmap, r), X(dmap, r + dist)
             if kind == "ct":
-                ct(sg, sl, a, b, S)
+                if S % 96 == 0 and canon[r + dist]:
+                    ct_core(sg, sl, a, b, S >= 96, tsrc=(b[0], b[1]))
+                else:
+                    ct(sg, sl, a, b, S)
+                canon[r] = canon[r + dist] = False
             else:
-                gs(sg, sl, a, b, S)
+                canon[r + dist] = gs(sg, sl, a, b, S, canon[r], canon[r + dist])
+                canon[r] = False
             bf += 1
         for i, op in enumerate(sg.ops):
             op.idx = i
@@ -583,7 +626,10 @@ def pair_stage(B, dmap, fwd):
                 canon(sg, ct_sl, a)
                 canon(sg, ct_sl, b)
             else:
-                gs_core(sg, sl, a, b)
+                # inputs are canonical (loaded data): a' = a + b, b <- a - b, no canonicalisation
+                add_part1(sg, sl, a[0], a[1], b[0], b[1])
+                sub_seq(sg, sl, b[0], b[1], a[0], a[1], b[0], b[1])
+                add_part2(sg, sl, a[2])
                 gmul(sg, m, b, wlo, whi, b[0], b[1])
                 regroup(sg, dmap, k, tmp, False)
         for j, op in enumerate(sg.ops):
@@ -620,8 +666,9 @@ def gen_fwd(tabs, stop=None):
     if stop == "t1":
         B.raw(*store_raw(dmap)); return B
     fb = free_blocks_except(dmap)
+    cf = [True] * 32  # twist outputs are canonical
     for q in range(5):
-        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb)
+        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf)
     if stop == "cyc":
         B.raw(*store_raw(dmap)); return B
     pair_stage(B, dmap, True)
@@ -642,8 +689,9 @@ def gen_inv(tabs, stop=None):
     dmap = t1(B, dmap, 8, 64)
     pair_stage(B, dmap, False)
     fb = free_blocks_except(dmap)
+    cf = [False] * 32
     for q in range(4, -1, -1):
-        B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb)
+        B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
     dmap = t_iw0(B, dmap, False, 96, 64)
     # untwist: table rows in v8..v23 are free? dmap now occupies v8..v39 (rows 0..15) and v64..v95
     free = free_blocks_except(dmap)
@@ -657,8 +705,9 @@ def gen_inv(tabs, stop=None):
                 f"offset:{512 * k}" for k in range(8)], "s_waitcnt vmcnt(0)")
         B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms)
     fb = free_blocks_except(dmap)
+    cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
-        B.stage("gs", 16 >> s, tabs["G1_INV"][s], dmap, fb)
+        B.stage("gs", 16 >> s, tabs["G1_INV"][s], dmap, fb, cf)
     sg = Seg()
     sls = B.slots(fb)
     for r in range(32):
