@@ -189,6 +189,35 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
     return res
 
 
+def bench_ext_product(args, eng, torch, dev, world, barrier):
+    """Config 3: batched GGSW x GLWE external product (BNF: native GLWEs, Raw NTT GGSW), l = 1, base 2^23."""
+    M = eng.ntt64_pbs
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    batch = args.batch
+    ggsw = torch.empty((1, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ggsw, SEED + 30, SOLINAS_P)
+    glwe = torch.empty((batch, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(glwe, SEED + 31, 0)
+    out = torch.zeros((batch, 2, N), dtype=torch.int64, device=dev)
+    run = lambda: M.add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, PBS_BASE_LOG, 1)
+    run()
+    torch.cuda.synchronize()
+    K = max(3, args.steps // 5)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    return {"metric": "GGSW x GLWE external products/sec (config 3)", "value": world * batch * K / el,
+            "unit": "external products/s", "ms_per_step": el / K * 1e3,
+            "config": {"workload": "add_external_product_ntt64_bnf_assign, N=2048, k=1, level 1, base_log 23",
+                       "batch_per_gpu": batch},
+            "algorithmic_bytes_per_unit": 32768 + 65536}
+
+
 def load_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*/pmc_traffic.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -293,6 +322,7 @@ def main():
         "cpu_baseline": None,
     }
     if not args.no_pbs:
+        out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
