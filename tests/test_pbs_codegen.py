@@ -1,0 +1,51 @@
+"""CPU checks of the generated blind-rotation asm (tools/gen_pbs_kernel.py, no GPU): the committed
+header matches its generator, and a 2-wave emulation of the body (tools/asm_emu.py) followed by the
+wrapper's final rotation + sample extraction (pbs_tw.hip) equals the oracle BNF PBS bit for bit."""
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from test_tw_codegen import _tables
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "tfhe-rs-main_modified_amd", "csrc", "pbs_tw_body.hpp")
+P = 0xFFFFFFFF00000001
+N = 2048
+
+
+def test_pbs_header_is_generated():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_pbs_kernel.py")], capture_output=True,
+                         text=True, check=True).stdout
+    assert out == open(HDR).read(), "regenerate csrc/pbs_tw_body.hpp with tools/gen_pbs_kernel.py"
+
+
+def _extract(acc, body, oracle):
+    """pbs_tw.hip epilogue: rotate by -ms(b), sample-extract coefficient 0."""
+    glwe = np.concatenate([oracle.poly_monomial_div(acc[c], oracle.modulus_switch(body, 12)) for c in range(2)])
+    return oracle.sample_extract(glwe, N, 1)
+
+
+@pytest.mark.parametrize("seed,base_log", [(1, 23), (2, 10), (3, 31)])
+def test_emulated_pbs_matches_oracle(oracle, seed, base_log):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_emu
+    plan, tf, ti = _tables(oracle)
+    ctx = oracle.NttContext(N)
+    rnd = random.Random(seed)
+    n_lwe = 4
+    bsk = np.array([rnd.randrange(P) for _ in range(n_lwe * 4 * N)], dtype=np.uint64)
+    n_inv = int(plan.n_inv)
+    bsk_norm = np.array([int(v) * n_inv % P for v in bsk], dtype=np.uint64)
+    lut = np.array([rnd.getrandbits(64) for _ in range(2 * N)], dtype=np.uint64)
+    # mask values: ms = 0 (skipped step), ms >= N (negacyclic wrap), ms = 2047 / 1 (extremes), random
+    ms_vals = [0, 2048 + 5, 2047, 1] if seed == 1 else [rnd.randrange(4096) for _ in range(n_lwe)]
+    lwe = [(m << 52) + rnd.getrandbits(50) - (1 << 50) & (2**64 - 1) for m in ms_vals] + [rnd.getrandbits(64)]
+    lwe = np.array(lwe, dtype=np.uint64)
+    want = ctx.pbs(lwe, lut, bsk, 1, base_log, 1, bnf=True)
+    acc = asm_emu.run_pbs(HDR, lwe, lut, bsk_norm, tf + ti, base_log, n_lwe)
+    got = _extract(acc, int(lwe[-1]), oracle)
+    assert np.array_equal(got, want)

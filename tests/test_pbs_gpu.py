@@ -103,7 +103,7 @@ def _pbs_inputs(g, batch, n_lwe, q):
 
 
 @pytest.mark.parametrize("bnf,centered", [(True, False), (True, True), (False, False)])
-@pytest.mark.parametrize("level,base_log", [(1, 23), (2, 15)])
+@pytest.mark.parametrize("level,base_log", [(1, 23), (2, 15), (1, 1), (1, 31)])
 def test_pbs_parity_random_key(engine, plan, ctx, oracle, bnf, centered, level, base_log):
     q = 0 if bnf else P
     g = H.rng(31 + 2 * bnf + centered + 10 * level)
@@ -124,9 +124,13 @@ def test_pbs_parity_random_key(engine, plan, ctx, oracle, bnf, centered, level, 
     assert np.array_equal(host(out), want)
 
 
-def test_pbs_parity_config4_shape(engine, plan, ctx):
+@pytest.mark.parametrize("kernel", ["twisted", "generic"])
+def test_pbs_parity_config4_shape(engine, plan, ctx, monkeypatch, kernel):
     """PARAM_MESSAGE_2_CARRY_2 shape (n = 918, beta = 2^23, l = 1, BNF) on a random key, vs the
-    multi-threaded oracle."""
+    multi-threaded oracle; both the twisted-transform kernel (default, pbs_tw.hip) and the generic
+    one (pbs_kernels.hip, MI_PBS_VARIANT=0)."""
+    if kernel == "generic":
+        monkeypatch.setenv("MI_PBS_VARIANT", "0")
     g = H.rng(918)
     n_lwe, batch, base_log, level = 918, 48, 23, 1
     bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)

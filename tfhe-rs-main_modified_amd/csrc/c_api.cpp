@@ -72,6 +72,12 @@ int env_variant() {
   return v ? std::atoi(v) : -1;
 }
 
+// MI_PBS_VARIANT=0 forces the generic PBS kernel (pbs_kernels.hip) where the twisted one applies.
+int env_pbs_variant() {
+  const char* v = std::getenv("MI_PBS_VARIANT");
+  return v ? std::atoi(v) : -1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -194,13 +200,14 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
           b = mi::host::mul_mod(b, rho_inv, p);
         }
       }
-      if (hipMalloc(&plan->d_twist_f, (n + 32) * sizeof(u64)) == hipSuccess &&
-          hipMalloc(&plan->d_twist_i, (n + 32) * sizeof(u64)) == hipSuccess &&
+      // one allocation [fwd | inverse] (the PBS body addresses both from one base, pbs_tw.hip)
+      if (hipMalloc(&plan->d_twist_f, 2 * (n + 32) * sizeof(u64)) == hipSuccess &&
           hipMemcpy(plan->d_twist_f, tf.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess &&
-          hipMemcpy(plan->d_twist_i, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess) {
+          hipMemcpy(plan->d_twist_f + n + 32, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
+              hipSuccess) {
+        plan->d_twist_i = plan->d_twist_f + n + 32;
       } else {
         if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);
-        if (plan->d_twist_i) (void)hipFree(plan->d_twist_i);
         plan->d_twist_f = plan->d_twist_i = nullptr;
         (void)hipFree(plan->d_twid);
         (void)hipFree(plan->d_inv_twid);
@@ -221,8 +228,7 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
     DeviceGuard g(plan->device);
     if (plan->d_twid) (void)hipFree(plan->d_twid);
     if (plan->d_inv_twid) (void)hipFree(plan->d_inv_twid);
-    if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);
-    if (plan->d_twist_i) (void)hipFree(plan->d_twist_i);
+    if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);  // d_twist_i points into the same allocation
   }
   delete plan;
   return MI_OK;
@@ -454,6 +460,12 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   const mi_ntt64_plan* plan = key->plan;
   DeviceGuard g(plan->device);
+  if (key->variant == MI_NTT64_BNF && key->level == 1 && key->base_log <= 31 && plan->d_twist_f &&
+      env_pbs_variant() != 0) {
+    hipError_t e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
+                                     plan->d_twist_f, ms_mode == MI_MS_CENTERED, (hipStream_t)stream);
+    return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
+  }
   hipError_t e = mi::launch_pbs(key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe,
                                 batch, key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED,
                                 (hipStream_t)stream);

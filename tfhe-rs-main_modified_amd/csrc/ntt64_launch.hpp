@@ -46,5 +46,8 @@ hipError_t launch_ext_product(bool bnf, bool cmux, int level, uint64_t* out, uin
 hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s);
+// BNF, level 1, base_log <= 31, on the twisted transform; tab = plan twist tables [fwd | inverse]
+hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const uint64_t* bsk, size_t n_lwe,
+                         size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s);
 
 }  // namespace mi

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Tiny functional emulator (one wave64) for the instruction subset the generated twisted-NTT
-bodies use (tools/gen_tw_kernel.py).  Checks the data path's logic on the CPU — not hazards or
-timing, which only the GPU run can.
+"""Small functional emulator of gfx950 wave64 execution for the instruction subset of the generated
+asm bodies (tools/gen_tw_kernel.py transforms, tools/gen_pbs_kernel.py blind rotation).  Checks the
+data path's logic on the CPU — not hazards or timing, which only the GPU run can.  Several waves of
+one workgroup share LDS and run round-robin between s_barrier instructions.
 
-  python tools/asm_emu.py            # runs the forward body on one random polynomial vs the oracle
+  python tools/asm_emu.py            # runs the transform bodies on one random polynomial vs the oracle
 """
 import os
 import re
@@ -13,46 +14,54 @@ import numpy as np
 
 M32 = np.uint64(0xFFFFFFFF)
 LANES = 64
+SH = np.arange(32, dtype=np.uint64)
+
+
+def _bits(word):
+    w = np.array([word & 0xFFFFFFFF, word >> 32], dtype=np.uint64)
+    return np.concatenate([((w[0] >> SH) & np.uint64(1)), ((w[1] >> SH) & np.uint64(1))]).astype(bool)
+
+
+def _word(m):
+    b = m.astype(np.uint64)
+    return int((b[:32] << SH).sum()) | (int((b[32:] << SH).sum()) << 32)
 
 
 class Wave:
-    def __init__(self, ops, mem, lds_bytes=65536):
+    def __init__(self, ops, mem, lds=None, lds_bytes=65536):
         self.v = np.zeros((256, LANES), dtype=np.uint64)   # 32-bit values kept in uint64
         self.s = np.zeros(128, dtype=np.uint64)
         self.exec = np.ones(LANES, dtype=bool)
-        self.vcc = np.zeros(LANES, dtype=bool)
-        self.lds = np.zeros(lds_bytes // 8, dtype=np.uint64)
+        self.lds = lds if lds is not None else np.zeros(lds_bytes // 8, dtype=np.uint64)
         self.mem = mem          # dict base_address -> np.uint64 array (global memory regions)
-        self.ops = ops          # operand name -> value
+        self.ops = ops          # operand name -> text
+        self.scc = 0
 
     # ---- operand parsing ----------------------------------------------------------------------
-    def vreg(self, tok):
+    @staticmethod
+    def vreg(tok):
         m = re.fullmatch(r"v(\d+)", tok)
         return int(m.group(1)) if m else None
 
-    def vpair(self, tok):
+    @staticmethod
+    def vpair(tok):
         m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
         return int(m.group(1)) if m else None
 
-    def spair(self, tok):
+    @staticmethod
+    def spair(tok):
         m = re.fullmatch(r"s\[(\d+):(\d+)\]", tok)
         return int(m.group(1)) if m else None
 
     def mask(self, tok):
-        if tok == "vcc":
-            return self.vcc.copy()
         b = self.spair(tok)
         if b is None:
             raise ValueError(tok)
-        word = int(self.s[b]) | (int(self.s[b + 1]) << 32)
-        return np.array([(word >> l) & 1 for l in range(LANES)], dtype=bool)
+        return _bits(int(self.s[b]) | (int(self.s[b + 1]) << 32))
 
     def set_mask(self, tok, m):
-        m = m & self.exec | (self.mask(tok) & ~self.exec) if tok != "vcc" else m
-        word = 0
-        for l in range(LANES):
-            if m[l]:
-                word |= 1 << l
+        m = (m & self.exec) | (self.mask(tok) & ~self.exec)
+        word = _word(m)
         b = self.spair(tok)
         self.s[b] = np.uint64(word & 0xFFFFFFFF)
         self.s[b + 1] = np.uint64(word >> 32)
@@ -64,15 +73,13 @@ class Wave:
         m = re.fullmatch(r"s(\d+)", tok)
         if m:
             return np.full(LANES, self.s[int(m.group(1))], dtype=np.uint64)
-        val = int(tok, 0)
-        return np.full(LANES, np.uint64(val & 0xFFFFFFFF), dtype=np.uint64)
+        return np.full(LANES, np.uint64(int(tok, 0) & 0xFFFFFFFF), dtype=np.uint64)
 
     def src64(self, tok):
         b = self.vpair(tok)
         if b is not None:
             return self.v[b] | (self.v[b + 1] << np.uint64(32))
-        val = int(tok, 0)
-        return np.full(LANES, np.uint64(val & 0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+        return np.full(LANES, np.uint64(int(tok, 0) & 0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
 
     def wv(self, r, val):
         self.v[r] = np.where(self.exec, val & M32, self.v[r])
@@ -82,20 +89,40 @@ class Wave:
         self.wv(b + 1, val >> np.uint64(32))
 
     # ---- execution ------------------------------------------------------------------------------
-    def run(self, lines):
+    def load(self, lines):
+        self.prog, self.labels = [], {}
         for line in lines:
             line = line.strip()
-            if not line or line.startswith("s_nop") or line.startswith("s_waitcnt"):
-                continue
             for k, v in self.ops.items():
                 line = line.replace(f"%[{k}]", v)
+            line = line.replace("%=", "0")
+            if not line or line.startswith("s_nop") or line.startswith("s_waitcnt"):
+                continue
+            if line.endswith(":"):
+                self.labels[line[:-1]] = len(self.prog)
+                continue
             mn, _, rest = line.partition(" ")
             args = [a.strip() for a in re.split(r",(?![^\[]*\])", rest)] if rest else []
-            getattr(self, "op_" + mn.replace(".", "_"), None) or self.unknown(mn)
-            getattr(self, "op_" + mn)(args)
+            fn = getattr(self, "op_" + mn, None)
+            if fn is None:
+                raise NotImplementedError(mn)
+            self.prog.append((fn, args, mn))
+        self.pc = 0
 
-    def unknown(self, mn):
-        raise NotImplementedError(mn)
+    def steps(self):
+        """Generator: runs to the end, yielding at every s_barrier."""
+        while self.pc < len(self.prog):
+            fn, args, mn = self.prog[self.pc]
+            self.pc += 1
+            if mn == "s_barrier":
+                yield
+                continue
+            fn(args)
+
+    def run(self, lines):
+        self.load(lines)
+        for _ in self.steps():
+            pass
 
     # VALU
     def op_v_mov_b32(self, a):
@@ -104,8 +131,8 @@ class Wave:
     def op_v_mov_b32_dpp(self, a):
         src = self.src32(a[1].split()[0])
         perm = [int(x) for x in re.search(r"quad_perm:\[(.*?)\]", a[1]).group(1).split(",")]
-        out = np.array([src[(l & ~3) + perm[l & 3]] for l in range(LANES)], dtype=np.uint64)
-        self.wv(self.vreg(a[0]), out)
+        idx = np.array([(l & ~3) + perm[l & 3] for l in range(LANES)])
+        self.wv(self.vreg(a[0]), src[idx])
 
     def op_v_lshlrev_b32(self, a):
         self.wv(self.vreg(a[0]), (self.src32(a[2]) << (self.src32(a[1]) & np.uint64(31))) & M32)
@@ -113,23 +140,55 @@ class Wave:
     def op_v_lshrrev_b32(self, a):
         self.wv(self.vreg(a[0]), self.src32(a[2]) >> (self.src32(a[1]) & np.uint64(31)))
 
+    def op_v_ashrrev_i32(self, a):
+        x = self.src32(a[2]).astype(np.int64)
+        x = np.where(x >= 2 ** 31, x - 2 ** 32, x)
+        self.wv(self.vreg(a[0]), (x >> (self.src32(a[1]).astype(np.int64) & 31)).astype(np.uint64) & M32)
+
     def op_v_lshlrev_b64(self, a):
         self.wv64(self.vpair(a[0]), self.src64(a[2]) << (self.src32(a[1]) & np.uint64(63)))
 
     def op_v_lshrrev_b64(self, a):
         self.wv64(self.vpair(a[0]), self.src64(a[2]) >> (self.src32(a[1]) & np.uint64(63)))
 
+    def op_v_add_u32(self, a):
+        self.wv(self.vreg(a[0]), (self.src32(a[1]) + self.src32(a[2])) & M32)
+
+    def op_v_subrev_u32(self, a):
+        self.wv(self.vreg(a[0]), (self.src32(a[2]) - self.src32(a[1])) & M32)
+
+    def op_v_and_b32(self, a):
+        self.wv(self.vreg(a[0]), self.src32(a[1]) & self.src32(a[2]))
+
+    def op_v_or_b32(self, a):
+        self.wv(self.vreg(a[0]), self.src32(a[1]) | self.src32(a[2]))
+
+    def op_v_xor_b32(self, a):
+        self.wv(self.vreg(a[0]), self.src32(a[1]) ^ self.src32(a[2]))
+
+    def op_v_mul_u32_u24(self, a):
+        x, y = self.src32(a[1]) & np.uint64(0xFFFFFF), self.src32(a[2]) & np.uint64(0xFFFFFF)
+        self.wv(self.vreg(a[0]), (x * y) & M32)
+
+    def op_v_bfe_u32(self, a):
+        x, off, w = self.src32(a[1]), self.src32(a[2]) & np.uint64(31), self.src32(a[3]) & np.uint64(31)
+        self.wv(self.vreg(a[0]), (x >> off) & ((np.uint64(1) << w) - np.uint64(1)))
+
+    def op_v_cmp_le_u32_e64(self, a):
+        self.set_mask(a[0], self.src32(a[1]) <= self.src32(a[2]))
+
     def op_v_mad_u64_u32(self, a):
         x, y, z = self.src32(a[2]), self.src32(a[3]), self.src64(a[4])
-        full = [int(x[l]) * int(y[l]) + int(z[l]) for l in range(LANES)]
-        self.wv64(self.vpair(a[0]), np.array([f & 0xFFFFFFFFFFFFFFFF for f in full], dtype=np.uint64))
-        self.set_mask(a[1], np.array([f >> 64 != 0 for f in full]))
+        prod = x * y
+        s = prod + z
+        self.wv64(self.vpair(a[0]), s)
+        self.set_mask(a[1], s < z)
 
     def _carry_op(self, a, fn):
-        x, y = self.src32(a[2]), self.src32(a[3])
-        cin = self.mask(a[4]).astype(np.uint64) if len(a) > 4 else np.zeros(LANES, dtype=np.uint64)
-        res, co = fn(x.astype(np.int64), y.astype(np.int64), cin.astype(np.int64))
-        self.wv(self.vreg(a[0]), (res.astype(np.uint64)) & M32)
+        x, y = self.src32(a[2]).astype(np.int64), self.src32(a[3]).astype(np.int64)
+        cin = self.mask(a[4]).astype(np.int64) if len(a) > 4 else np.zeros(LANES, dtype=np.int64)
+        res, co = fn(x, y, cin)
+        self.wv(self.vreg(a[0]), res.astype(np.uint64) & M32)
         self.set_mask(a[1], co)
 
     def op_v_add_co_u32_e64(self, a):
@@ -149,26 +208,27 @@ class Wave:
         self.wv(self.vreg(a[0]), np.where(m, self.src32(a[2]), self.src32(a[1])))
 
     # SALU
-    def op_s_mov_b32(self, a):
-        val = self.s_src(a[1])
-        if a[0] == "exec_lo":
-            for l in range(32):
-                self.exec[l] = bool((val >> l) & 1)
-        elif a[0] == "exec_hi":
-            for l in range(32):
-                self.exec[32 + l] = bool((val >> l) & 1)
-        else:
-            self.s[int(a[0][1:])] = np.uint64(val)
-
     def s_src(self, tok):
         m = re.fullmatch(r"s(\d+)", tok)
         if m:
             return int(self.s[int(m.group(1))])
         return int(tok, 0) & 0xFFFFFFFF
 
+    def s_set(self, tok, val):
+        self.s[int(tok[1:])] = np.uint64(val & 0xFFFFFFFF)
+
+    def op_s_mov_b32(self, a):
+        val = self.s_src(a[1])
+        if a[0] == "exec_lo":
+            self.exec[:32] = _bits(val)[:32]
+        elif a[0] == "exec_hi":
+            self.exec[32:] = _bits(val)[:32]
+        else:
+            self.s_set(a[0], val)
+
     def op_s_mov_b64(self, a):
         if a[1] == "exec":
-            word = sum(1 << l for l in range(LANES) if self.exec[l])
+            word = _word(self.exec)
             b = self.spair(a[0])
             self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
         elif a[0] == "exec":
@@ -177,80 +237,117 @@ class Wave:
             raise NotImplementedError(a)
 
     def op_s_or_b64(self, a):
-        m = self.mask(a[1]) | self.mask(a[2])
-        word = sum(1 << l for l in range(LANES) if m[l])
+        word = _word(self.mask(a[1]) | self.mask(a[2]))
         b = self.spair(a[0])
         self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
+        self.scc = int(word != 0)
 
     def op_s_add_u32(self, a):
         x = self.s_src(a[1]) + self.s_src(a[2])
-        self.s[int(a[0][1:])] = np.uint64(x & 0xFFFFFFFF)
+        self.s_set(a[0], x)
         self.scc = x >> 32
 
     def op_s_addc_u32(self, a):
         x = self.s_src(a[1]) + self.s_src(a[2]) + self.scc
-        self.s[int(a[0][1:])] = np.uint64(x & 0xFFFFFFFF)
+        self.s_set(a[0], x)
         self.scc = x >> 32
 
-    # memory
-    def _addr(self, voff, sbase, off):
-        b = self.spair(sbase)
-        base = int(self.s[b]) | (int(self.s[b + 1]) << 32)
-        return [base + int(voff[l]) + off for l in range(LANES)]
+    def op_s_sub_u32(self, a):
+        x = self.s_src(a[1]) - self.s_src(a[2])
+        self.s_set(a[0], x)
+        self.scc = int(x < 0)
 
+    def op_s_and_b32(self, a):
+        x = self.s_src(a[1]) & self.s_src(a[2])
+        self.s_set(a[0], x)
+        self.scc = int(x != 0)
+
+    def op_s_lshl_b32(self, a):
+        x = (self.s_src(a[1]) << (self.s_src(a[2]) & 31)) & 0xFFFFFFFF
+        self.s_set(a[0], x)
+        self.scc = int(x != 0)
+
+    def op_s_lshr_b32(self, a):
+        x = self.s_src(a[1]) >> (self.s_src(a[2]) & 31)
+        self.s_set(a[0], x)
+        self.scc = int(x != 0)
+
+    def op_s_cmp_eq_u32(self, a):
+        self.scc = int(self.s_src(a[0]) == self.s_src(a[1]))
+
+    def op_s_cbranch_scc1(self, a):
+        if self.scc:
+            self.pc = self.labels[a[0]]
+
+    def op_s_branch(self, a):
+        self.pc = self.labels[a[0]]
+
+    def op_s_barrier(self, a):
+        pass
+
+    def op_s_load_dwordx2(self, a):
+        b = self.spair(a[1])
+        addr = int(self.s[b]) | (int(self.s[b + 1]) << 32)
+        arr, i = self._mem(addr + int(a[2], 0))
+        val = int(arr[i])
+        d = self.spair(a[0])
+        self.s[d], self.s[d + 1] = np.uint64(val & 0xFFFFFFFF), np.uint64(val >> 32)
+
+    # memory
     def _mem(self, addr):
         for base, arr in self.mem.items():
             if base <= addr < base + arr.size * 8:
                 return arr, (addr - base) // 8
         raise IndexError(hex(addr))
 
-    def op_global_load_dwordx2(self, a):
-        parts = a[2].split()
+    def _gaddr(self, voff, tok):
+        parts = tok.split()
         off = int(parts[1].split(":")[1]) if len(parts) > 1 else 0
-        addrs = self._addr(self.src32(a[1]), parts[0], off)
-        vals = np.zeros(LANES, dtype=np.uint64)
-        for l in range(LANES):
-            if self.exec[l]:
-                arr, i = self._mem(addrs[l])
-                vals[l] = arr[i]
+        b = self.spair(parts[0])
+        base = int(self.s[b]) | (int(self.s[b + 1]) << 32)
+        addrs = voff.astype(np.uint64) + np.uint64(base + off)
+        lo = int(addrs[self.exec].min()) if self.exec.any() else base
+        arr, i0 = self._mem(lo)
+        region = lo - i0 * 8
+        idx = ((addrs - np.uint64(region)) // np.uint64(8)).astype(np.int64)
+        if self.exec.any() and int(idx[self.exec].max()) >= arr.size:
+            raise IndexError("global access crosses a region")
+        return arr, idx
+
+    def op_global_load_dwordx2(self, a):
+        arr, idx = self._gaddr(self.src32(a[1]), a[2])
+        vals = np.where(self.exec, arr[np.where(self.exec, idx, 0)], np.uint64(0))
         self.wv64(self.vpair(a[0]), vals)
 
     def op_global_store_dwordx2(self, a):
-        parts = a[2].split()
-        off = int(parts[1].split(":")[1]) if len(parts) > 1 else 0
-        addrs = self._addr(self.src32(a[0]), parts[0], off)
+        arr, idx = self._gaddr(self.src32(a[0]), a[2])
         vals = self.src64(a[1])
-        for l in range(LANES):
-            if self.exec[l]:
-                arr, i = self._mem(addrs[l])
-                arr[i] = vals[l]
+        arr[idx[self.exec]] = vals[self.exec]
 
     def op_ds_write_b64(self, a):
         parts = a[1].split()
         off = int(parts[1].split(":")[1]) if len(parts) > 1 else 0
-        addr = self.src32(a[0])
-        vals = self.src64(parts[0])
-        for l in range(LANES):
-            if self.exec[l]:
-                self.lds[(int(addr[l]) + off) // 8] = vals[l]
+        addr = (self.src32(a[0]) + np.uint64(off)).astype(np.int64)
+        if (addr[self.exec] % 8).any():
+            raise ValueError("unaligned ds_write_b64")
+        self.lds[addr[self.exec] // 8] = self.src64(parts[0])[self.exec]
 
     def op_ds_read_b64(self, a):
         parts = a[1].split()
         off = int(parts[1].split(":")[1]) if len(parts) > 1 else 0
-        addr = self.src32(parts[0])
-        vals = np.array([self.lds[(int(addr[l]) + off) // 8] for l in range(LANES)], dtype=np.uint64)
-        self.wv64(self.vpair(a[0]), vals)
+        addr = (self.src32(parts[0]) + np.uint64(off)).astype(np.int64)
+        self.wv64(self.vpair(a[0]), self.lds[np.where(self.exec, addr, 0) // 8])
 
 
-def body_lines(hdr, name):
+def body_lines(hdr, name, prefix="MI_TW_BODY_"):
     txt = open(hdr).read()
-    start = txt.index(f"#define MI_TW_BODY_{name.upper()}(")
+    start = txt.index(f"#define {prefix}{name.upper()}(")
     end = txt.index(":: __VA_ARGS__", start)
     return [m.group(1) for m in re.finditer(r'"(.*?)\\n"', txt[start:end])]
 
 
 def run_body(hdr, name, poly, twist_tab, fwd=True):
-    """Emulate one wave (wave 0 of a workgroup) on one polynomial."""
+    """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial."""
     data = np.array(poly, dtype=np.uint64).copy()
     tw = np.array(twist_tab, dtype=np.uint64)
     GB, TB = 0x100000000, 0x200000000
@@ -266,15 +363,45 @@ def run_body(hdr, name, poly, twist_tab, fwd=True):
     for k, (name_, val) in enumerate(vin.items()):
         w.v[200 + k] = val.astype(np.uint64)   # outside the body's v8..v127
         ops[name_] = f"v{200 + k}"
-    # lw: SGPR pair at s[100:101]
     lw = TB + 2048 * 8
     w.s[100], w.s[101] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
     ops["lw"] = "s[100:101]"
-    # the body writes s22:23 <- exec; 'ops' substitution
     w.ops = ops
-    w.scc = 0
     w.run(body_lines(hdr, name))
     return data
+
+
+def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
+    """Emulate the 2-wave workgroup of the blind-rotation body (tools/gen_pbs_kernel.py) on one LWE
+    ciphertext.  bsk: n x 2 x 2 x N NTT-domain key (N^-1 folded in), tab: the plan's twist tables
+    [fwd | lane-pair | inverse | lane-pair].  Returns the accumulator (2 x N) the body leaves in LDS."""
+    N = 2048
+    LB, UB, KB, TB = 0x100000000, 0x200000000, 0x300000000, 0x400000000
+    mem = {LB: np.array(lwe, dtype=np.uint64), UB: np.array(lut, dtype=np.uint64).reshape(-1),
+           KB: np.array(bsk, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
+    lds = np.zeros(2 * N, dtype=np.uint64)
+    lines = body_lines(hdr, name, "MI_PBS_BODY_")
+    waves = []
+    for w in range(2):
+        ops = {"lane": "v0", "S": str(w * N * 8), "SP": str((1 - w) * N * 8),
+               "lut_lo": str((UB + w * N * 8) & 0xFFFFFFFF), "lut_hi": str((UB + w * N * 8) >> 32),
+               "gown_lo": str((KB + 3 * w * N * 8) & 0xFFFFFFFF), "gown_hi": str((KB + 3 * w * N * 8) >> 32),
+               "gpar_lo": str((KB + (2 - w) * N * 8) & 0xFFFFFFFF), "gpar_hi": str((KB + (2 - w) * N * 8) >> 32),
+               "lwe_lo": str(LB & 0xFFFFFFFF), "lwe_hi": str(LB >> 32), "n": str(n_lwe),
+               "tab_lo": str(TB & 0xFFFFFFFF), "tab_hi": str(TB >> 32), "bl": str(base_log)}
+        wv = Wave(ops, mem, lds=lds)
+        wv.v[0] = np.arange(LANES, dtype=np.uint64)
+        wv.load(lines)
+        waves.append(wv.steps())
+    live = [True, True]
+    while any(live):
+        for k in range(2):
+            if live[k]:
+                try:
+                    next(waves[k])
+                except StopIteration:
+                    live[k] = False
+    return lds.reshape(2, N).copy()
 
 
 if __name__ == "__main__":

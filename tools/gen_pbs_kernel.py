@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Generate tfhe-rs-main_modified_amd/csrc/pbs_tw_body.hpp: the whole blind-rotation loop of the
+BNF programmable bootstrap (level 1) as ONE hand-scheduled gfx950 asm body per wave, built on the
+twisted transform cores of tools/gen_tw_kernel.py.
+
+Reference: tfhe/src/core_crypto/algorithms/lwe_programmable_bootstrapping/ntt64_bnf_pbs.rs:208-726
+(blind_rotate_ntt64_bnf_assign_mem_optimized -> cmux -> add_external_product_ntt64_bnf_assign).
+
+Work split: one workgroup = 2 waves = one LWE ciphertext.  Wave w owns GLWE polynomial w of the
+accumulator (32 coefficients per lane, W0 layout: element 64 r + lane in register pair r) for the
+whole loop, in v128..v191.  Per CMUX step i (a_i = ms(lwe[i]) != 0):
+  ROT     acc -> own LDS buffer; ct1[e] = +-acc[(e - a) mod N] - acc[e]     (monomial mul + cmux diff)
+  DECOMP  level-1 signed decomposition of ct1 (decomposer.rs:156-185, iter.rs:131-151), into [0, p)
+  FWD     twisted forward transform (fwd_core)
+  MAC     own transform -> own LDS buffer, barrier, partner's rows from its buffer:
+          y_w = x_w * G[w][w] + x_{1-w} * G[1-w][w] (mod p, canonical; key pre-multiplied by N^-1)
+  INV     twisted inverse transform (inv_core)
+  MS      q = v + floor((v EPS + p/2) / p) = v + v_hi + [v_lo EPS + p/2 - v_hi >= p]  (ntt64.rs:184-197)
+          acc += q (wrapping)
+The step's GGSW rows are prefetched (two 4-row chunks ahead) into v208..v239 while the rotation and
+the forward transform run.  At the end acc goes to the wave's LDS buffer in natural order; the C++
+wrapper (pbs_tw.hip) does the final rotation by -ms(b) and the sample extraction.
+
+Register map (the body owns v8..v255, s20..s31, s36..s93):
+  v8..v127 transform data + scratch, v128..v191 acc, v192..v195 lane*8 + 4096 m (row-group offsets),
+  v196..v203 per-lane LDS addresses of the transposes, v204 S, v205 partner exchange address,
+  v206 rotation offset, v207 0x7fffffff, v208..v239 GGSW prefetch, v240..v247 partner rows.
+
+Usage: python tools/gen_pbs_kernel.py > tfhe-rs-main_modified_amd/csrc/pbs_tw_body.hpp
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import gen_tw_kernel as T  # noqa: E402
+from gen_tw_kernel import (JUNK, SG0, Addr, Body, MulSlot, Seg, X, free_blocks_except, gmul,  # noqa: E402
+                           pv)
+
+ACC = 128
+VOFF = 192
+V_T1W, V_T1R, V_LWO, V_T2WL, V_T2WH, V_T2R, V_T4W, V_T4R = range(196, 204)
+V_S, V_PX, V_U8, V_HHI = 204, 205, 206, 207
+GBUF, PBUF = 208, 240
+
+S_SH, S_MASKB, S_BM1, S_HALF, S_K1, S_FULL = 26, 27, 28, 29, 30, 31
+S_TWF, S_TWI, S_GOWN, S_GPAR, S_LWE = 78, 80, 82, 84, 86
+S_CNT, S_AMS, S_A, S_R8, S_HLO = 88, 89, 90, 92, 93
+SGPR_CLOBBER = list(range(20, 32)) + list(range(36, 94))
+STEP_BYTES = 4 * 2048 * 8   # one level-1 GGSW (2 x 2 polynomials)
+
+
+def sp(b):
+    return f"s[{b}:{b + 1}]"
+
+
+def addr_for(tab):
+    return Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, v{VOFF + bt}, {sp(tab)} offset:{512 * k}",
+                t1w=f"v{V_T1W}", t1r=f"v{V_T1R}", t2wl=f"v{V_T2WL}", t2wh=f"v{V_T2WH}", t2r=f"v{V_T2R}",
+                t4w=f"v{V_T4W}", t4r=f"v{V_T4R}", lwo=f"v{V_LWO}", lw=sp(tab))
+
+
+FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
+
+
+def sched(B, sg):
+    for i, op in enumerate(sg.ops):
+        op.idx = i
+    B.out(sg.schedule())
+
+
+def prologue(B):
+    B.raw(f"s_mov_b64 s[{T.S_EXE}:{T.S_EXE + 1}], exec",
+          f"s_mov_b32 s{T.S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{T.S_PAR + 1}, 0xaaaaaaaa",
+          f"s_mov_b32 s{S_TWF}, %[tab_lo]", f"s_mov_b32 s{S_TWF + 1}, %[tab_hi]",
+          f"s_add_u32 s{S_TWI}, %[tab_lo], {2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0",
+          f"s_mov_b32 s{S_GOWN}, %[gown_lo]", f"s_mov_b32 s{S_GOWN + 1}, %[gown_hi]",
+          f"s_mov_b32 s{S_GPAR}, %[gpar_lo]", f"s_mov_b32 s{S_GPAR + 1}, %[gpar_hi]",
+          f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]",
+          f"s_mov_b32 s{S_CNT}, %[n]",
+          # base-log constants: 31 - B, 2^B - 1, B - 1, 2^(B-1), 2^32 - 2^B + 1
+          f"s_sub_u32 s{S_SH}, 31, %[bl]",
+          f"s_lshl_b32 s{S_HALF}, 1, %[bl]",
+          f"s_sub_u32 s{S_K1}, 1, s{S_HALF}",
+          f"s_add_u32 s{S_MASKB}, s{S_HALF}, -1",
+          f"s_sub_u32 s{S_BM1}, %[bl], 1",
+          f"s_lshr_b32 s{S_HALF}, s{S_HALF}, 1",
+          f"s_mov_b32 s{S_HLO}, 0x80000000",
+          f"s_mov_b32 s{S_A}, %[lut_lo]", f"s_mov_b32 s{S_A + 1}, %[lut_hi]",
+          # per-lane addresses
+          f"v_lshlrev_b32 v{VOFF}, 3, %[lane]",
+          f"v_add_u32 v{VOFF + 1}, 0x1000, v{VOFF}",
+          f"v_add_u32 v{VOFF + 2}, 0x2000, v{VOFF}",
+          f"v_add_u32 v{VOFF + 3}, 0x3000, v{VOFF}",
+          f"v_mov_b32 v{V_S}, %[S]",
+          f"v_add_u32 v{V_PX}, %[SP], v{VOFF}",
+          f"v_add_u32 v{V_T4R}, %[S], v{VOFF}",
+          f"v_mov_b32 v{V_HHI}, 0x7fffffff",
+          "v_and_b32 v8, 31, %[lane]", "v_lshlrev_b32 v8, 3, v8", f"v_add_u32 v{V_T1W}, %[S], v8",
+          "v_and_b32 v9, 1, %[lane]", "v_lshrrev_b32 v10, 1, %[lane]",
+          "v_mul_u32_u24 v11, 34, v10", "v_add_u32 v11, v11, v9", "v_lshlrev_b32 v11, 3, v11",
+          f"v_add_u32 v{V_T1R}, %[S], v11",
+          "v_and_b32 v12, 15, v10", "v_mul_u32_u24 v12, 0x42, v12",
+          "v_mul_u32_u24 v13, 33, v9", "v_add_u32 v13, v12, v13", "v_lshlrev_b32 v13, 3, v13",
+          f"v_add_u32 v{V_T2WL}, %[S], v13",
+          "v_mul_u32_u24 v14, 31, v9", "v_add_u32 v14, v12, v14", "v_add_u32 v14, 1, v14",
+          "v_lshlrev_b32 v14, 3, v14", f"v_add_u32 v{V_T2WH}, %[S], v14",
+          "v_lshrrev_b32 v15, 5, %[lane]", "v_xor_b32 v15, %[lane], v15", "v_lshlrev_b32 v15, 3, v15",
+          f"v_add_u32 v{V_T2R}, %[S], v15",
+          "v_add_u32 v16, v12, v9", "v_lshlrev_b32 v16, 3, v16", f"v_add_u32 v{V_T4W}, %[S], v16",
+          f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}")
+    # acc <- LUT polynomial of this wave
+    B.raw(*[f"global_load_dwordx2 {pv(ACC + 2 * r)}, v{VOFF + r // 8}, {sp(S_A)} offset:{512 * (r % 8)}"
+            for r in range(32)], "s_waitcnt vmcnt(0)")
+
+
+def gload(c):
+    """GGSW rows of MAC chunk c (rows 4c..4c+3) of this step into prefetch buffer c % 2."""
+    out = []
+    base = GBUF + 16 * (c % 2)
+    for k in range(4):
+        r = 4 * c + k
+        out.append(f"global_load_dwordx2 {pv(base + 2 * k)}, v{VOFF + r // 8}, {sp(S_GOWN)} offset:{512 * (r % 8)}")
+        out.append(f"global_load_dwordx2 {pv(base + 8 + 2 * k)}, v{VOFF + r // 8}, {sp(S_GPAR)} offset:{512 * (r % 8)}")
+    return out
+
+
+def slots_at(bases):
+    return [T.Slot(b, SG0 + 6 * i) for i, b in enumerate(bases)]
+
+
+def rotate_decompose(B):
+    """dmap v64..v127 <- decompose(+-acc[(e - a) mod N] - acc[e])."""
+    B.raw(f"s_and_b32 s{S_R8}, s{S_AMS}, 0x7ff", f"s_lshl_b32 s{S_R8}, s{S_R8}, 3",
+          f"s_lshr_b32 s{S_FULL}, s{S_AMS}, 11", f"s_sub_u32 s{S_FULL}, 0, s{S_FULL}",
+          f"v_subrev_u32 v{V_U8}, s{S_R8}, v{VOFF}")
+    B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(ACC + 2 * r)} offset:{512 * r}" for r in range(32)])
+    for h in range(2):
+        rows = list(range(16 * h, 16 * h + 16))
+        sg = Seg()
+        for q, r in enumerate(rows):
+            a = f"v{8 + q}"
+            sg.add(f"v_add_u32 {a}, {512 * r}, v{V_U8}", [f"v{V_U8}"], [a])
+            sg.add(f"v_and_b32 {a}, 0x3ff8, {a}", [a], [a])
+            sg.add(f"v_add_u32 {a}, %[S], {a}", [a], [a])
+        sched(B, sg)
+        B.raw(*[f"ds_read_b64 {pv(64 + 2 * r)}, v{8 + q}" for q, r in enumerate(rows)], "s_waitcnt lgkmcnt(0)")
+        sg = Seg()
+        sls = slots_at([8, 16, 24, 32, 40, 48, 56])
+        for q, r in enumerate(rows):
+            sl = sls[q % len(sls)]
+            v, c = sl.v, sl.c
+            xl, xh = f"v{64 + 2 * r}", f"v{65 + 2 * r}"
+            al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+            m = v[0]
+            sg.add(f"v_add_u32 {m}, {512 * r}, v{V_U8}", [f"v{V_U8}"], [m])
+            sg.add(f"v_ashrrev_i32 {m}, 31, {m}", [m], [m])
+            sg.add(f"v_xor_b32 {m}, s{S_FULL}, {m}", [m], [m])
+            sg.add(f"v_xor_b32 {xl}, {m}, {xl}", [m, xl], [xl])
+            sg.add(f"v_xor_b32 {xh}, {m}, {xh}", [m, xh], [xh])
+            sg.add(f"v_sub_co_u32_e64 {xl}, {c[0]}, {xl}, {m}", [xl, m], [xl, c[0]])
+            sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {m}, {c[0]}", [xh, m, c[0]], [xh, JUNK])
+            sg.add(f"v_sub_co_u32_e64 {xl}, {c[1]}, {xl}, {al}", [xl, al], [xl, c[1]])
+            sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {c[1]}", [xh, ah, c[1]], [xh, JUNK])
+            # level-1 signed decomposition (closest representable + one digit), mapped into [0, p)
+            t, res, u, w, ln, hn = v[1], v[2], v[3], v[4], v[5], v[6]
+            sg.add(f"v_lshrrev_b32 {t}, s{S_SH}, {xh}", [xh], [t])
+            sg.add(f"v_add_u32 {res}, 1, {t}", [t], [res])
+            sg.add(f"v_bfe_u32 {res}, {res}, 1, %[bl]", [res], [res])
+            sg.add(f"v_add_u32 {u}, -1, {res}", [res], [u])
+            sg.add(f"v_lshlrev_b32 {w}, s{S_BM1}, {t}", [t], [w])
+            sg.add(f"v_or_b32 {u}, {u}, {w}", [u, w], [u])
+            sg.add(f"v_and_b32 {u}, {u}, {res}", [u, res], [u])
+            sg.add(f"v_cmp_le_u32_e64 {c[2]}, s{S_HALF}, {u}", [u], [c[2]])
+            sg.add(f"v_add_co_u32_e64 {ln}, {c[0]}, s{S_K1}, {res}", [res], [ln, c[0]])
+            sg.add(f"v_addc_co_u32_e64 {hn}, {JUNK}, -2, 0, {c[0]}", [c[0]], [hn, JUNK])
+            sg.add(f"v_cndmask_b32_e64 {xl}, {res}, {ln}, {c[2]}", [res, ln, c[2]], [xl])
+            sg.add(f"v_cndmask_b32_e64 {xh}, 0, {hn}, {c[2]}", [hn, c[2]], [xh])
+        sched(B, sg)
+
+
+def add_canon(sg, m, a, b):
+    """a <- a + b mod p (both canonical), temps from multiply slot m."""
+    alo, ahi, _ = a
+    blo, bhi, _ = b
+    v, P, c = m.v, m.P, m.c
+    sg.add(f"v_add_co_u32_e64 {v[0]}, {c[0]}, {alo}, {blo}", [alo, blo], [v[0], c[0]])
+    sg.add(f"v_addc_co_u32_e64 {v[1]}, {c[1]}, {ahi}, {bhi}, {c[0]}", [ahi, bhi, c[0]], [v[1], c[1]])
+    sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, -1, 1, {P[0]}", [P[0]], [P[1], c[0]])
+    sg.add(f"s_or_b64 {c[0]}, {c[0]}, {c[1]}", [c[0], c[1]], [c[0], "scc"], "salu")
+    sg.add(f"v_cndmask_b32_e64 {alo}, {v[0]}, {v[2]}, {c[0]}", [v[0], v[2], c[0]], [alo])
+    sg.add(f"v_cndmask_b32_e64 {ahi}, {v[1]}, {v[3]}, {c[0]}", [v[1], v[3], c[0]], [ahi])
+
+
+def mac(B, dmap):
+    B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(dmap[r])} offset:{512 * r}" for r in range(32)],
+          "s_waitcnt lgkmcnt(0)", "s_barrier")
+    free = free_blocks_except(dmap)
+    regs = []
+    for b in free:
+        regs += list(range(b, b + 8))
+    ms = [MulSlot(regs[12 * i], SG0 + 6 * i) for i in range(4)]
+    for c in range(8):
+        B.raw(*[f"ds_read_b64 {pv(PBUF + 2 * k)}, v{V_PX} offset:{512 * (4 * c + k)}" for k in range(4)],
+              f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt(0)")
+        sg = Seg()
+        gb = GBUF + 16 * (c % 2)
+        for k in range(4):
+            r = 4 * c + k
+            m1, m2 = ms[(2 * k) % 4], ms[(2 * k + 1) % 4]
+            x = X(dmap, r)
+            pl, ph = f"v{PBUF + 2 * k}", f"v{PBUF + 2 * k + 1}"
+            gmul(sg, m1, x, f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}", x[0], x[1])
+            gmul(sg, m2, (pl, ph, pv(PBUF + 2 * k)), f"v{gb + 8 + 2 * k}", f"v{gb + 9 + 2 * k}", pl, ph)
+            add_canon(sg, m1, x, (pl, ph, pv(PBUF + 2 * k)))
+        sched(B, sg)
+        if c + 2 < 8:
+            B.raw(*gload(c + 2))
+    B.raw("s_barrier")
+
+
+def modswitch_acc(B, dmap):
+    sg = Seg()
+    sls = B.slots(free_blocks_except(dmap))
+    for r in range(32):
+        sl = sls[r % len(sls)]
+        v, P, c = sl.v, sl.P, sl.c
+        vl, vh, _ = X(dmap, r)
+        al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+        sg.add(f"v_sub_co_u32_e64 {v[0]}, {c[0]}, s{S_HLO}, {vh}", [vh], [v[0], c[0]])
+        sg.add(f"v_subb_co_u32_e64 {v[1]}, {JUNK}, v{V_HHI}, 0, {c[0]}", [c[0]], [v[1], JUNK])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[1]}, {vl}, -1, {P[0]}", [vl, P[0]], [P[1], c[1]])
+        sg.add(f"v_mad_u64_u32 {P[2]}, {c[2]}, -1, 1, {P[1]}", [P[1]], [P[2], c[2]])
+        sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[2]}", [c[1], c[2]], [c[1], "scc"], "salu")
+        sg.add(f"v_addc_co_u32_e64 {v[6]}, {c[2]}, {vl}, {vh}, {c[1]}", [vl, vh, c[1]], [v[6], c[2]])
+        sg.add(f"v_addc_co_u32_e64 {v[7]}, {JUNK}, {vh}, 0, {c[2]}", [vh, c[2]], [v[7], JUNK])
+        sg.add(f"v_add_co_u32_e64 {al}, {c[0]}, {al}, {v[6]}", [al, v[6]], [al, c[0]])
+        sg.add(f"v_addc_co_u32_e64 {ah}, {JUNK}, {ah}, {v[7]}, {c[0]}", [ah, v[7], c[0]], [ah, JUNK])
+    sched(B, sg)
+
+
+def gen_pbs(tabs):
+    B = Body(tabs)
+    prologue(B)
+    B.raw("Lpbs_top_%=:",
+          f"s_cmp_eq_u32 s{S_CNT}, 0",
+          "s_cbranch_scc1 Lpbs_end_%=",
+          f"s_load_dwordx2 {sp(S_A)}, {sp(S_LWE)}, 0x0",
+          f"s_add_u32 s{S_LWE}, s{S_LWE}, 8", f"s_addc_u32 s{S_LWE + 1}, s{S_LWE + 1}, 0",
+          f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
+          "s_waitcnt lgkmcnt(0)",
+          f"s_add_u32 s{S_AMS}, s{S_A + 1}, 0x80000",      # ms(a) = (a + 2^51) >> 52 (log_mod 12)
+          f"s_lshr_b32 s{S_AMS}, s{S_AMS}, 20",
+          f"s_cmp_eq_u32 s{S_AMS}, 0",
+          "s_cbranch_scc1 Lpbs_skip_%=")
+    B.raw(*gload(0), *gload(1))
+    rotate_decompose(B)
+    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
+    mac(B, dmap)
+    dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
+    modswitch_acc(B, dmap)
+    B.raw("Lpbs_skip_%=:",
+          f"s_add_u32 s{S_GOWN}, s{S_GOWN}, {STEP_BYTES}", f"s_addc_u32 s{S_GOWN + 1}, s{S_GOWN + 1}, 0",
+          f"s_add_u32 s{S_GPAR}, s{S_GPAR}, {STEP_BYTES}", f"s_addc_u32 s{S_GPAR + 1}, s{S_GPAR + 1}, 0",
+          "s_branch Lpbs_top_%=",
+          "Lpbs_end_%=:")
+    B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(ACC + 2 * r)} offset:{512 * r}" for r in range(32)],
+          "s_waitcnt lgkmcnt(0)")
+    return B
+
+
+def emit(name, body):
+    clob = [f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
+    return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
+            f"#define MI_PBS_BODY_{name.upper()}(...) asm volatile(\\\n" +
+            "\\\n".join(f'      "{l}\\n"' for l in body.lines) +
+            f"\\\n      :: __VA_ARGS__ \\\n      : {', '.join(clob)})\n")
+
+
+def main():
+    tabs = T.load_tables()
+    b = gen_pbs(tabs)
+    print("// GENERATED by tools/gen_pbs_kernel.py — do not edit.  Blind-rotation loop of the BNF PBS")
+    print("// (level 1) as one asm body per wave (pbs_tw.hip).  Owns v8..v255, s20..s31 + s36..s93, exec (restored).")
+    print("#pragma once")
+    print(emit("bnf_l1", b))
+    print(f"// pbs body {b.nvalu} VALU", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()

@@ -491,28 +491,42 @@ EXEC_HI = [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
 EXEC_ALL = [f"s_mov_b64 exec, s[{S_EXE}:{S_EXE + 1}]"]
 
 
-def t1(body, dmap, ybase, newhi):
+class Addr:
+    """Where the transform cores find their per-lane LDS addresses and tables: asm operand names in
+    the standalone transform kernel, fixed registers inside bigger bodies (tools/gen_pbs_kernel.py)."""
+
+    def __init__(self, tw_load, **regs):
+        self.tw_load = tw_load    # (batch bt, row k, dst pair base) -> load line of table row 8 bt + k
+        self.__dict__.update(regs)
+
+
+NTT_ADDR = Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] "
+                                   f"offset:{512 * k}",
+                **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw")})
+
+
+def t1(body, dmap, ybase, newhi, ad=NTT_ADDR):
     """W0 -> W1 (split by j half).  Returns the new dmap (x[q] in y for q < 16, x[16+q] at newhi)."""
     L = []
     L += [f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"]
     for r in range(32):
-        L.append(f"ds_write_b64 %[t1w], {pv(dmap[r])} offset:{r * 34 * 8}")
+        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * 34 * 8}")
     L += EXEC_ALL
     for q in range(16):
-        L.append(f"ds_read_b64 {pv(ybase + 2 * q)}, %[t1r] offset:{2 * q * 8}")
+        L.append(f"ds_read_b64 {pv(ybase + 2 * q)}, {ad.t1r} offset:{2 * q * 8}")
     L += [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
     for r in range(32):
-        L.append(f"ds_write_b64 %[t1w], {pv(dmap[r])} offset:{r * 34 * 8}")
+        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * 34 * 8}")
     L += EXEC_ALL
     L.append("s_waitcnt lgkmcnt(0)")
     for q in range(16):
-        L.append(f"ds_read_b64 {pv(newhi + 2 * q)}, %[t1r] offset:{2 * q * 8}")
+        L.append(f"ds_read_b64 {pv(newhi + 2 * q)}, {ad.t1r} offset:{2 * q * 8}")
     L.append("s_waitcnt lgkmcnt(0)")
     body.raw(*L)
     return [ybase + 2 * q for q in range(16)] + [newhi + 2 * q for q in range(16)]
 
 
-def t_iw0(body, dmap, pairs, ybase, newhi):
+def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
     """W1 (pairs=False) or W1' (pairs=True) -> W0, halves split by i (row stride 66)."""
     L = []
     for h in range(2):
@@ -521,16 +535,16 @@ def t_iw0(body, dmap, pairs, ybase, newhi):
         for k in range(32):
             if pairs:
                 if k < 16:
-                    L.append(f"ds_write_b64 %[t2wl], {pv(dmap[k])} offset:{2 * k * 8}")
+                    L.append(f"ds_write_b64 {ad.t2wl}, {pv(dmap[k])} offset:{2 * k * 8}")
                 else:
-                    L.append(f"ds_write_b64 %[t2wh], {pv(dmap[k])} offset:{2 * (k - 16) * 8}")
+                    L.append(f"ds_write_b64 {ad.t2wh}, {pv(dmap[k])} offset:{2 * (k - 16) * 8}")
             else:
-                L.append(f"ds_write_b64 %[t4w], {pv(dmap[k])} offset:{2 * k * 8}")
+                L.append(f"ds_write_b64 {ad.t4w}, {pv(dmap[k])} offset:{2 * k * 8}")
         L += EXEC_ALL
         if h == 1:
             L.append("s_waitcnt lgkmcnt(0)")
         dst = ybase if h == 0 else newhi
-        rb = "%[t2r]" if pairs else "%[t4r]"
+        rb = ad.t2r if pairs else ad.t4r
         for r in range(16):
             L.append(f"ds_read_b64 {pv(dst + 2 * r)}, {rb} offset:{r * 66 * 8}")
     L.append("s_waitcnt lgkmcnt(0)")
@@ -591,7 +605,7 @@ def slot_view(m, c23):
     return sl
 
 
-def pair_stage(B, dmap, fwd):
+def pair_stage(B, dmap, fwd, ad=NTT_ADDR):
     """Cyclic stage q = 5 on lane pairs: regroup W1 -> W1' (DPP), butterfly with the per-lane twiddle
     w_g, g = k + 16 (lane & 1), from the 32-entry table; forward: CT then canonical outputs (layout
     stays W1' for T2); inverse: GS then regroup back to W1."""
@@ -605,7 +619,7 @@ def pair_stage(B, dmap, fwd):
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
     for half in range(2):
         ks = list(range(8 * half, 8 * half + 8))
-        B.raw(*[f"global_load_dwordx2 {pv(wb[2 * i])}, %[lwo], %[lw] offset:{8 * k}" for i, k in enumerate(ks)],
+        B.raw(*[f"global_load_dwordx2 {pv(wb[2 * i])}, {ad.lwo}, {ad.lw} offset:{8 * k}" for i, k in enumerate(ks)],
               "s_waitcnt vmcnt(0)", "s_nop 1")
         sg = Seg()
         for i, k in enumerate(ks):
@@ -641,6 +655,37 @@ def store_raw(dmap):
     return store_rows(dmap, S_GB) + ["s_waitcnt vmcnt(0)"]
 
 
+def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
+    """Forward transform of the W0 data in dmap (must be v64..v127); returns the output dmap (W0,
+    canonical).  With `stop`, returns early (debug bodies)."""
+    fb = free_blocks_except(dmap)
+    for s in range(5):
+        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
+    if stop == "g1":
+        return dmap
+    # twist: 4 batches of 8 rows, table rows in v8..v23, 3 multiply slots in v24..v59
+    ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
+    for bt in range(4):
+        rows = list(range(8 * bt, 8 * bt + 8))
+        B.raw(*[ad.tw_load(bt, k, 8 + 2 * k) for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms)
+    if stop == "twist":
+        return dmap
+    dmap = t1(B, dmap, 8, 64, ad)
+    if stop == "t1":
+        return dmap
+    fb = free_blocks_except(dmap)
+    cf = [True] * 32  # twist outputs are canonical
+    for q in range(5):
+        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf)
+    if stop == "cyc":
+        return dmap
+    pair_stage(B, dmap, True, ad)
+    if stop == "last":
+        return dmap
+    return t_iw0(B, dmap, True, 96, 64, ad)
+
+
 def gen_fwd(tabs, stop=None):
     B = Body(tabs)
     dmap = [64 + 2 * r for r in range(32)]
@@ -648,52 +693,24 @@ def gen_fwd(tabs, stop=None):
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    fb = free_blocks_except(dmap)
-    for s in range(5):
-        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
-    if stop == "g1":
-        B.raw(*store_raw(dmap)); return B
-    # twist: 4 batches of 8 rows, table rows in v8..v23, 3 multiply slots in v24..v59
-    ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
-    for bt in range(4):
-        rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[f"global_load_dwordx2 {pv(8 + 2 * k)}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] offset:{512 * k}"
-                for k in range(8)], "s_waitcnt vmcnt(0)")
-        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms)
-    if stop == "twist":
-        B.raw(*store_raw(dmap)); return B
-    dmap = t1(B, dmap, 8, 64)
-    if stop == "t1":
-        B.raw(*store_raw(dmap)); return B
-    fb = free_blocks_except(dmap)
-    cf = [True] * 32  # twist outputs are canonical
-    for q in range(5):
-        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf)
-    if stop == "cyc":
-        B.raw(*store_raw(dmap)); return B
-    pair_stage(B, dmap, True)
-    if stop == "last":
-        B.raw(*store_raw(dmap)); return B
-    dmap = t_iw0(B, dmap, True, 96, 64)
+    dmap = fwd_core(B, tabs, dmap, stop=stop)
+    if stop:
+        B.raw(*store_raw(dmap))
+        return B
     B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     return B
 
 
-def gen_inv(tabs, stop=None):
-    B = Body(tabs)
-    dmap = [64 + 2 * r for r in range(32)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
-    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
-    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    dmap = t1(B, dmap, 8, 64)
-    pair_stage(B, dmap, False)
+def inv_core(B, tabs, dmap, ad=NTT_ADDR):
+    """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical)."""
+    dmap = t1(B, dmap, 8, 64, ad)
+    pair_stage(B, dmap, False, ad)
     fb = free_blocks_except(dmap)
     cf = [False] * 32
     for q in range(4, -1, -1):
         B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
-    dmap = t_iw0(B, dmap, False, 96, 64)
-    # untwist: table rows in v8..v23 are free? dmap now occupies v8..v39 (rows 0..15) and v64..v95
+    dmap = t_iw0(B, dmap, False, 96, 64, ad)
+    # untwist: table rows and multiply slots in the registers the data does not occupy
     free = free_blocks_except(dmap)
     regs = []
     for b in free:
@@ -701,8 +718,7 @@ def gen_inv(tabs, stop=None):
     ms = [MulSlot(regs[16 + 12 * i], SG0 + 6 * i) for i in range((len(regs) - 16) // 12)]
     for bt in range(4):
         rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[f"global_load_dwordx2 {pv(regs[2 * k])}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] "
-                f"offset:{512 * k}" for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.raw(*[ad.tw_load(bt, k, regs[2 * k]) for k in range(8)], "s_waitcnt vmcnt(0)")
         B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
@@ -715,6 +731,17 @@ def gen_inv(tabs, stop=None):
     for j, op in enumerate(sg.ops):
         op.idx = j
     B.out(sg.schedule())
+    return dmap
+
+
+def gen_inv(tabs, stop=None):
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    dmap = inv_core(B, tabs, dmap)
     B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     return B
 
