@@ -184,6 +184,14 @@ class Wave:
         self.wv64(self.vpair(a[0]), s)
         self.set_mask(a[1], s < z)
 
+    def op_v_mad_i64_i32(self, a):
+        x, y = self.src32(a[2]).astype(np.int64), self.src32(a[3]).astype(np.int64)
+        x = np.where(x >= 2 ** 31, x - 2 ** 32, x)
+        y = np.where(y >= 2 ** 31, y - 2 ** 32, y)
+        prod = (x * y).astype(np.uint64)          # |x y| < 2^62: exact, then two's complement
+        self.wv64(self.vpair(a[0]), prod + self.src64(a[4]))
+        self.set_mask(a[1], np.zeros(LANES, dtype=bool))  # overflow flag: unused (junk destination)
+
     def _carry_op(self, a, fn):
         x, y = self.src32(a[2]).astype(np.int64), self.src32(a[3]).astype(np.int64)
         cin = self.mask(a[4]).astype(np.int64) if len(a) > 4 else np.zeros(LANES, dtype=np.int64)

@@ -42,7 +42,7 @@ V_T1W, V_T1R, V_LWO, V_T2WL, V_T2WH, V_T2R, V_T4W, V_T4R = range(196, 204)
 V_S, V_PX, V_U8, V_HHI = 204, 205, 206, 207
 GBUF, PBUF = 208, 240
 
-S_SH, S_MASKB, S_BM1, S_HALF, S_K1, S_FULL = 26, 27, 28, 29, 30, 31
+S_SH, S_BM1, S_HALF, S_K1, S_FULL = 26, 28, 29, 30, 31   # s27: T.S_X15
 S_TWF, S_TWI, S_GOWN, S_GPAR, S_LWE = 78, 80, 82, 84, 86
 S_CNT, S_AMS, S_A, S_R8, S_HLO = 88, 89, 90, 92, 93
 SGPR_CLOBBER = list(range(20, 32)) + list(range(36, 94))
@@ -71,17 +71,17 @@ def sched(B, sg):
 def prologue(B):
     B.raw(f"s_mov_b64 s[{T.S_EXE}:{T.S_EXE + 1}], exec",
           f"s_mov_b32 s{T.S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{T.S_PAR + 1}, 0xaaaaaaaa",
+          f"s_mov_b32 s{T.S_X15}, 0x11111111",
           f"s_mov_b32 s{S_TWF}, %[tab_lo]", f"s_mov_b32 s{S_TWF + 1}, %[tab_hi]",
           f"s_add_u32 s{S_TWI}, %[tab_lo], {2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0",
           f"s_mov_b32 s{S_GOWN}, %[gown_lo]", f"s_mov_b32 s{S_GOWN + 1}, %[gown_hi]",
           f"s_mov_b32 s{S_GPAR}, %[gpar_lo]", f"s_mov_b32 s{S_GPAR + 1}, %[gpar_hi]",
           f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]",
           f"s_mov_b32 s{S_CNT}, %[n]",
-          # base-log constants: 31 - B, 2^B - 1, B - 1, 2^(B-1), 2^32 - 2^B + 1
+          # base-log constants: 31 - B, B - 1, 2^(B-1), 2^32 - 2^B + 1
           f"s_sub_u32 s{S_SH}, 31, %[bl]",
           f"s_lshl_b32 s{S_HALF}, 1, %[bl]",
           f"s_sub_u32 s{S_K1}, 1, s{S_HALF}",
-          f"s_add_u32 s{S_MASKB}, s{S_HALF}, -1",
           f"s_sub_u32 s{S_BM1}, %[bl], 1",
           f"s_lshr_b32 s{S_HALF}, s{S_HALF}, 1",
           f"s_mov_b32 s{S_HLO}, 0x80000000",

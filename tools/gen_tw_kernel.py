@@ -231,9 +231,9 @@ def tmul(sg, S, xlo, xhi, xp, sl, tlo, thi):
         sg.add(f"v_lshlrev_b32 {u}, {32 - K}, {xlo}", [xlo], [u])
     sg.add(f"v_mad_u64_u32 {P[1]}, {JUNK}, {u}, 1, {P[0]}", [u, P[0]], [P[1], JUNK])
     sg.add(f"v_sub_co_u32_e64 {v[3]}, {c[0]}, {v[3]}, {u}", [v[3], u], [v[3], c[0]])
-    sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -1, {c[0]}", [c[0]], [v[5]])
-    sg.add(f"v_addc_co_u32_e64 {tlo}, {c[1]}, {v[2]}, 0, {c[0]}", [v[2], c[0]], [tlo, c[1]])
-    sg.add(f"v_addc_co_u32_e64 {thi}, {JUNK}, {v[3]}, {v[5]}, {c[1]}", [v[3], v[5], c[1]], [thi, JUNK])
+    sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -15, {c[0]}", [c[0]], [v[5]])
+    tp = pair_of(tlo, thi)
+    sg.add(f"v_mad_i64_i32 {tp}, {JUNK}, {v[5]}, s{S_X15}, {P[1]}", [v[5], P[1]], [tp, tlo, thi, JUNK])
     return neg
 
 
@@ -249,13 +249,24 @@ def add_part2(sg, sl, dp):
     sg.add(f"v_mad_u64_u32 {dp}, {JUNK}, {v[5]}, 1, {P[0]}", [v[5], P[0]], [dp, JUNK])
 
 
+def pair_of(lo, hi):
+    a, b = int(lo[1:]), int(hi[1:])
+    assert b == a + 1 and a % 2 == 0, (lo, hi)
+    return pv(a)
+
+
+def minus_eps(sg, m, c, dp):
+    """dp <- dp - EPS where the SGPR mask c is set (a borrow: + p mod 2^64): m = c ? -15 : 0, then
+    dp += m * 0x11111111 (signed 32 x 32 + 64)."""
+    sg.add(f"v_cndmask_b32_e64 {m}, 0, -15, {c}", [c], [m])
+    sg.add(f"v_mad_i64_i32 {dp}, {JUNK}, {m}, s{S_X15}, {dp}", [m, dp], [dp, JUNK])
+
+
 def sub_seq(sg, sl, dlo, dhi, alo, ahi, tlo, thi):
     v, c = sl.v, sl.c
     sg.add(f"v_sub_co_u32_e64 {dlo}, {c[0]}, {alo}, {tlo}", [alo, tlo], [dlo, c[0]])
     sg.add(f"v_subb_co_u32_e64 {dhi}, {c[1]}, {ahi}, {thi}, {c[0]}", [ahi, thi, c[0]], [dhi, c[1]])
-    sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[1]}", [c[1]], [v[4]])
-    sg.add(f"v_addc_co_u32_e64 {dlo}, {c[0]}, {dlo}, 0, {c[1]}", [dlo, c[1]], [dlo, c[0]])
-    sg.add(f"v_addc_co_u32_e64 {dhi}, {JUNK}, {dhi}, {v[4]}, {c[0]}", [dhi, v[4], c[0]], [dhi, JUNK])
+    minus_eps(sg, v[4], c[1], pair_of(dlo, dhi))
 
 
 def ct_core(sg, sl, a, b, neg, tsrc=None):
@@ -352,9 +363,7 @@ def gmul(sg, ms, x, wlo, whi, olo, ohi):
     sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {C1}, 1, {PD}", [C1, PD], [PB, JUNK])          # H = D + C.hi
     sg.add(f"v_sub_co_u32_e64 {D0}, {c[0]}, {A0}, {B1}", [A0, B1], [D0, c[0]])          # T = L - H1
     sg.add(f"v_subb_co_u32_e64 {D1}, {c[1]}, {C0}, 0, {c[0]}", [C0, c[0]], [D1, c[1]])
-    sg.add(f"v_cndmask_b32_e64 {Z2l}, 0, -1, {c[1]}", [c[1]], [Z2l])
-    sg.add(f"v_sub_co_u32_e64 {D0}, {c[0]}, {D0}, {Z2l}", [D0, Z2l], [D0, c[0]])
-    sg.add(f"v_subb_co_u32_e64 {D1}, {JUNK}, {D1}, 0, {c[0]}", [D1, c[0]], [D1, JUNK])
+    minus_eps(sg, Z2l, c[1], PD)
     sg.add(f"v_mad_u64_u32 {PA}, {c[0]}, {B0}, -1, {PD}", [B0, PD], [PA, c[0]])         # R = T + H0 EPS
     sg.add(f"v_mad_u64_u32 {PC}, {c[1]}, -1, 1, {PA}", [PA], [PC, c[1]])                # U = R + EPS
     sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
@@ -452,6 +461,7 @@ def load_tables():
 S_GB = 78    # s[78:85]: data row-group bases g + 4096 m, m = 0..3
 S_TB = 86    # s[86:93]: table bases
 S_PAR = 20   # s[20:21]: odd-lane mask
+S_X15 = 27   # s27 = 0x11111111 = EPS / 15: d - EPS = d + (-15) * 0x11111111 in one v_mad_i64_i32
 S_EXE = 22   # s[22:23]: saved exec
 
 
@@ -689,7 +699,7 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
 def gen_fwd(tabs, stop=None):
     B = Body(tabs)
     dmap = [64 + 2 * r for r in range(32)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
@@ -737,7 +747,7 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR):
 def gen_inv(tabs, stop=None):
     B = Body(tabs)
     dmap = [64 + 2 * r for r in range(32)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec")
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
