@@ -49,3 +49,24 @@ def test_emulated_pbs_matches_oracle(oracle, seed, base_log):
     acc = asm_emu.run_pbs(HDR, lwe, lut, bsk_norm, tf + ti, base_log, n_lwe)
     got = _extract(acc, int(lwe[-1]), oracle)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("cmux", [False, True])
+def test_emulated_ext_product_matches_oracle(oracle, cmux):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_emu
+    plan, tf, ti = _tables(oracle)
+    n_inv = int(plan.n_inv)
+    ti_norm = [v * n_inv % P for v in ti[:N]] + ti[N:]
+    ctx = oracle.NttContext(N)
+    rnd = random.Random(7 + cmux)
+    ggsw = np.array([rnd.randrange(P) for _ in range(4 * N)], dtype=np.uint64)
+    glwe = np.array([rnd.getrandbits(64) for _ in range(2 * N)], dtype=np.uint64)
+    out = np.array([rnd.getrandbits(64) for _ in range(2 * N)], dtype=np.uint64)
+    g, o = asm_emu.run_ext(HDR, glwe, out, ggsw, tf + ti + ti_norm, 23, cmux)
+    if cmux:
+        want = ctx.cmux(out, glwe, ggsw, 1, 23, 1, bnf=True)
+        assert np.array_equal(g.reshape(-1), glwe - out)
+    else:
+        want = ctx.ext_product(out, ggsw, glwe, 1, 23, 1, bnf=True)
+    assert np.array_equal(o.reshape(-1), want)

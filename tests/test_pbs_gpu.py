@@ -53,9 +53,13 @@ def test_bsk_conversion(engine, plan, ctx, width, normalize):
     assert np.array_equal(host(d), want)
 
 
-@pytest.mark.parametrize("bnf", [True, False])
-@pytest.mark.parametrize("base_log,level", [(23, 1), (12, 2), (7, 3), (1, 1), (21, 3)])
-def test_external_product_parity(engine, plan, ctx, bnf, base_log, level):
+@pytest.mark.parametrize("bnf,kernel", [(True, "default"), (True, "generic"), (False, "default")])
+@pytest.mark.parametrize("base_log,level", [(23, 1), (12, 2), (7, 3), (1, 1), (21, 3), (31, 1)])
+def test_external_product_parity(engine, plan, ctx, monkeypatch, bnf, kernel, base_log, level):
+    """BNF level 1 (base_log <= 31) runs on the twisted-transform kernel by default (pbs_tw.hip);
+    'generic' forces pbs_kernels.hip (MI_PBS_VARIANT=0)."""
+    if kernel == "generic":
+        monkeypatch.setenv("MI_PBS_VARIANT", "0")
     q = 0 if bnf else P
     g = H.rng(base_log * 10 + level + 1000 * bnf)
     batch = 6
@@ -74,8 +78,10 @@ def test_external_product_parity(engine, plan, ctx, bnf, base_log, level):
     assert np.array_equal(host(tg), glwe)  # input untouched
 
 
-@pytest.mark.parametrize("bnf", [True, False])
-def test_cmux_parity(engine, plan, ctx, bnf):
+@pytest.mark.parametrize("bnf,kernel", [(True, "default"), (True, "generic"), (False, "default")])
+def test_cmux_parity(engine, plan, ctx, monkeypatch, bnf, kernel):
+    if kernel == "generic":
+        monkeypatch.setenv("MI_PBS_VARIANT", "0")
     q = 0 if bnf else P
     g = H.rng(7 + bnf)
     batch, base_log, level = 5, 23, 1

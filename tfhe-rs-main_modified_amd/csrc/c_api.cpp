@@ -200,10 +200,15 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
           b = mi::host::mul_mod(b, rho_inv, p);
         }
       }
-      // one allocation [fwd | inverse] (the PBS body addresses both from one base, pbs_tw.hip)
-      if (hipMalloc(&plan->d_twist_f, 2 * (n + 32) * sizeof(u64)) == hipSuccess &&
+      // one allocation [fwd | inverse | inverse with N^-1 folded into the untwist rows]; the PBS /
+      // external-product bodies address all three from one base (pbs_tw.hip)
+      std::vector<u64> tn(ti);
+      for (unsigned e = 0; e < n; ++e) tn[e] = mi::host::mul_mod(ti[e], plan->n_inv, p);
+      if (hipMalloc(&plan->d_twist_f, 3 * (n + 32) * sizeof(u64)) == hipSuccess &&
           hipMemcpy(plan->d_twist_f, tf.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess &&
           hipMemcpy(plan->d_twist_f + n + 32, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
+              hipSuccess &&
+          hipMemcpy(plan->d_twist_f + 2 * (n + 32), tn.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
               hipSuccess) {
         plan->d_twist_i = plan->d_twist_f + n + 32;
       } else {
@@ -360,6 +365,12 @@ static int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int l
   return MI_OK;
 }
 
+// the twisted-transform bodies (pbs_tw.hip) cover BNF, level 1, base_log <= 31 on the Solinas N = 2048
+// plan; MI_PBS_VARIANT=0 forces the generic kernels
+static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int base_log, int level) {
+  return variant == MI_NTT64_BNF && level == 1 && base_log <= 31 && plan->d_twist_f && env_pbs_variant() != 0;
+}
+
 int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
                     unsigned in_modulus_width, int normalize, void* stream) {
   if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
@@ -383,6 +394,11 @@ int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, co
   if (!out_glwe || !in_glwe || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
+  if (twisted_ext_applies(plan, variant, base_log, level)) {
+    hipError_t e = mi::launch_ext_tw(false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_ntt, batch, base_log,
+                                     plan->d_twist_f, (hipStream_t)stream);
+    return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
+  }
   hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
                                         ggsw_ntt, batch, base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv,
                                         (hipStream_t)stream);
@@ -397,6 +413,10 @@ int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1,
   if (!ct0 || !ct1 || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
+  if (twisted_ext_applies(plan, variant, base_log, level)) {
+    hipError_t e = mi::launch_ext_tw(true, ct0, ct1, ggsw_ntt, batch, base_log, plan->d_twist_f, (hipStream_t)stream);
+    return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
+  }
   hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
                                         plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
@@ -460,8 +480,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   const mi_ntt64_plan* plan = key->plan;
   DeviceGuard g(plan->device);
-  if (key->variant == MI_NTT64_BNF && key->level == 1 && key->base_log <= 31 && plan->d_twist_f &&
-      env_pbs_variant() != 0) {
+  if (twisted_ext_applies(plan, key->variant, key->base_log, key->level)) {
     hipError_t e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
                                      plan->d_twist_f, ms_mode == MI_MS_CENTERED, (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");

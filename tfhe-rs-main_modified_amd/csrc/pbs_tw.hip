@@ -55,7 +55,7 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
 }
 
 // lwe_in: batch x (n+1); lut: 2 x N; bsk: n x 2 x 2 x N (NTT domain, N^-1 folded in);
-// tab: [fwd twist (N) | fwd lane-pair twiddles (32) | inverse twist (N) | inverse lane-pair (32)].
+// tab: [fwd twist (N) | fwd lane-pair twiddles (32) | inverse twist (N) | inverse lane-pair (32) | ...].
 __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                                      const u64* __restrict__ lut, const u64* __restrict__ bsk,
                                                      uint32_t n_lwe, uint32_t batch, int base_log,
@@ -105,7 +105,52 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   }
 }
 
+// external product / CMUX batch (config 3): one workgroup per GLWE pair, wave w on polynomial w
+template <bool CMUX>
+__global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                     const u64* __restrict__ ggsw, uint32_t batch, int base_log,
+                                                     const u64* __restrict__ tab) {
+  __shared__ u64 buf[2 * N];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;
+  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
+  u64* o = out + ((size_t)b * 2 + w) * N;
+  u64* g = glwe + ((size_t)b * 2 + w) * N;
+  const u64* gown = ggsw + (size_t)3 * w * N;
+  const u64* gpar = ggsw + (size_t)(2 - w) * N;
+  const uint32_t o_lo = (uint32_t)(uintptr_t)o, o_hi = (uint32_t)((uintptr_t)o >> 32);
+  const uint32_t g_lo = (uint32_t)(uintptr_t)g, g_hi = (uint32_t)((uintptr_t)g >> 32);
+  const uint32_t gown_lo = (uint32_t)(uintptr_t)gown, gown_hi = (uint32_t)((uintptr_t)gown >> 32);
+  const uint32_t gpar_lo = (uint32_t)(uintptr_t)gpar, gpar_hi = (uint32_t)((uintptr_t)gpar >> 32);
+  const uint32_t tab_lo = (uint32_t)(uintptr_t)tab, tab_hi = (uint32_t)((uintptr_t)tab >> 32);
+  if constexpr (CMUX)
+    MI_PBS_BODY_CMUX_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
+                            [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
+                            [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
+                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log));
+  else
+    MI_PBS_BODY_EXT_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
+                           [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
+                           [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
+                           [tab_hi] "s"(tab_hi), [bl] "s"(base_log));
+}
+
 }  // namespace pbstw
+
+hipError_t launch_ext_tw(bool cmux, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch, int base_log,
+                         const uint64_t* tab, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
+  if (cmux)
+    hipLaunchKernelGGL(pbstw::ext_tw_kernel<true>, dim3((unsigned)batch), dim3(128), 0, s, out, glwe, ggsw,
+                       (uint32_t)batch, base_log, tab);
+  else
+    hipLaunchKernelGGL(pbstw::ext_tw_kernel<false>, dim3((unsigned)batch), dim3(128), 0, s, out, glwe, ggsw,
+                       (uint32_t)batch, base_log, tab);
+  return hipGetLastError();
+}
 
 hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const uint64_t* bsk, size_t n_lwe,
                          size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s) {

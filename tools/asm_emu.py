@@ -412,6 +412,41 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
     return lds.reshape(2, N).copy()
 
 
+def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
+    """Emulate the 2-wave external-product / CMUX body on one GLWE pair (glwe, out: 2 x N, updated
+    in place and returned); ggsw: 2 x 2 x N Raw NTT key; tab: [fwd | inverse | inverse * N^-1]."""
+    N = 2048
+    GB, OB, KB, TB = 0x100000000, 0x200000000, 0x300000000, 0x400000000
+    g = np.array(glwe, dtype=np.uint64).reshape(-1).copy()
+    o = np.array(out, dtype=np.uint64).reshape(-1).copy()
+    mem = {GB: g, OB: o, KB: np.array(ggsw, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
+    lds = np.zeros(2 * N, dtype=np.uint64)
+    lines = body_lines(hdr, "cmux_bnf_l1" if cmux else "ext_bnf_l1", "MI_PBS_BODY_")
+    waves = []
+    for w in range(2):
+        lo = lambda a: str(a & 0xFFFFFFFF)
+        hi = lambda a: str(a >> 32)
+        ops = {"lane": "v0", "S": str(w * N * 8), "SP": str((1 - w) * N * 8),
+               "glwe_lo": lo(GB + w * N * 8), "glwe_hi": hi(GB + w * N * 8),
+               "out_lo": lo(OB + w * N * 8), "out_hi": hi(OB + w * N * 8),
+               "gown_lo": lo(KB + 3 * w * N * 8), "gown_hi": hi(KB + 3 * w * N * 8),
+               "gpar_lo": lo(KB + (2 - w) * N * 8), "gpar_hi": hi(KB + (2 - w) * N * 8),
+               "tab_lo": lo(TB), "tab_hi": hi(TB), "bl": str(base_log)}
+        wv = Wave(ops, mem, lds=lds)
+        wv.v[0] = np.arange(LANES, dtype=np.uint64)
+        wv.load(lines)
+        waves.append(wv.steps())
+    live = [True, True]
+    while any(live):
+        for k in range(2):
+            if live[k]:
+                try:
+                    next(waves[k])
+                except StopIteration:
+                    live[k] = False
+    return g.reshape(2, N), o.reshape(2, N)
+
+
 if __name__ == "__main__":
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
     import random

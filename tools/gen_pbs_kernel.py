@@ -76,8 +76,6 @@ def prologue(B):
           f"s_add_u32 s{S_TWI}, %[tab_lo], {2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0",
           f"s_mov_b32 s{S_GOWN}, %[gown_lo]", f"s_mov_b32 s{S_GOWN + 1}, %[gown_hi]",
           f"s_mov_b32 s{S_GPAR}, %[gpar_lo]", f"s_mov_b32 s{S_GPAR + 1}, %[gpar_hi]",
-          f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]",
-          f"s_mov_b32 s{S_CNT}, %[n]",
           # base-log constants: 31 - B, B - 1, 2^(B-1), 2^32 - 2^B + 1
           f"s_sub_u32 s{S_SH}, 31, %[bl]",
           f"s_lshl_b32 s{S_HALF}, 1, %[bl]",
@@ -85,7 +83,6 @@ def prologue(B):
           f"s_sub_u32 s{S_BM1}, %[bl], 1",
           f"s_lshr_b32 s{S_HALF}, s{S_HALF}, 1",
           f"s_mov_b32 s{S_HLO}, 0x80000000",
-          f"s_mov_b32 s{S_A}, %[lut_lo]", f"s_mov_b32 s{S_A + 1}, %[lut_hi]",
           # per-lane addresses
           f"v_lshlrev_b32 v{VOFF}, 3, %[lane]",
           f"v_add_u32 v{VOFF + 1}, 0x1000, v{VOFF}",
@@ -108,9 +105,16 @@ def prologue(B):
           f"v_add_u32 v{V_T2R}, %[S], v15",
           "v_add_u32 v16, v12, v9", "v_lshlrev_b32 v16, 3, v16", f"v_add_u32 v{V_T4W}, %[S], v16",
           f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}")
-    # acc <- LUT polynomial of this wave
-    B.raw(*[f"global_load_dwordx2 {pv(ACC + 2 * r)}, v{VOFF + r // 8}, {sp(S_A)} offset:{512 * (r % 8)}"
-            for r in range(32)], "s_waitcnt vmcnt(0)")
+
+
+def load_rows(dst, base):
+    return [f"global_load_dwordx2 {pv(dst + 2 * r)}, v{VOFF + r // 8}, {sp(base)} offset:{512 * (r % 8)}"
+            for r in range(32)]
+
+
+def store_rows(src, base):
+    return [f"global_store_dwordx2 v{VOFF + r // 8}, {pv(src + 2 * r)}, {sp(base)} offset:{512 * (r % 8)}"
+            for r in range(32)]
 
 
 def gload(c):
@@ -126,6 +130,27 @@ def gload(c):
 
 def slots_at(bases):
     return [T.Slot(b, SG0 + 6 * i) for i, b in enumerate(bases)]
+
+
+def decompose(sg, sl, xl, xh):
+    """Level-1 signed decomposition of the native u64 (xl, xh) in place (closest representable +
+    one balanced digit, decomposer.rs:156-185 + iter.rs:131-151), mapped into [0, p) (ntt64.rs:231-238).
+    With one level the digit equals the balanced state: res = round(x / 2^(64-B)) mod 2^B, minus 2^B
+    when the balancing bit is set."""
+    v, c = sl.v, sl.c
+    t, res, u, w, ln, hn = v[1], v[2], v[3], v[4], v[5], v[6]
+    sg.add(f"v_lshrrev_b32 {t}, s{S_SH}, {xh}", [xh], [t])
+    sg.add(f"v_add_u32 {res}, 1, {t}", [t], [res])
+    sg.add(f"v_bfe_u32 {res}, {res}, 1, %[bl]", [res], [res])
+    sg.add(f"v_add_u32 {u}, -1, {res}", [res], [u])
+    sg.add(f"v_lshlrev_b32 {w}, s{S_BM1}, {t}", [t], [w])
+    sg.add(f"v_or_b32 {u}, {u}, {w}", [u, w], [u])
+    sg.add(f"v_and_b32 {u}, {u}, {res}", [u, res], [u])
+    sg.add(f"v_cmp_le_u32_e64 {c[2]}, s{S_HALF}, {u}", [u], [c[2]])
+    sg.add(f"v_add_co_u32_e64 {ln}, {c[0]}, s{S_K1}, {res}", [res], [ln, c[0]])
+    sg.add(f"v_addc_co_u32_e64 {hn}, {JUNK}, -2, 0, {c[0]}", [c[0]], [hn, JUNK])
+    sg.add(f"v_cndmask_b32_e64 {xl}, {res}, {ln}, {c[2]}", [res, ln, c[2]], [xl])
+    sg.add(f"v_cndmask_b32_e64 {xh}, 0, {hn}, {c[2]}", [hn, c[2]], [xh])
 
 
 def rotate_decompose(B):
@@ -161,20 +186,7 @@ def rotate_decompose(B):
             sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {m}, {c[0]}", [xh, m, c[0]], [xh, JUNK])
             sg.add(f"v_sub_co_u32_e64 {xl}, {c[1]}, {xl}, {al}", [xl, al], [xl, c[1]])
             sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {c[1]}", [xh, ah, c[1]], [xh, JUNK])
-            # level-1 signed decomposition (closest representable + one digit), mapped into [0, p)
-            t, res, u, w, ln, hn = v[1], v[2], v[3], v[4], v[5], v[6]
-            sg.add(f"v_lshrrev_b32 {t}, s{S_SH}, {xh}", [xh], [t])
-            sg.add(f"v_add_u32 {res}, 1, {t}", [t], [res])
-            sg.add(f"v_bfe_u32 {res}, {res}, 1, %[bl]", [res], [res])
-            sg.add(f"v_add_u32 {u}, -1, {res}", [res], [u])
-            sg.add(f"v_lshlrev_b32 {w}, s{S_BM1}, {t}", [t], [w])
-            sg.add(f"v_or_b32 {u}, {u}, {w}", [u, w], [u])
-            sg.add(f"v_and_b32 {u}, {u}, {res}", [u, res], [u])
-            sg.add(f"v_cmp_le_u32_e64 {c[2]}, s{S_HALF}, {u}", [u], [c[2]])
-            sg.add(f"v_add_co_u32_e64 {ln}, {c[0]}, s{S_K1}, {res}", [res], [ln, c[0]])
-            sg.add(f"v_addc_co_u32_e64 {hn}, {JUNK}, -2, 0, {c[0]}", [c[0]], [hn, JUNK])
-            sg.add(f"v_cndmask_b32_e64 {xl}, {res}, {ln}, {c[2]}", [res, ln, c[2]], [xl])
-            sg.add(f"v_cndmask_b32_e64 {xh}, 0, {hn}, {c[2]}", [hn, c[2]], [xh])
+            decompose(sg, sl, xl, xh)
         sched(B, sg)
 
 
@@ -241,6 +253,9 @@ def modswitch_acc(B, dmap):
 def gen_pbs(tabs):
     B = Body(tabs)
     prologue(B)
+    B.raw(f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]", f"s_mov_b32 s{S_CNT}, %[n]",
+          f"s_mov_b32 s{S_A}, %[lut_lo]", f"s_mov_b32 s{S_A + 1}, %[lut_hi]")
+    B.raw(*load_rows(ACC, S_A), "s_waitcnt vmcnt(0)")    # acc <- LUT polynomial of this wave
     B.raw("Lpbs_top_%=:",
           f"s_cmp_eq_u32 s{S_CNT}, 0",
           "s_cbranch_scc1 Lpbs_end_%=",
@@ -268,6 +283,41 @@ def gen_pbs(tabs):
     return B
 
 
+def gen_ext(tabs, cmux):
+    """One external product (cmux=False: out += GGSW . glwe) or CMUX (glwe -= out, then
+    out += GGSW . glwe), BNF, level 1; wave w handles polynomial w of one GLWE pair."""
+    B = Body(tabs)
+    prologue(B)
+    S_GL, S_OUT = S_LWE, S_A
+    # the GGSW is the reference's Raw NTT key: N^-1 comes from the third table (untwist * N^-1)
+    B.raw(f"s_add_u32 s{S_TWI}, %[tab_lo], {2 * 2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0")
+    B.raw(f"s_mov_b32 s{S_GL}, %[glwe_lo]", f"s_mov_b32 s{S_GL + 1}, %[glwe_hi]",
+          f"s_mov_b32 s{S_OUT}, %[out_lo]", f"s_mov_b32 s{S_OUT + 1}, %[out_hi]")
+    B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
+    sg = Seg()
+    sls = slots_at([8, 16, 24, 32, 40, 48, 56])
+    for r in range(32):
+        sl = sls[r % len(sls)]
+        xl, xh = f"v{64 + 2 * r}", f"v{65 + 2 * r}"
+        if cmux:  # ct1 -= ct0 (ntt64_bnf_pbs.rs:683-705, wrapping)
+            al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+            sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[1]}, {xl}, {al}", [xl, al], [xl, sl.c[1]])
+            sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {sl.c[1]}", [xh, ah, sl.c[1]], [xh, JUNK])
+    sched(B, sg)
+    if cmux:
+        B.raw(*store_rows(64, S_GL))
+    sg = Seg()
+    for r in range(32):
+        decompose(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}")
+    sched(B, sg)
+    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
+    mac(B, dmap)
+    dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
+    modswitch_acc(B, dmap)
+    B.raw(*store_rows(ACC, S_OUT), "s_waitcnt vmcnt(0)")
+    return B
+
+
 def emit(name, body):
     clob = [f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
@@ -279,11 +329,14 @@ def emit(name, body):
 def main():
     tabs = T.load_tables()
     b = gen_pbs(tabs)
-    print("// GENERATED by tools/gen_pbs_kernel.py — do not edit.  Blind-rotation loop of the BNF PBS")
-    print("// (level 1) as one asm body per wave (pbs_tw.hip).  Owns v8..v255, s20..s31 + s36..s93, exec (restored).")
+    print("// GENERATED by tools/gen_pbs_kernel.py — do not edit.  BNF level-1 blind-rotation loop, external")
+    print("// product and CMUX as asm bodies per wave (pbs_tw.hip).  Own v8..v255, s20..s31 + s36..s93, exec (restored).")
     print("#pragma once")
     print(emit("bnf_l1", b))
-    print(f"// pbs body {b.nvalu} VALU", file=sys.stderr)
+    e, c = gen_ext(tabs, False), gen_ext(tabs, True)
+    print(emit("ext_bnf_l1", e))
+    print(emit("cmux_bnf_l1", c))
+    print(f"// pbs step {b.nvalu} VALU, ext {e.nvalu}, cmux {c.nvalu}", file=sys.stderr)
 
 
 if __name__ == "__main__":
