@@ -263,24 +263,32 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(K):
-        ev[k][0].record()
         plan.fwd(buf)
-        ev[k][1].record()
         plan.inv(buf)
-        ev[k][2].record()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = eng.multi_gpu.max_over_ranks(elapsed, dev)
 
-    fwd_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / K
-    inv_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / K
+    # per-kernel durations, outside the timed loop: HIP events around K back-to-back launches of one
+    # kernel (an event between every launch would add its own ~6-10 us barrier to each interval).
+    # The plan launches on torch's current stream, which is what these events record on.
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record()
+    for k in range(K):
+        plan.fwd(buf)
+    e1.record()
+    for k in range(K):
+        plan.inv(buf)
+    e2.record()
+    torch.cuda.synchronize()
+    fwd_ms = e0.elapsed_time(e1) / K
+    inv_ms = e1.elapsed_time(e2) / K
     dom_ms = max(fwd_ms, inv_ms)
     dom = "fwd" if fwd_ms >= inv_ms else "inv"
     bytes_launch = batch * BYTES_PER_POLY_PASS
