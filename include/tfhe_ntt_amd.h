@@ -138,6 +138,54 @@ int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key *key);
 int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
 
+/* ---- prime32::Plan (tfhe-ntt/src/prime32.rs:632-1025) ----------------------------------------
+ * The same negacyclic transform and pointwise ops on u32 buffers for a prime p < 2^32.  try_new
+ * (prime32.rs:662-671) returns None for N < 32, N not a power of two, p not prime, no 2N-th root:
+ * here MI_ERR_INVALID_ARG / MI_ERR_NOT_PRIME / MI_ERR_NO_ROOT.  Twiddles follow
+ * init_negacyclic_twiddles (prime32.rs:223-246), outputs are canonical (< p) as the reference's
+ * tests assert (prime32.rs:1114-1133). */
+typedef struct mi_ntt32_plan mi_ntt32_plan;
+int mi_ntt32_plan_create(size_t n, uint32_t p, int device, mi_ntt32_plan **out_plan);
+int mi_ntt32_plan_destroy(mi_ntt32_plan *plan);
+int mi_ntt32_plan_info(const mi_ntt32_plan *plan, size_t *n, uint32_t *p, int *device);
+/* Plan::fwd / Plan::inv (prime32.rs:797-898) */
+int mi_ntt32_fwd_batch(const mi_ntt32_plan *plan, uint32_t *buf, size_t batch, size_t stride, void *stream);
+int mi_ntt32_inv_batch(const mi_ntt32_plan *plan, uint32_t *buf, size_t batch, size_t stride, void *stream);
+/* Plan::normalize / mul_assign_normalize / mul_accumulate (prime32.rs:900-1025) */
+int mi_ntt32_normalize_batch(const mi_ntt32_plan *plan, uint32_t *buf, size_t batch, size_t stride, void *stream);
+int mi_ntt32_mul_assign_normalize_batch(const mi_ntt32_plan *plan, uint32_t *lhs, const uint32_t *rhs,
+                                        size_t batch, size_t stride, void *stream);
+int mi_ntt32_mul_accumulate_batch(const mi_ntt32_plan *plan, uint32_t *acc, const uint32_t *lhs,
+                                  const uint32_t *rhs, size_t batch, size_t stride, void *stream);
+
+/* ---- Exact native-modulus negacyclic products over a CRT of NTT primes ----------------------
+ * negacyclic_polymul of native32.rs:410-500, native64.rs:1041-1160, native128.rs:297-320 and the
+ * binary-RHS plans native_binary{32,64,128}.rs (rhs coefficients in {0,1}): prod = lhs * rhs in
+ * Z_{2^W}[X]/(X^N + 1), W = 32 / 64 / 128 (u128 = two little-endian u64 words).  The prime sets are
+ * the reference's (lib.rs primes32 / primes52).  Plan52 kinds exist in the reference only on CPUs
+ * with AVX-512 IFMA (their try_new returns None otherwise); here they always exist. */
+typedef enum mi_native_kind {
+    MI_NATIVE32_PLAN32 = 0,        /* native32::Plan32           P0..P2 (32-bit)  */
+    MI_NATIVE32_PLAN52 = 1,        /* native32::Plan52           P0..P1 (52-bit)  */
+    MI_NATIVE64_PLAN32 = 2,        /* native64::Plan32           P0..P4 (32-bit)  */
+    MI_NATIVE64_PLAN52 = 3,        /* native64::Plan52           P0..P2 (52-bit)  */
+    MI_NATIVE128_PLAN32 = 4,       /* native128::Plan32          P0..P9 (32-bit)  */
+    MI_NATIVE_BINARY32_PLAN32 = 5, /* native_binary32::Plan32    P0..P1 (32-bit)  */
+    MI_NATIVE_BINARY32_PLAN52 = 6, /* native_binary32::Plan52    P0     (52-bit)  */
+    MI_NATIVE_BINARY64_PLAN32 = 7, /* native_binary64::Plan32    P0..P2 (32-bit)  */
+    MI_NATIVE_BINARY64_PLAN52 = 8, /* native_binary64::Plan52    P0..P1 (52-bit)  */
+    MI_NATIVE_BINARY128_PLAN32 = 9 /* native_binary128::Plan32   P0..P4 (32-bit)  */
+} mi_native_kind;
+typedef struct mi_native_plan mi_native_plan;
+/* Plan32/Plan52::try_new(n) (e.g. native64.rs:932-941): None when a component prime plan is. */
+int mi_native_plan_create(int kind, size_t n, int device, mi_native_plan **out_plan);
+int mi_native_plan_destroy(mi_native_plan *plan);
+int mi_native_plan_info(const mi_native_plan *plan, size_t *n, int *width_bits, int *num_primes);
+/* Batched negacyclic_polymul: `batch` contiguous polynomials of n words each in prod/lhs/rhs
+ * (device pointers, async on `stream`; scratch is stream-ordered and freed before return). */
+int mi_native_polymul_batch(const mi_native_plan *plan, void *prod, const void *lhs, const void *rhs, size_t batch,
+                            void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -491,4 +491,217 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
 }
 
+// ---- prime32 plans (prime32.rs:632-1025) -------------------------------------------------------
+
+struct mi_ntt32_plan {
+  mi_ntt64_plan* p64 = nullptr;  // same twiddle convention (prime32.rs:223-246 == prime64.rs:184-203)
+};
+
+int mi_ntt32_plan_create(size_t n, uint32_t p, int device, mi_ntt32_plan** out_plan) {
+  if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
+  *out_plan = nullptr;
+  // prime32.rs:662-671: N < 32, N not a power of two, p not prime, no root -> None
+  if (n < 32 || (n & (n - 1)) != 0) return fail(MI_ERR_INVALID_ARG, "polynomial size must be a power of two >= 32");
+  mi_ntt64_plan* p64 = nullptr;
+  int st = mi_ntt64_plan_create(n, p, device, &p64);
+  if (st != MI_OK) return st;
+  mi_ntt32_plan* plan = new (std::nothrow) mi_ntt32_plan;
+  if (!plan) {
+    mi_ntt64_plan_destroy(p64);
+    return fail(MI_ERR_OOM, "host allocation failed");
+  }
+  plan->p64 = p64;
+  *out_plan = plan;
+  return MI_OK;
+}
+
+int mi_ntt32_plan_destroy(mi_ntt32_plan* plan) {
+  if (!plan) return MI_OK;
+  mi_ntt64_plan_destroy(plan->p64);
+  delete plan;
+  return MI_OK;
+}
+
+int mi_ntt32_plan_info(const mi_ntt32_plan* plan, size_t* n, uint32_t* p, int* device) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (n) *n = plan->p64->n;
+  if (p) *p = (uint32_t)plan->p64->p;
+  if (device) *device = plan->p64->device;
+  return MI_OK;
+}
+
+static int run_ntt32(bool fwd, const mi_ntt32_plan* plan, uint32_t* buf, size_t batch, size_t stride, void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  const mi_ntt64_plan* q = plan->p64;
+  int st = check_batch(q, buf, batch, stride);
+  if (st != MI_OK || batch == 0) return st;
+  DeviceGuard g(q->device);
+  hipError_t e = mi::launch_ntt_u32(fwd, q->logn, q->mp, buf, batch, stride, fwd ? q->d_twid : q->d_inv_twid,
+                                    (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, fwd ? "fwd launch" : "inv launch");
+}
+
+int mi_ntt32_fwd_batch(const mi_ntt32_plan* plan, uint32_t* buf, size_t batch, size_t stride, void* stream) {
+  return run_ntt32(true, plan, buf, batch, stride, stream);
+}
+
+int mi_ntt32_inv_batch(const mi_ntt32_plan* plan, uint32_t* buf, size_t batch, size_t stride, void* stream) {
+  return run_ntt32(false, plan, buf, batch, stride, stream);
+}
+
+static int run_pw32(int op, const mi_ntt32_plan* plan, uint32_t* out, const uint32_t* a, const uint32_t* b,
+                    size_t batch, size_t stride, void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  const mi_ntt64_plan* q = plan->p64;
+  int st = check_batch(q, out, batch, stride);
+  if (st != MI_OK || batch == 0) return st;
+  if (op >= 1 && !b) return fail(MI_ERR_INVALID_ARG, "rhs is NULL");
+  if (op == 2 && !a) return fail(MI_ERR_INVALID_ARG, "lhs is NULL");
+  const u64 c = op == 0 ? q->c_normalize : (op == 1 ? q->c_man : q->c_macc);
+  DeviceGuard g(q->device);
+  hipError_t e = mi::launch_pointwise_u32(op, q->mp, out, a, b, q->n, batch, stride, c, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "pointwise launch");
+}
+
+int mi_ntt32_normalize_batch(const mi_ntt32_plan* plan, uint32_t* buf, size_t batch, size_t stride, void* stream) {
+  return run_pw32(0, plan, buf, nullptr, nullptr, batch, stride, stream);
+}
+
+int mi_ntt32_mul_assign_normalize_batch(const mi_ntt32_plan* plan, uint32_t* lhs, const uint32_t* rhs, size_t batch,
+                                        size_t stride, void* stream) {
+  return run_pw32(1, plan, lhs, nullptr, rhs, batch, stride, stream);
+}
+
+int mi_ntt32_mul_accumulate_batch(const mi_ntt32_plan* plan, uint32_t* acc, const uint32_t* lhs, const uint32_t* rhs,
+                                  size_t batch, size_t stride, void* stream) {
+  return run_pw32(2, plan, acc, lhs, rhs, batch, stride, stream);
+}
+
+// ---- exact native-modulus products over a CRT of primes (native{32,64,128}.rs, native_binary*.rs) --
+
+struct mi_native_plan {
+  int kind = 0, width = 64, binary = 0;
+  size_t n = 0;
+  int device = 0;
+  int k = 0;
+  mi_ntt64_plan* primes[mi::MI_CRT_MAX] = {};
+  mi::CrtConst crt;
+};
+
+namespace {
+// tfhe-ntt/src/lib.rs primes32 (P0..P9) and primes52 (P0..P5)
+constexpr uint32_t PRIMES32[10] = {0x3F5A0001u, 0x3F5D0001u, 0x3F760001u, 0x3F820001u, 0x3FAC0001u,
+                                   0x3FAF0001u, 0x3FB10001u, 0x3FBB0001u, 0x3FDE0001u, 0x3FFC0001u};
+constexpr u64 PRIMES52[6] = {0x3FFFFFE770001ull, 0x3FFFFFEB90001ull, 0x3FFFFFEC80001ull,
+                             0x3FFFFFF8B0001ull, 0x3FFFFFFB80001ull, 0x3FFFFFFC70001ull};
+
+struct NativeKind {
+  int width, binary, prime_bits, k;
+};
+// index = mi_native_kind
+constexpr NativeKind NATIVE_KINDS[] = {
+    {32, 0, 32, 3},   // native32::Plan32   (native32.rs:337-343)
+    {32, 0, 52, 2},   // native32::Plan52   (native32.rs:440-444)
+    {64, 0, 32, 5},   // native64::Plan32   (native64.rs:932-941)
+    {64, 0, 52, 3},   // native64::Plan52   (native64.rs:1077-1086)
+    {128, 0, 32, 10}, // native128::Plan32  (native128.rs:123-137)
+    {32, 1, 32, 2},   // native_binary32::Plan32 (native_binary32.rs:189-192)
+    {32, 1, 52, 1},   // native_binary32::Plan52 (native_binary32.rs:270-273)
+    {64, 1, 32, 3},   // native_binary64::Plan32 (native_binary64.rs:344-351)
+    {64, 1, 52, 2},   // native_binary64::Plan52 (native_binary64.rs:452-456)
+    {128, 1, 32, 5},  // native_binary128::Plan32 (native_binary128.rs:68-77)
+};
+}  // namespace
+
+int mi_native_plan_create(int kind, size_t n, int device, mi_native_plan** out_plan) {
+  if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
+  *out_plan = nullptr;
+  if (kind < 0 || kind >= (int)(sizeof(NATIVE_KINDS) / sizeof(NATIVE_KINDS[0])))
+    return fail(MI_ERR_INVALID_ARG, "unknown native plan kind");
+  const NativeKind nk = NATIVE_KINDS[kind];
+  // the component plans are prime32 plans (N >= 32) or prime64 plans (N >= 16)
+  if (nk.prime_bits == 32 && n < 32) return fail(MI_ERR_INVALID_ARG, "polynomial size must be >= 32");
+  mi_native_plan* plan = new (std::nothrow) mi_native_plan;
+  if (!plan) return fail(MI_ERR_OOM, "host allocation failed");
+  plan->kind = kind;
+  plan->width = nk.width;
+  plan->binary = nk.binary;
+  plan->n = n;
+  plan->device = device;
+  plan->k = nk.k;
+  mi::CrtConst& c = plan->crt;
+  c.k = nk.k;
+  c.prime_bits = nk.prime_bits;
+  u128 prefix = 1;  // prod_{l<k} p_l mod 2^128
+  for (int i = 0; i < nk.k; ++i) {
+    const u64 p = nk.prime_bits == 32 ? (u64)PRIMES32[i] : PRIMES52[i];
+    int st = mi_ntt64_plan_create(n, p, device, &plan->primes[i]);
+    if (st != MI_OK) {
+      mi_native_plan_destroy(plan);
+      return st;
+    }
+    c.p[i] = p;
+    c.prefix_lo[i] = (u64)prefix;
+    c.prefix_hi[i] = (u64)(prefix >> 64);
+    u64 pm = 1;  // prod_{l<i} p_l mod p_i
+    for (int l = 0; l < i; ++l) pm = mi::host::mul_mod(pm, c.p[l] % p, p);
+    c.inv_prefix[i] = i == 0 ? 1 : mi::host::exp_mod(pm, p - 2, p);
+    prefix *= p;
+  }
+  c.m_lo = (u64)prefix;
+  c.m_hi = (u64)(prefix >> 64);
+  *out_plan = plan;
+  return MI_OK;
+}
+
+int mi_native_plan_destroy(mi_native_plan* plan) {
+  if (!plan) return MI_OK;
+  for (int i = 0; i < mi::MI_CRT_MAX; ++i)
+    if (plan->primes[i]) mi_ntt64_plan_destroy(plan->primes[i]);
+  delete plan;
+  return MI_OK;
+}
+
+int mi_native_plan_info(const mi_native_plan* plan, size_t* n, int* width_bits, int* num_primes) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (n) *n = plan->n;
+  if (width_bits) *width_bits = plan->width;
+  if (num_primes) *num_primes = plan->k;
+  return MI_OK;
+}
+
+int mi_native_polymul_batch(const mi_native_plan* plan, void* prod, const void* lhs, const void* rhs, size_t batch,
+                            void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (batch == 0) return MI_OK;
+  if (!prod || !lhs || !rhs) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t count = batch * plan->n;
+  DeviceGuard g(plan->device);
+  u64* scratch = nullptr;  // [lhs residues: k planes | rhs residues: k planes], stream-ordered
+  hipError_t e = hipMallocAsync((void**)&scratch, 2 * (size_t)plan->k * count * sizeof(u64), s);
+  if (e != hipSuccess) return fail(MI_ERR_OOM, "scratch allocation failed");
+  u64* a = scratch;
+  u64* b = scratch + (size_t)plan->k * count;
+  e = mi::launch_crt_residues(a, lhs, count, plan->width, 0, plan->crt, s);
+  if (e == hipSuccess) e = mi::launch_crt_residues(b, rhs, count, plan->width, plan->binary, plan->crt, s);
+  int st = e == hipSuccess ? MI_OK : hip_fail(e, "residue launch");
+  for (int i = 0; i < plan->k && st == MI_OK; ++i) {
+    const mi_ntt64_plan* q = plan->primes[i];
+    u64* ai = a + (size_t)i * count;
+    u64* bi = b + (size_t)i * count;
+    st = run_ntt(true, q, ai, batch, plan->n, stream);
+    if (st == MI_OK) st = run_ntt(true, q, bi, batch, plan->n, stream);
+    if (st == MI_OK) st = run_pw(1, q, ai, nullptr, bi, batch, plan->n, stream);
+    if (st == MI_OK) st = run_ntt(false, q, ai, batch, plan->n, stream);
+  }
+  if (st == MI_OK) {
+    e = mi::launch_crt_reconstruct(prod, a, count, plan->width, plan->crt, s);
+    if (e != hipSuccess) st = hip_fail(e, "reconstruct launch");
+  }
+  (void)hipFreeAsync(scratch, s);
+  return st;
+}
+
 }  // extern "C"

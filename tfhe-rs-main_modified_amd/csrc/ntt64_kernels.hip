@@ -24,8 +24,10 @@
 
 namespace mi {
 
-template <class G, bool FWD, class Mod>
-__global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(u64* __restrict__ data, uint32_t batch, uint64_t stride,
+// IO = u64 (prime64 plans) or uint32_t (prime32 plans, prime32.rs:797-898: the same transform on
+// u32 buffers; arithmetic stays 64-bit Montgomery, exact for any odd prime)
+template <class G, bool FWD, class Mod, class IO>
+__global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__ data, uint32_t batch, uint64_t stride,
                                                                 const u64* __restrict__ tw, Mod mod) {
   __shared__ u64 lds[G::PPW * G::PADDED];
   const int tid = threadIdx.x;
@@ -33,14 +35,14 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(u64* __restrict_
   const int t = tid & (G::T - 1);    // lane within the polynomial
   const uint64_t poly = (uint64_t)blockIdx.x * G::PPW + pw;
   const bool valid = poly < batch;
-  u64* __restrict__ src = data + poly * stride;
+  IO* __restrict__ src = data + poly * stride;
   u64* sh = lds + pw * G::PADDED;
 
   u64 x[G::E];
   {
     const int lo = win_lo<G, FWD>(0);
 #pragma unroll
-    for (int r = 0; r < G::E; ++r) x[r] = valid ? src[elem<G>(t, r, lo)] : 0;
+    for (int r = 0; r < G::E; ++r) x[r] = valid ? (u64)src[elem<G>(t, r, lo)] : 0;
   }
 #pragma unroll
   for (int w = 0; w < G::NWIN; ++w) {
@@ -58,25 +60,25 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(u64* __restrict_
   if (valid) {
     const int lo = win_lo<G, FWD>(G::NWIN - 1);
 #pragma unroll
-    for (int r = 0; r < G::E; ++r) src[elem<G>(t, r, lo)] = x[r];
+    for (int r = 0; r < G::E; ++r) src[elem<G>(t, r, lo)] = (IO)x[r];
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // launch dispatch
 
-template <int LOGN, int LOGE, bool FWD, class Mod>
-static hipError_t launch_window(u64* data, size_t batch, size_t stride, const u64* tw, const Mod& mod,
+template <int LOGN, int LOGE, bool FWD, class Mod, class IO>
+static hipError_t launch_window(IO* data, size_t batch, size_t stride, const u64* tw, const Mod& mod,
                                 hipStream_t stream) {
   using G = Geo<LOGN, LOGE>;
   const unsigned grid = (unsigned)((batch + G::PPW - 1) / G::PPW);
-  hipLaunchKernelGGL((ntt_window_kernel<G, FWD, Mod>), dim3(grid), dim3(G::THREADS), 0, stream, data,
+  hipLaunchKernelGGL((ntt_window_kernel<G, FWD, Mod, IO>), dim3(grid), dim3(G::THREADS), 0, stream, data,
                      (uint32_t)batch, (uint64_t)stride, tw, mod);
   return hipGetLastError();
 }
 
-template <bool FWD, class Mod>
-static hipError_t dispatch(int logn, int variant, u64* data, size_t batch, size_t stride, const u64* tw,
+template <bool FWD, class Mod, class IO>
+static hipError_t dispatch(int logn, int variant, IO* data, size_t batch, size_t stride, const u64* tw,
                            const Mod& mod, hipStream_t s) {
   switch (logn) {
     case 4: return launch_window<4, 3, FWD>(data, batch, stride, tw, mod, s);
@@ -112,6 +114,13 @@ hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const Mo
              : dispatch<false>(logn, variant, data, batch, stride, tw, m, s);
 }
 
+hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* data, size_t batch, size_t stride,
+                          const uint64_t* tw, hipStream_t s) {
+  Montgomery m{mp.p, mp.pinv, mp.r2};
+  return fwd ? dispatch<true>(logn, 0, data, batch, stride, tw, m, s)
+             : dispatch<false>(logn, 0, data, batch, stride, tw, m, s);
+}
+
 // ---------------------------------------------------------------------------------------------
 // pointwise ops (prime64.rs:1050-1222), 2 u64 per lane per iteration, grid-stride
 
@@ -127,9 +136,9 @@ __device__ __forceinline__ u64 pw_one(u64 o, u64 a, u64 b, u64 c, const Mod& mod
 }
 
 // VW = values per lane per iteration (2 -> 16-byte accesses, needs even stride + 16-B alignment)
-template <int OP, int VW, class Mod>
-__global__ __launch_bounds__(256) void pointwise_kernel(u64* __restrict__ out, const u64* __restrict__ a,
-                                                        const u64* __restrict__ b, uint32_t n, uint32_t batch,
+template <int OP, int VW, class Mod, class IO = u64>
+__global__ __launch_bounds__(256) void pointwise_kernel(IO* __restrict__ out, const IO* __restrict__ a,
+                                                        const IO* __restrict__ b, uint32_t n, uint32_t batch,
                                                         uint64_t stride, u64 c, Mod mod) {
   const uint64_t per_poly = n / VW;
   const uint64_t total = per_poly * batch;
@@ -137,7 +146,7 @@ __global__ __launch_bounds__(256) void pointwise_kernel(u64* __restrict__ out, c
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t poly = i / per_poly;
     const uint64_t off = poly * stride + VW * (i - poly * per_poly);
-    if (VW == 2) {
+    if constexpr (VW == 2) {
       const ulonglong2 ov = *reinterpret_cast<const ulonglong2*>(out + off);
       ulonglong2 av = make_ulonglong2(0, 0), bv = make_ulonglong2(0, 0);
       if (OP == PW_MUL_ACCUMULATE) av = *reinterpret_cast<const ulonglong2*>(a + off);
@@ -145,9 +154,9 @@ __global__ __launch_bounds__(256) void pointwise_kernel(u64* __restrict__ out, c
       *reinterpret_cast<ulonglong2*>(out + off) =
           make_ulonglong2(pw_one<OP>(ov.x, av.x, bv.x, c, mod), pw_one<OP>(ov.y, av.y, bv.y, c, mod));
     } else {
-      const u64 av = (OP == PW_MUL_ACCUMULATE) ? a[off] : 0;
-      const u64 bv = (OP != PW_NORMALIZE) ? b[off] : 0;
-      out[off] = pw_one<OP>(out[off], av, bv, c, mod);
+      const u64 av = (OP == PW_MUL_ACCUMULATE) ? (u64)a[off] : 0;
+      const u64 bv = (OP != PW_NORMALIZE) ? (u64)b[off] : 0;
+      out[off] = (IO)pw_one<OP>((u64)out[off], av, bv, c, mod);
     }
   }
 }
@@ -182,6 +191,22 @@ hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, u64* 
   if (op == PW_NORMALIZE) return launch_pw<PW_NORMALIZE>(out, a, b, n, batch, stride, c, m, s);
   if (op == PW_MUL_ASSIGN_NORMALIZE) return launch_pw<PW_MUL_ASSIGN_NORMALIZE>(out, a, b, n, batch, stride, c, m, s);
   return launch_pw<PW_MUL_ACCUMULATE>(out, a, b, n, batch, stride, c, m, s);
+}
+
+hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, const uint32_t* a, const uint32_t* b,
+                                size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s) {
+  Montgomery m{mp.p, mp.pinv, mp.r2};
+  uint64_t blocks = ((uint64_t)n * batch + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+#define MI_PW32(OP)                                                                                         \
+  hipLaunchKernelGGL((pointwise_kernel<OP, 1, Montgomery, uint32_t>), dim3((unsigned)blocks), dim3(256), 0, s, \
+                     out, a, b, (uint32_t)n, (uint32_t)batch, (uint64_t)stride, c, m)
+  if (op == PW_NORMALIZE) MI_PW32(PW_NORMALIZE);
+  else if (op == PW_MUL_ASSIGN_NORMALIZE) MI_PW32(PW_MUL_ASSIGN_NORMALIZE);
+  else MI_PW32(PW_MUL_ACCUMULATE);
+#undef MI_PW32
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -16,6 +16,12 @@ struct MontParams {
 hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, uint64_t* data,
                       size_t batch, size_t stride, const uint64_t* tw, hipStream_t s);
 
+// prime32 plans (u32 buffers, generic Montgomery arithmetic)
+hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* data, size_t batch, size_t stride,
+                          const uint64_t* tw, hipStream_t s);
+hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, const uint32_t* a, const uint32_t* b,
+                                size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
+
 // Goldilocks persistent kernels (ntt64_gl.hip); hipErrorInvalidValue when the size is not covered.
 hipError_t launch_ntt_gl(bool fwd, int logn, int variant, uint64_t* data, size_t batch, size_t stride,
                          const uint64_t* tw, hipStream_t s);
@@ -28,6 +34,19 @@ hipError_t launch_ntt_tw(bool fwd, int variant, uint64_t* data, size_t batch, si
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
 hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,
                             const uint64_t* b, size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
+
+// native-modulus CRT products (native_crt.hip): up to 10 primes; prefix = prod_{l<k} p_l mod 2^128,
+// inv_prefix[k] = (prod_{l<k} p_l)^-1 mod p_k, m = prod of all primes mod 2^128
+constexpr int MI_CRT_MAX = 10;
+struct CrtConst {
+  int k = 0, prime_bits = 32;
+  uint64_t p[MI_CRT_MAX] = {}, inv_prefix[MI_CRT_MAX] = {}, prefix_lo[MI_CRT_MAX] = {}, prefix_hi[MI_CRT_MAX] = {};
+  uint64_t m_lo = 0, m_hi = 0;
+};
+hipError_t launch_crt_residues(uint64_t* planes, const void* in, size_t count, int width, int binary,
+                               const CrtConst& c, hipStream_t s);
+hipError_t launch_crt_reconstruct(void* out, const uint64_t* planes, size_t count, int width, const CrtConst& c,
+                                  hipStream_t s);
 
 hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint64_t p, hipStream_t s);
 

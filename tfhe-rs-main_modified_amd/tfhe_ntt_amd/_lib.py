@@ -57,6 +57,18 @@ _SIGS = {
     "mi_pbs_ntt64_key_create": (_int, [_vp, _vp, _sz, _int, _int, _int, _int, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_key_destroy": (_int, [_vp]),
     "mi_pbs_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_ntt32_plan_create": (_int, [_sz, ctypes.c_uint32, _int, ctypes.POINTER(_vp)]),
+    "mi_ntt32_plan_destroy": (_int, [_vp]),
+    "mi_ntt32_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(_int)]),
+    "mi_ntt32_fwd_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt32_inv_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt32_normalize_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt32_mul_assign_normalize_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt32_mul_accumulate_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_native_plan_create": (_int, [_int, _sz, _int, ctypes.POINTER(_vp)]),
+    "mi_native_plan_destroy": (_int, [_vp]),
+    "mi_native_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "mi_native_polymul_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None
