@@ -96,10 +96,12 @@ int mi_fill_uniform(uint64_t *buf, size_t count, uint64_t seed, uint64_t p, int 
  * (ntt64_bnf_pbs.rs). */
 typedef enum mi_ntt64_variant { MI_NTT64_SOLINAS = 0, MI_NTT64_BNF = 1 } mi_ntt64_variant;
 
-/* Modulus switch of the PBS input (BNF only): standard rounding (fft_impl/common.rs:10-23, as
- * ntt64_bnf_pbs.rs:512) or the centered-binary variant the shortint parameters use
- * (algorithms/modulus_switch.rs:35-104). */
-typedef enum mi_ms_mode { MI_MS_STANDARD = 0, MI_MS_CENTERED = 1 } mi_ms_mode;
+/* Modulus switch of the PBS input: standard rounding (fft_impl/common.rs:10-23, as
+ * ntt64_bnf_pbs.rs:512; ntt64_pbs.rs:540-549 for Solinas), the centered-binary variant the shortint
+ * parameters use (BNF only, algorithms/modulus_switch.rs:35-104), or PRE_SWITCHED: lwe_in already
+ * holds the switched values in [0, 2N) (the ModulusSwitchedLweCiphertext input of
+ * blind_rotate_ntt64[_bnf]_assign_mem_optimized, ntt64_bnf_pbs.rs:208-266 / ntt64_pbs.rs:213-286). */
+typedef enum mi_ms_mode { MI_MS_STANDARD = 0, MI_MS_CENTERED = 1, MI_MS_PRE_SWITCHED = 2 } mi_ms_mode;
 
 /* convert_standard_lwe_bootstrap_key_to_ntt64 (algorithms/lwe_bootstrap_key_conversion.rs:294-365)
  * over `n_polys` polynomials (= n_lwe * (k+1)^2 * level): bsk_ntt = fwd(switch(bsk_std)) [* N^{-1}],

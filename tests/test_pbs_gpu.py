@@ -209,3 +209,29 @@ def test_pbs_errors(engine, plan):
     M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe[:0], out[:0], lut, key)  # empty batch
     with pytest.raises(ValueError):
         M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe[:, :4], out, lut, key)
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+def test_pbs_pre_switched(engine, plan, ctx, oracle, bnf):
+    """MS_PRE_SWITCHED: lwe_in holds modulus-switched values (the ModulusSwitchedLweCiphertext input
+    of blind_rotate_ntt64[_bnf]_assign_mem_optimized); the result equals the standard path on the raw
+    ciphertexts and the oracle."""
+    q = 0 if bnf else P
+    g = H.rng(77 + bnf)
+    n_lwe, batch, base_log, level = 30, 5, 23, 1
+    bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)
+    lut = rand_q(g, (K + 1, N), q)
+    lwe = _pbs_inputs(g, batch, n_lwe, q)
+    if bnf:
+        msed = np.vectorize(lambda x: oracle.modulus_switch(int(x), 12), otypes=[np.uint64])(lwe)
+    else:
+        msed = np.vectorize(lambda x: oracle.pbs_modulus_switch_non_native(int(x), N, P), otypes=[np.uint64])(lwe)
+    want = np.stack([ctx.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, bnf=bnf)
+                     for b in range(batch)])
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(plan, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    fn = (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf
+          else M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)
+    fn(dev(msed), out, dev(lut), key, M.MS_PRE_SWITCHED)
+    assert np.array_equal(host(out), want)

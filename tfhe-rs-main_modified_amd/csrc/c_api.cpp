@@ -472,22 +472,37 @@ int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key* key) {
 int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
                        size_t batch, int ms_mode, void* stream) {
   if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
-  if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED) return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
+  if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED && ms_mode != MI_MS_PRE_SWITCHED)
+    return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
   if (ms_mode == MI_MS_CENTERED && key->variant != MI_NTT64_BNF)
     return fail(MI_ERR_INVALID_ARG, "centered modulus switch applies to native-modulus (BNF) inputs");
   if (batch == 0) return MI_OK;
   if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   const mi_ntt64_plan* plan = key->plan;
+  const hipStream_t s = (hipStream_t)stream;
   DeviceGuard g(plan->device);
-  if (twisted_ext_applies(plan, key->variant, key->base_log, key->level)) {
-    hipError_t e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
-                                     plan->d_twist_f, ms_mode == MI_MS_CENTERED, (hipStream_t)stream);
-    return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
+  u64* lifted = nullptr;  // PRE_SWITCHED: stream-ordered copy lifted back to the standard switch
+  if (ms_mode == MI_MS_PRE_SWITCHED) {
+    const size_t count = batch * (key->n_lwe + 1);
+    if (hipMallocAsync((void**)&lifted, count * sizeof(u64), s) != hipSuccess)
+      return fail(MI_ERR_OOM, "scratch allocation failed");
+    hipError_t e = mi::launch_lift_switched(lifted, lwe_in, count, key->variant == MI_NTT64_BNF, s);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(lifted, s);
+      return hip_fail(e, "lift launch");
+    }
+    lwe_in = lifted;
+    ms_mode = MI_MS_STANDARD;
   }
-  hipError_t e = mi::launch_pbs(key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe,
-                                batch, key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED,
-                                (hipStream_t)stream);
+  hipError_t e;
+  if (twisted_ext_applies(plan, key->variant, key->base_log, key->level))
+    e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
+                          ms_mode == MI_MS_CENTERED, s);
+  else
+    e = mi::launch_pbs(key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
+                       key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);
+  if (lifted) (void)hipFreeAsync(lifted, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
 }
 

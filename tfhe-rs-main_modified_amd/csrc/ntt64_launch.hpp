@@ -55,6 +55,7 @@ hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint6
 namespace mi {
 
 // pbs_kernels.hip — Goldilocks, N = 2048, k = 1 only (callers validate the shape).
+hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, hipStream_t s);
 hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
                              uint64_t n_inv, const uint64_t* tw, hipStream_t s);
 hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s);

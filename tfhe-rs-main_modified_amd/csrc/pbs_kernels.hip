@@ -390,7 +390,27 @@ __global__ __launch_bounds__(256) void scale_kernel(u64* __restrict__ dst, const
     dst[i] = gl.mul(src[i], c);
 }
 
+// PRE_SWITCHED inputs: lift each switched value v in [0, 2N) to a representative whose standard
+// switch is v again — BNF: v << 52 ((v 2^52 + 2^51) >> 52 = v); Solinas: round(v p / 2N), whose
+// ms_non_native is v (the rounding error is < 2N / p) and which is 0 iff v is 0 (same skip).
+__global__ __launch_bounds__(256) void lift_switched_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
+                                                            uint64_t count, int bnf) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
+    const u64 v = src[i] & (2 * N - 1);
+    dst[i] = bnf ? v << (64 - (G::LOGN + 1)) : (u64)(((unsigned __int128)v * P + N) >> (G::LOGN + 1));
+  }
+}
+
 }  // namespace pbs
+
+hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pbs::lift_switched_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, (uint64_t)count,
+                     bnf ? 1 : 0);
+  return hipGetLastError();
+}
 
 hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
                              uint64_t n_inv, const uint64_t* tw, hipStream_t s) {

@@ -24,6 +24,7 @@ SOLINAS = 0
 BNF = 1
 MS_STANDARD = 0
 MS_CENTERED = 1
+MS_PRE_SWITCHED = 2  # lwe_in already modulus-switched to [0, 2N) (ModulusSwitchedLweCiphertext)
 
 
 def _dev(t, name):
@@ -157,15 +158,19 @@ def programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe_in, lwe_ou
     _pbs(key, lwe_in, lwe_out, accumulator, ms_mode)
 
 
-def programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key) -> None:
-    """Batched PBS of LWEs modulo the Solinas prime (ntt64_pbs.rs:482-538)."""
+def programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key,
+                                                              ms_mode: int = MS_STANDARD) -> None:
+    """Batched PBS of LWEs modulo the Solinas prime (ntt64_pbs.rs:482-538); ms_mode STANDARD or
+    PRE_SWITCHED."""
     if key.variant != SOLINAS:
         raise ValueError("key was not prepared for the Solinas variant")
-    _pbs(key, lwe_in, lwe_out, accumulator, MS_STANDARD)
+    if ms_mode == MS_CENTERED:
+        raise ValueError("centered modulus switch applies to native-modulus (BNF) inputs")
+    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode)
 
 
 __all__ = [
-    "SOLINAS", "BNF", "MS_STANDARD", "MS_CENTERED", "MiError", "NttBootstrapKey",
+    "SOLINAS", "BNF", "MS_STANDARD", "MS_CENTERED", "MS_PRE_SWITCHED", "MiError", "NttBootstrapKey",
     "convert_standard_lwe_bootstrap_key_to_ntt64", "add_external_product_ntt64_assign",
     "add_external_product_ntt64_bnf_assign", "cmux_ntt64_assign", "cmux_ntt64_bnf_assign",
     "programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized",
