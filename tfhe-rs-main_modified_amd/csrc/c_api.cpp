@@ -268,7 +268,7 @@ static int check_batch(const mi_ntt64_plan* plan, const void* buf, size_t batch,
 // exist (MI_NTT_VARIANT=4), else the register-window kernels.
 static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride,
                                    hipStream_t s) {
-  if (plan->variant >= 4 && plan->variant <= 6 && plan->d_twist_f)
+  if (plan->variant >= 4 && plan->variant <= 7 && plan->d_twist_f)
     return mi::launch_ntt_tw(fwd, plan->variant, buf, batch, stride, fwd ? plan->d_twist_f : plan->d_twist_i, s);
   return mi::launch_ntt(fwd, plan->logn, plan->variant >= 4 ? 0 : plan->variant, plan->goldilocks, plan->mp, buf,
                         batch, stride, fwd ? plan->d_twid : plan->d_inv_twid, s);

@@ -373,11 +373,77 @@ __global__ __launch_bounds__(256, 4) void ntt_tw_body_kernel(u64* __restrict__ d
   }
 }
 
+// ---- persistent software-pipelined kernel (tools/gen_tw_kernel.py gen_pipe) ------------------------
+// One 8-wave workgroup per CU (192 VGPRs per wave: 2 waves per SIMD).  The workgroup copies the
+// direction's twist + pair-stage tables (N + 32 u64) into LDS once; each wave then walks the
+// polynomials poly0, poly0 + step, ... with the next one's rows prefetched into v128..v191 while the
+// current one is transformed.  HBM load latency is exposed once per wave, not once per polynomial.
+static constexpr int PIPE_WAVES = 8;
+static constexpr int TAB = 2048 + 32;
+
+template <bool FWD>
+__global__ __launch_bounds__(64 * PIPE_WAVES, 1) void ntt_tw_pipe_kernel(u64* __restrict__ data, uint32_t batch,
+                                                                          uint32_t stride_bytes,
+                                                                          const u64* __restrict__ twist) {
+  __shared__ u64 lds[PIPE_WAVES * WAVE_LDS2];
+  __shared__ u64 tab[TAB];
+  for (int t = threadIdx.x; t < TAB; t += 64 * PIPE_WAVES) tab[t] = twist[t];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t poly0 = blockIdx.x * PIPE_WAVES + wv;
+  const uint32_t step = gridDim.x * PIPE_WAVES;
+  if (poly0 >= batch) return;  // whole wave; no barrier follows
+  const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
+  const uint32_t par = lane & 1, i = lane >> 1;
+  const uint32_t l8 = lane * 8;
+  const uint32_t t1w = S + (lane & 31) * 8;
+  const uint32_t t1r = S + (i * 34 + par) * 8;
+  const uint32_t twl = (uint32_t)(uintptr_t)tab + lane * 8;
+  const uint32_t lwl = (uint32_t)(uintptr_t)(tab + 2048) + par * 128;
+  const uint32_t glo = (uint32_t)(uintptr_t)data, ghi = (uint32_t)((uintptr_t)data >> 32);
+  if constexpr (FWD) {
+    const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
+    const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
+    const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
+    MI_TW_PIPE_FWD([g_lo] "s"(glo), [g_hi] "s"(ghi), [p0] "s"(poly0), [batch] "s"(batch), [step] "s"(step),
+                   [sb] "s"(stride_bytes), [l8] "v"(l8), [twl] "v"(twl), [lwl] "v"(lwl), [t1w] "v"(t1w),
+                   [t1r] "v"(t1r), [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r));
+  } else {
+    const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
+    const uint32_t t4r = S + lane * 8;
+    MI_TW_PIPE_INV([g_lo] "s"(glo), [g_hi] "s"(ghi), [p0] "s"(poly0), [batch] "s"(batch), [step] "s"(step),
+                   [sb] "s"(stride_bytes), [l8] "v"(l8), [twl] "v"(twl), [lwl] "v"(lwl), [t1w] "v"(t1w),
+                   [t1r] "v"(t1r), [t4w] "v"(t4w), [t4r] "v"(t4r));
+  }
+}
+
 }  // namespace tw
+
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return cus;
+}
 
 hipError_t launch_ntt_tw(bool fwd, int variant, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
                          hipStream_t s) {
   if (batch == 0) return hipSuccess;
+  if (variant == 7) {  // persistent pipelined asm body: one 8-wave workgroup per CU
+    if (batch > 0xFFFFFFFFull || stride * 8 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    static const int cus = device_cus();
+    const size_t wgs = (batch + tw::PIPE_WAVES - 1) / tw::PIPE_WAVES;
+    const unsigned grid = (unsigned)(wgs < (size_t)cus ? wgs : (size_t)cus);
+    if (fwd)
+      hipLaunchKernelGGL((tw::ntt_tw_pipe_kernel<true>), dim3(grid), dim3(64 * tw::PIPE_WAVES), 0, s, data,
+                         (uint32_t)batch, (uint32_t)(stride * 8), twist);
+    else
+      hipLaunchKernelGGL((tw::ntt_tw_pipe_kernel<false>), dim3(grid), dim3(64 * tw::PIPE_WAVES), 0, s, data,
+                         (uint32_t)batch, (uint32_t)(stride * 8), twist);
+    return hipGetLastError();
+  }
   const unsigned grid = (unsigned)((batch + 3) / 4);
   if (variant == 4) {  // whole-body asm
     if (fwd)

@@ -507,6 +507,9 @@ class Addr:
 
     def __init__(self, tw_load, **regs):
         self.tw_load = tw_load    # (batch bt, row k, dst pair base) -> load line of table row 8 bt + k
+        self.tw_wait = "s_waitcnt vmcnt(0)"
+        # (dst pair base, table entry k) -> load line of the lane's pair-stage twiddle k (+16 odd lanes)
+        self.lw_load = lambda dst, k: f"global_load_dwordx2 {pv(dst)}, {self.lwo}, {self.lw} offset:{8 * k}"
         self.__dict__.update(regs)
 
 
@@ -629,8 +632,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR):
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
     for half in range(2):
         ks = list(range(8 * half, 8 * half + 8))
-        B.raw(*[f"global_load_dwordx2 {pv(wb[2 * i])}, {ad.lwo}, {ad.lw} offset:{8 * k}" for i, k in enumerate(ks)],
-              "s_waitcnt vmcnt(0)", "s_nop 1")
+        B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in enumerate(ks)], ad.tw_wait, "s_nop 1")
         sg = Seg()
         for i, k in enumerate(ks):
             tmp = [f"v{r}" for r in tmps[i % 2]]
@@ -677,7 +679,7 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
     ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
     for bt in range(4):
         rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[ad.tw_load(bt, k, 8 + 2 * k) for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.raw(*[ad.tw_load(bt, k, 8 + 2 * k) for k in range(8)], ad.tw_wait)
         B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms)
     if stop == "twist":
         return dmap
@@ -728,7 +730,7 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR):
     ms = [MulSlot(regs[16 + 12 * i], SG0 + 6 * i) for i in range((len(regs) - 16) // 12)]
     for bt in range(4):
         rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[ad.tw_load(bt, k, regs[2 * k]) for k in range(8)], "s_waitcnt vmcnt(0)")
+        B.raw(*[ad.tw_load(bt, k, regs[2 * k]) for k in range(8)], ad.tw_wait)
         B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
@@ -756,6 +758,61 @@ def gen_inv(tabs, stop=None):
     return B
 
 
+# ------------------------------------------------------------------------------------------------
+# Persistent, software-pipelined variant (ntt64_tw.hip ntt_tw_pipe_kernel): each wave walks the
+# polynomials poly0, poly0 + step, ... < batch; the next polynomial's 32 rows are loaded into
+# v128..v191 while the current one is transformed, so HBM latency is exposed once per wave instead
+# of once per polynomial.  The twist / pair-stage tables live in LDS (copied once per workgroup), so
+# the body issues no global load besides the prefetch and vmcnt only ever counts prefetch + stores.
+VPF = 128                                   # prefetch rows v128..v191
+S_NXT, S_BAT, S_STP, S_SB, S_GD = 94, 95, 96, 97, 98   # s98:99 data base
+PIPE_SGPR_CLOBBER = SGPR_CLOBBER + list(range(94, 100))
+
+LDS_ADDR = Addr(lambda bt, k, dst: f"ds_read_b64 {pv(dst)}, %[twl] offset:{512 * (8 * bt + k)}",
+                **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r")})
+LDS_ADDR.tw_wait = "s_waitcnt lgkmcnt(0)"
+# pair-stage table: 32 entries after the 2048 twist rows; lane parity selects entries 16..31
+LDS_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, %[lwl] offset:{8 * k}"
+
+
+def poly_bases(dst):
+    """s[dst .. dst+7] = data base + s_NXT * stride_bytes + 4096 m (m = 0..3)."""
+    return [f"s_mul_i32 s{dst}, s{S_NXT}, s{S_SB}", f"s_mul_hi_u32 s{dst + 1}, s{S_NXT}, s{S_SB}",
+            f"s_add_u32 s{dst}, s{dst}, s{S_GD}", f"s_addc_u32 s{dst + 1}, s{dst + 1}, s{S_GD + 1}"] + \
+        [l for m in range(1, 4) for l in (f"s_add_u32 s{dst + 2 * m}, s{dst}, {4096 * m}",
+                                          f"s_addc_u32 s{dst + 2 * m + 1}, s{dst + 1}, 0")]
+
+
+def gen_pipe(tabs, fwd):
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    pf = [VPF + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(f"s_mov_b32 s{S_NXT}, %[p0]", f"s_mov_b32 s{S_BAT}, %[batch]", f"s_mov_b32 s{S_STP}, %[step]",
+          f"s_mov_b32 s{S_SB}, %[sb]", f"s_mov_b32 s{S_GD}, %[g_lo]", f"s_mov_b32 s{S_GD + 1}, %[g_hi]")
+    B.raw(*poly_bases(S_GB), *load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    B.raw(".Ltw_top_%=:",
+          f"s_add_u32 s{S_NXT}, s{S_NXT}, s{S_STP}", f"s_cmp_lt_u32 s{S_NXT}, s{S_BAT}",
+          "s_cbranch_scc0 .Ltw_nopf_%=",
+          *poly_bases(S_TB), *load_rows(pf, S_TB), ".Ltw_nopf_%=:")
+    out = fwd_core(B, tabs, dmap, LDS_ADDR) if fwd else inv_core(B, tabs, dmap, LDS_ADDR)
+    B.raw(*store_rows(out, S_GB), f"s_cmp_lt_u32 s{S_NXT}, s{S_BAT}", "s_cbranch_scc0 .Ltw_end_%=",
+          "s_waitcnt vmcnt(32)")
+    B.raw(*[f"v_mov_b64 {pv(d)}, {pv(p)}" for d, p in zip(dmap, pf)])
+    B.raw(*[f"s_mov_b64 s[{S_GB + 2 * m}:{S_GB + 2 * m + 1}], s[{S_TB + 2 * m}:{S_TB + 2 * m + 1}]" for m in range(4)],
+          "s_branch .Ltw_top_%=", ".Ltw_end_%=:", "s_waitcnt vmcnt(0)")
+    return B
+
+
+def emit_pipe(name, body):
+    clob = [f'"v{i}"' for i in range(VLO, VPF + 64)] + [f'"s{i}"' for i in PIPE_SGPR_CLOBBER] + ['"scc"', '"memory"']
+    return (f"// {name}: {body.nvalu} VALU per polynomial (incl. 32 v_mov_b64), {len(body.lines)} lines\n"
+            f"#define MI_TW_PIPE_{name.upper()}(...) asm volatile(\\\n" +
+            "\\\n".join(f'      "{l}\\n"' for l in body.lines) +
+            f"\\\n      :: __VA_ARGS__ \\\n      : {', '.join(clob)})\n")
+
+
 def emit(name, body, ops_in):
     clob = [f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
     text = "\n".join(f'      "{l}\\n"' for l in body.lines)
@@ -778,6 +835,8 @@ def main():
     print("#pragma once")
     print(emit("fwd", f, None))
     print(emit("inv", i, None))
+    print(emit_pipe("fwd", gen_pipe(tabs, True)))
+    print(emit_pipe("inv", gen_pipe(tabs, False)))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 
