@@ -218,6 +218,49 @@ def bench_ext_product(args, eng, torch, dev, world, barrier):
             "algorithmic_bytes_per_unit": 32768 + 65536}
 
 
+KS_IN, KS_BASE_LOG, KS_LEVEL = 2048, 4, 4  # PARAM_MESSAGE_2_CARRY_2 keyswitch (ks_pbs.rs:38-39): k*N -> n
+I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: i8 MFMA = 2x the dense bf16 rate (~2.5 PF)
+
+
+def bench_keyswitch(args, eng, torch, dev, world, barrier):
+    """The keyswitch in front of the PBS (shortint KS-PBS order): batched 2048 -> 918 LWE keyswitch,
+    base 2^4, 4 levels, on the int8 matrix cores; key and inputs resident."""
+    KS = eng.lwe_keyswitch
+    batch = args.pbs_batch
+    ksk = torch.empty((KS_IN, KS_LEVEL, PBS_N_LWE + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ksk, SEED + 40, 0)
+    key = KS.LweKeyswitchKey(ksk, KS_BASE_LOG, KS_LEVEL)
+    del ksk
+    lwe = torch.empty((batch, KS_IN + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 41, 0)
+    out = torch.empty((batch, PBS_N_LWE + 1), dtype=torch.int64, device=dev)
+    run = lambda: KS.keyswitch_lwe_ciphertext(key, lwe, out)
+    run()
+    torch.cuda.synchronize()
+    K = max(5, args.steps)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(K):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / K
+    # algorithmic int8 MACs: 8 byte planes x (out_dim + 1) columns x in_dim*level digits per ciphertext
+    ops = 2.0 * batch * 8 * (PBS_N_LWE + 1) * KS_IN * KS_LEVEL
+    return {"metric": "LWE keyswitches/sec (KS of KS-PBS)", "value": world * batch * K / el, "unit": "KS/s",
+            "ms_per_step": el / K * 1e3, "kernel_ms": ms,
+            "config": {"workload": "keyswitch_lwe_ciphertext 2048 -> 918, base_log 4, level 4, native modulus",
+                       "batch_per_gpu": batch},
+            "roofline": {"bound": "mfma", "achieved": ops / (ms * 1e-3) / 1e12, "peak": I8_PEAK_TOPS,
+                         "unit": "TOP/s", "frac": ops / (ms * 1e-3) / 1e12 / I8_PEAK_TOPS,
+                         "note": "digit pass + i8 MFMA GEMM (8 byte planes) per step"}}
+
+
 def load_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*/pmc_traffic.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -332,6 +375,10 @@ def main():
     if not args.no_pbs:
         out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
+        out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
+        ks_ms, pbs_ms = out["keyswitch"]["ms_per_step"], out["pbs"]["ms_per_step"]
+        out["ks_pbs"] = {"metric": "KS-PBS/sec (keyswitch then PBS, PARAM_MESSAGE_2_CARRY_2 shape)",
+                         "value": world * args.pbs_batch / ((ks_ms + pbs_ms) * 1e-3), "unit": "KS-PBS/s"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_pbs:

@@ -188,6 +188,26 @@ int mi_native_plan_info(const mi_native_plan *plan, size_t *n, int *width_bits, 
 int mi_native_polymul_batch(const mi_native_plan *plan, void *prod, const void *lhs, const void *rhs, size_t batch,
                             void *stream);
 
+/* ---- LWE keyswitch (tfhe/src/core_crypto/algorithms/lwe_keyswitch.rs) ---------------------------
+ * The keyswitch in front of the PBS in the shortint KS-PBS order (PARAM_MESSAGE_2_CARRY_2:
+ * 2048 -> 918, base 2^4, 4 levels; shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/ks_pbs.rs:29-47).
+ * mi_lwe_ksk_create takes the reference's LweKeyswitchKey layout as a device pointer: in_dim blocks of
+ * `level` LWE ciphertexts of out_dim + 1 u64, levels stored as generate_lwe_keyswitch_key writes them
+ * (lwe_keyswitch_key_generation.rs:169-199), and prepares a private device copy (the caller's buffer
+ * may be freed afterwards).  MI_ERR_INVALID_ARG where SignedDecomposer::new would assert
+ * (base_log * level >= 64); MI_ERR_UNSUPPORTED when in_dim * level * ceil((base_log + 1) / 8) >= 2^17
+ * (beyond the exact int32 accumulation of the int8 matrix-core path). */
+typedef struct mi_lwe_ksk mi_lwe_ksk;
+int mi_lwe_ksk_create(const uint64_t *ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device,
+                      mi_lwe_ksk **out_key);
+int mi_lwe_ksk_destroy(mi_lwe_ksk *key);
+int mi_lwe_ksk_info(const mi_lwe_ksk *key, size_t *in_dim, size_t *out_dim, int *base_log, int *level);
+/* keyswitch_lwe_ciphertext_native_mod_compatible (lwe_keyswitch.rs:137-227) over a batch:
+ * lwe_out[b] (out_dim + 1 u64) = keyswitch(lwe_in[b] (in_dim + 1 u64)), native 2^64 modulus, bit-exact.
+ * Device pointers, async on `stream` (stream-ordered scratch, freed before return). */
+int mi_lwe_keyswitch_batch(const mi_lwe_ksk *key, uint64_t *lwe_out, const uint64_t *lwe_in, size_t batch,
+                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -362,3 +362,36 @@ def sample_extract(glwe, n, k, q=0):
     out = np.zeros(k * n + 1, np.uint64)
     _plib().ora_sample_extract(_ptr(_u(glwe)), _ptr(out), n, k, q)
     return out
+
+
+# ---- LWE keyswitch (ks_oracle.h) ---------------------------------------------------------
+_KS_SIGS = {
+    "ora_lwe_keyswitch": (None, [_p64, _sz, _sz, ctypes.c_int, ctypes.c_int, _p64, _p64]),
+    "ora_lwe_keyswitch_batch": (None, [_p64, _sz, _sz, ctypes.c_int, ctypes.c_int, _p64, _p64, _sz, ctypes.c_int]),
+}
+_ks_ready = False
+
+
+def _klib():
+    global _ks_ready
+    L = lib()
+    if not _ks_ready:
+        for name, (res, args) in _KS_SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _ks_ready = True
+    return L
+
+
+def lwe_keyswitch(ksk, lwe_in, out_dim, base_log, level, threads=8):
+    """keyswitch_lwe_ciphertext (lwe_keyswitch.rs:137-227) over a batch: lwe_in (..., in_dim + 1),
+    ksk (in_dim, level, out_dim + 1) -> (..., out_dim + 1)."""
+    k = _u(ksk)
+    x = _u(lwe_in)
+    in_dim = x.shape[-1] - 1
+    assert k.size == in_dim * level * (out_dim + 1), "ksk shape"
+    batch = x.size // (in_dim + 1)
+    out = np.zeros(x.shape[:-1] + (out_dim + 1,), np.uint64)
+    _klib().ora_lwe_keyswitch_batch(_ptr(k), in_dim, out_dim, base_log, level, _ptr(x), _ptr(out), batch, threads)
+    return out

@@ -163,3 +163,25 @@ def decode(pt, delta, msg_mod, q=0):
         v -= q
     d = (v + delta // 2) // delta
     return d % (2 * msg_mod)
+
+
+def lwe_encrypt_batch(g, pts, lwe_sk, noise_log2):
+    """Native-modulus LWE encryptions of a vector of plaintexts: rows (a, <a, s> + m + e) mod 2^64."""
+    pts = np.asarray(pts, dtype=np.uint64)
+    a = uniform_u64(g, (pts.size, lwe_sk.size))
+    with np.errstate(over="ignore"):
+        b = (a * lwe_sk[None, :]).sum(axis=1, dtype=np.uint64) + pts + tuniform(g, pts.size, noise_log2)
+    return np.concatenate([a, b[:, None]], axis=1)
+
+
+def ksk_gen(g, in_sk, out_sk, base_log, level, noise_log2):
+    """LWE keyswitch key (in_dim, level, out_dim + 1): block i, entry li encrypts
+    s_in[i] << (64 - base_log * (level - li)) under out_sk (lwe_keyswitch_key_generation.rs:169-199)."""
+    pts = np.array([(int(s) << (64 - base_log * (level - li))) % 2**64 for s in in_sk for li in range(level)],
+                   dtype=np.uint64)
+    return lwe_encrypt_batch(g, pts, out_sk, noise_log2).reshape(in_sk.size, level, out_sk.size + 1)
+
+
+def lwe_decrypt_batch(cts, lwe_sk):
+    with np.errstate(over="ignore"):
+        return cts[..., -1] - (cts[..., :-1] * lwe_sk).sum(axis=-1, dtype=np.uint64)

@@ -719,4 +719,89 @@ int mi_native_polymul_batch(const mi_native_plan* plan, void* prod, const void* 
   return st;
 }
 
+// ---- LWE keyswitch (tfhe/src/core_crypto/algorithms/lwe_keyswitch.rs:137-227) -----------------------
+
+struct mi_lwe_ksk {
+  int device = 0;
+  size_t in_dim = 0, out_dim = 0;
+  int base_log = 0, level = 0;
+  void* frag = nullptr;  // byte-plane MFMA fragments (keyswitch.hip)
+};
+
+int mi_lwe_ksk_create(const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device,
+                      mi_lwe_ksk** out_key) {
+  if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
+  *out_key = nullptr;
+  if (!ksk) return fail(MI_ERR_INVALID_ARG, "ksk is NULL");
+  if (in_dim == 0 || out_dim == 0 || in_dim > 0xFFFFFFull || out_dim > 0xFFFFFFull)
+    return fail(MI_ERR_INVALID_ARG, "lwe dimension out of range");
+  // SignedDecomposer::new (decomposer.rs): base_log * level < 64, both >= 1
+  if (base_log < 1 || level < 1 || base_log * level >= 64)
+    return fail(MI_ERR_INVALID_ARG, "decomposition base_log * level must be in [1, 63]");
+  // exact int32 accumulation on the int8 matrix cores: GEMM depth in_dim * level * bytes-per-digit < 2^17
+  if ((double)in_dim * level * mi::ks_digit_bytes_per_term(base_log) >= 131072.0)
+    return fail(MI_ERR_UNSUPPORTED, "in_dim * level * ceil((base_log + 1) / 8) must stay below 2^17");
+  mi_lwe_ksk* key = new (std::nothrow) mi_lwe_ksk;
+  if (!key) return fail(MI_ERR_OOM, "host allocation failed");
+  key->device = device;
+  key->in_dim = in_dim;
+  key->out_dim = out_dim;
+  key->base_log = base_log;
+  key->level = level;
+  DeviceGuard g(device);
+  if (!g.ok) {
+    delete key;
+    return fail(MI_ERR_INVALID_ARG, "bad device");
+  }
+  if (hipMalloc(&key->frag, mi::ks_key_bytes(in_dim, out_dim, base_log, level)) != hipSuccess) {
+    delete key;
+    return fail(MI_ERR_OOM, "keyswitch key allocation failed");
+  }
+  hipError_t e = mi::launch_ksk_prepare(key->frag, ksk, in_dim, out_dim, base_log, level, nullptr);
+  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+  if (e != hipSuccess) {
+    (void)hipFree(key->frag);
+    delete key;
+    return hip_fail(e, "keyswitch key preparation");
+  }
+  *out_key = key;
+  return MI_OK;
+}
+
+int mi_lwe_ksk_destroy(mi_lwe_ksk* key) {
+  if (!key) return MI_OK;
+  {
+    DeviceGuard g(key->device);
+    if (key->frag) (void)hipFree(key->frag);
+  }
+  delete key;
+  return MI_OK;
+}
+
+int mi_lwe_ksk_info(const mi_lwe_ksk* key, size_t* in_dim, size_t* out_dim, int* base_log, int* level) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (in_dim) *in_dim = key->in_dim;
+  if (out_dim) *out_dim = key->out_dim;
+  if (base_log) *base_log = key->base_log;
+  if (level) *level = key->level;
+  return MI_OK;
+}
+
+int mi_lwe_keyswitch_batch(const mi_lwe_ksk* key, uint64_t* lwe_out, const uint64_t* lwe_in, size_t batch,
+                           void* stream) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (batch == 0) return MI_OK;
+  if (!lwe_out || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x3FFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  const hipStream_t s = (hipStream_t)stream;
+  DeviceGuard g(key->device);
+  void* digits = nullptr;  // int8 digit fragments, stream-ordered scratch
+  if (hipMallocAsync(&digits, mi::ks_digit_bytes(key->in_dim, key->base_log, key->level, batch), s) != hipSuccess)
+    return fail(MI_ERR_OOM, "scratch allocation failed");
+  hipError_t e = mi::launch_keyswitch(lwe_out, lwe_in, key->frag, digits, batch, key->in_dim, key->out_dim,
+                                      key->base_log, key->level, s);
+  (void)hipFreeAsync(digits, s);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "keyswitch launch");
+}
+
 }  // extern "C"

@@ -69,6 +69,11 @@ _SIGS = {
     "mi_native_plan_destroy": (_int, [_vp]),
     "mi_native_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "mi_native_polymul_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+    "mi_lwe_ksk_create": (_int, [_vp, _sz, _sz, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "mi_lwe_ksk_destroy": (_int, [_vp]),
+    "mi_lwe_ksk_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_int),
+                               ctypes.POINTER(_int)]),
+    "mi_lwe_keyswitch_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None
