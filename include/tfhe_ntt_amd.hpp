@@ -1,0 +1,183 @@
+// tfhe_ntt_amd.hpp — header-only C++17 mirror of tfhe_ntt::prime64::Plan over the C ABI.
+//
+// The host-side surface a compiled caller binds (the reference is Rust; its toolchain is absent from
+// this image, so the compiled host mirror is C++).  Names, argument meaning and error behaviour follow
+// tfhe-ntt/src/prime64.rs (paths relative to /root/reference):
+//   Plan::try_new(n, p)          prime64.rs:764-862  -> std::optional<Plan> (nullopt where the reference
+//                                                       returns None; HIP failures throw tfhe_ntt_amd::Error)
+//   ntt_size() / modulus()       prime64.rs:870-878
+//   fwd / inv (&mut [u64])       prime64.rs:897-1046 -> host slices of exactly n values; a length mismatch
+//                                                       throws std::invalid_argument where the reference
+//                                                       panics on assert_eq! (prime64.rs:898, 976)
+//   normalize / mul_assign_normalize / mul_accumulate   prime64.rs:1050-1222 (host slices, same rule)
+// plus the batched device-pointer forms (`*_batch`, async on a hipStream_t passed as void*) that the
+// GPU path is built for.  The plan is immutable and may be shared by threads and streams; it is
+// move-only (the C handle is owned).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+#include "tfhe_ntt_amd.h"
+
+namespace tfhe_ntt_amd {
+
+class Error : public std::runtime_error {
+ public:
+  Error(int status, const std::string& what) : std::runtime_error(what), status_(status) {}
+  int status() const noexcept { return status_; }
+
+ private:
+  int status_;
+};
+
+inline void check(int status) {
+  if (status != MI_OK)
+    throw Error(status, std::string(mi_status_string(status)) + ": " + mi_last_error_message());
+}
+
+namespace prime64 {
+
+class Plan {
+ public:
+  // prime64.rs:764-862: None for N < 16 / not a power of two / p not prime / no 2N-th root
+  static std::optional<Plan> try_new(size_t polynomial_size, uint64_t modulus, int device = 0) {
+    mi_ntt64_plan* raw = nullptr;
+    const int st = mi_ntt64_plan_create(polynomial_size, modulus, device, &raw);
+    if (st == MI_ERR_INVALID_ARG || st == MI_ERR_NOT_PRIME || st == MI_ERR_NO_ROOT) return std::nullopt;
+    check(st);
+    return Plan(raw, polynomial_size, modulus);
+  }
+
+  Plan(Plan&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), n_(o.n_), p_(o.p_) {}
+  Plan& operator=(Plan&& o) noexcept {
+    if (this != &o) {
+      reset();
+      raw_ = std::exchange(o.raw_, nullptr);
+      n_ = o.n_;
+      p_ = o.p_;
+    }
+    return *this;
+  }
+  Plan(const Plan&) = delete;
+  Plan& operator=(const Plan&) = delete;
+  ~Plan() { reset(); }
+
+  size_t ntt_size() const noexcept { return n_; }
+  uint64_t modulus() const noexcept { return p_; }
+  const mi_ntt64_plan* raw() const noexcept { return raw_; }
+
+  // ---- host slices (&mut [u64] of exactly ntt_size() values) ----------------------------------
+  void fwd(uint64_t* buf, size_t len) const {
+    require(len);
+    check(mi_ntt64_fwd_host(raw_, buf, 1));
+  }
+  void inv(uint64_t* buf, size_t len) const {
+    require(len);
+    check(mi_ntt64_inv_host(raw_, buf, 1));
+  }
+  void normalize(uint64_t* buf, size_t len) const {
+    require(len);
+    DeviceBuffer d(n_, 1);
+    d.upload(0, buf);
+    check(mi_ntt64_normalize_batch(raw_, d.at(0), 1, n_, nullptr));
+    d.download(0, buf);
+  }
+  void mul_assign_normalize(uint64_t* lhs, size_t lhs_len, const uint64_t* rhs, size_t rhs_len) const {
+    require(lhs_len);
+    require(rhs_len);
+    DeviceBuffer d(n_, 2);
+    d.upload(0, lhs);
+    d.upload(1, rhs);
+    check(mi_ntt64_mul_assign_normalize_batch(raw_, d.at(0), d.at(1), 1, n_, nullptr));
+    d.download(0, lhs);
+  }
+  void mul_accumulate(uint64_t* acc, size_t acc_len, const uint64_t* lhs, size_t lhs_len, const uint64_t* rhs,
+                      size_t rhs_len) const {
+    require(acc_len);
+    require(lhs_len);
+    require(rhs_len);
+    DeviceBuffer d(n_, 3);
+    d.upload(0, acc);
+    d.upload(1, lhs);
+    d.upload(2, rhs);
+    check(mi_ntt64_mul_accumulate_batch(raw_, d.at(0), d.at(1), d.at(2), 1, n_, nullptr));
+    d.download(0, acc);
+  }
+
+  // ---- device batches (batch polynomials, `stride` u64 apart), async on `stream` ---------------
+  void fwd_batch(uint64_t* dev, size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_fwd_batch(raw_, dev, batch, stride, stream));
+  }
+  void inv_batch(uint64_t* dev, size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_inv_batch(raw_, dev, batch, stride, stream));
+  }
+  void normalize_batch(uint64_t* dev, size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_normalize_batch(raw_, dev, batch, stride, stream));
+  }
+  void mul_assign_normalize_batch(uint64_t* lhs, const uint64_t* rhs, size_t batch, size_t stride,
+                                  void* stream = nullptr) const {
+    check(mi_ntt64_mul_assign_normalize_batch(raw_, lhs, rhs, batch, stride, stream));
+  }
+  void mul_accumulate_batch(uint64_t* acc, const uint64_t* lhs, const uint64_t* rhs, size_t batch, size_t stride,
+                            void* stream = nullptr) const {
+    check(mi_ntt64_mul_accumulate_batch(raw_, acc, lhs, rhs, batch, stride, stream));
+  }
+
+ private:
+  Plan(mi_ntt64_plan* raw, size_t n, uint64_t p) : raw_(raw), n_(n), p_(p) {}
+  void reset() noexcept {
+    if (raw_) (void)mi_ntt64_plan_destroy(raw_);
+    raw_ = nullptr;
+  }
+  void require(size_t len) const {
+    if (len != n_)
+      throw std::invalid_argument("assertion `left == right` failed: slice length " + std::to_string(len) +
+                                  " != ntt_size " + std::to_string(n_));
+  }
+
+  // scratch for the host-slice pointwise ops: `count` polynomials on the plan's device, through the
+  // engine's own staging calls (mi_ntt64_*_host copy in / run / copy out for the transforms)
+  class DeviceBuffer {
+   public:
+    DeviceBuffer(size_t n, size_t count);
+    ~DeviceBuffer();
+    uint64_t* at(size_t i) const { return ptr_ + i * n_; }
+    void upload(size_t i, const uint64_t* src) const;
+    void download(size_t i, uint64_t* dst) const;
+
+   private:
+    uint64_t* ptr_ = nullptr;
+    size_t n_;
+  };
+
+  mi_ntt64_plan* raw_ = nullptr;
+  size_t n_ = 0;
+  uint64_t p_ = 0;
+};
+
+}  // namespace prime64
+}  // namespace tfhe_ntt_amd
+
+// The staging buffer uses the HIP runtime directly (the only HIP dependency of this header).
+#include <hip/hip_runtime_api.h>
+
+inline tfhe_ntt_amd::prime64::Plan::DeviceBuffer::DeviceBuffer(size_t n, size_t count) : n_(n) {
+  const hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr_), n * count * sizeof(uint64_t));
+  if (e != hipSuccess) throw Error(MI_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+}
+inline tfhe_ntt_amd::prime64::Plan::DeviceBuffer::~DeviceBuffer() {
+  if (ptr_) (void)hipFree(ptr_);
+}
+inline void tfhe_ntt_amd::prime64::Plan::DeviceBuffer::upload(size_t i, const uint64_t* src) const {
+  const hipError_t e = hipMemcpy(at(i), src, n_ * sizeof(uint64_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) throw Error(MI_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+}
+inline void tfhe_ntt_amd::prime64::Plan::DeviceBuffer::download(size_t i, uint64_t* dst) const {
+  const hipError_t e = hipMemcpy(dst, at(i), n_ * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) throw Error(MI_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+}
