@@ -32,6 +32,11 @@ SOLINAS_P = 0xFFFFFFFF00000001
 SEED = 0x74666865 + 2  # 0x74666865 + config id
 BYTES_PER_POLY_PASS = 2 * N * 8  # read 16 KiB + write 16 KiB per polynomial per transform
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Integer-VALU issue model of the generated bodies (tools/valu_cost.py: instruction mix x the issue
+# costs measured by tools/valu_probe.hip; tests/test_bench_contract.py keeps these in sync), and the
+# MI355X peak engine clock it is priced at.
+VALU_CYCLES = {"fwd": 15139.2, "inv": 17669.9, "pbs_step": 41776.5}
+SIMDS, PEAK_CLOCK_HZ = 256 * 4, 2.4e9
 # PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
 PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
 
@@ -47,6 +52,9 @@ def parse():
     ap.add_argument("--no-pbs", action="store_true", help="skip the config-4 PBS leg")
     ap.add_argument("--pbs-batch", type=int, default=PBS_BATCH)
     ap.add_argument("--pbs-steps", type=int, default=3)
+    # rehearsal of the multi-rank path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--same-device", action="store_true")
     return ap.parse_args()
 
 
@@ -182,6 +190,9 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
             "bound": "valu",
             "note": "integer VALU-bound (3,672 NTTs + 11.3 M modmul-class ops per PBS); per-step HBM "
                     "traffic is the L2-resident key plus 23.7 KB of LWE in/out per PBS",
+            "issue_cycles_per_wave_step": VALU_CYCLES["pbs_step"],
+            "model_ms": 2 * n_lwe * batch * VALU_CYCLES["pbs_step"] / SIMDS / PEAK_CLOCK_HZ * 1e3,
+            "frac": 2 * n_lwe * batch * VALU_CYCLES["pbs_step"] / SIMDS / PEAK_CLOCK_HZ * 1e3 / kernel_ms,
         },
         "cpu_baseline": None,
     }
@@ -284,11 +295,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        torch.cuda.set_device(0 if args.same_device else local)
+        dist.init_process_group(backend=args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    global SIMDS
+    SIMDS = torch.cuda.get_device_properties(dev).multi_processor_count * 4
 
     plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
     batch = args.batch
@@ -360,6 +373,13 @@ def main():
             "parallelism": f"independent shards x{world} (no data-path collective)",
         },
         "kernels": {"fwd_ms": fwd_ms, "inv_ms": inv_ms},
+        # the binding limit: integer VALU issue (SIMD cycles per launch at the peak clock vs measured)
+        "valu_bound": {
+            kind: {"issue_cycles_per_poly": VALU_CYCLES[kind],
+                   "model_ms": batch * VALU_CYCLES[kind] / SIMDS / PEAK_CLOCK_HZ * 1e3,
+                   "measured_ms": ms,
+                   "frac": batch * VALU_CYCLES[kind] / SIMDS / PEAK_CLOCK_HZ * 1e3 / ms}
+            for kind, ms in (("fwd", fwd_ms), ("inv", inv_ms))},
         "roofline": {
             "bound": "hbm",
             "kernel": f"ntt {dom}",

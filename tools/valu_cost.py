@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Issue-cycle model of the generated asm bodies: instruction mix x per-instruction issue cost.
+
+Costs are the MI355X measurements of tools/valu_probe.hip (cycles per wave-instruction per SIMD,
+8 waves/SIMD of independent instructions).  The model is what bench.py's
+"valu_bound" reports against: cycles per polynomial pass (transform) or per CMUX step (PBS body).
+
+  python tools/valu_cost.py        -> JSON {"fwd": cycles, "inv": cycles, "pbs_step": cycles}
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+COST = {  # cycles per wave-instruction (tools/valu_probe.hip on MI355X)
+    "v_add_u32": 2.35, "v_sub_u32": 2.34, "v_subrev_u32": 2.34, "v_xor_b32": 2.35, "v_mov_b32": 2.36,
+    "v_lshrrev_b32": 2.32, "v_lshlrev_b32": 2.32, "v_not_b32": 2.33, "v_and_b32": 2.35, "v_or_b32": 2.35,
+    "v_ashrrev_i32": 2.35,
+    "v_add3_u32": 4.26, "v_alignbit_b32": 4.30, "v_cndmask_b32_e64": 4.31, "v_mad_u64_u32": 4.56,
+    "v_mad_i64_i32": 4.56, "v_lshl_add_u64": 4.22, "v_mov_b64": 4.21, "v_lshrrev_b64": 4.24,
+    "v_lshlrev_b64": 4.24, "v_mul_hi_u32": 4.29, "v_mul_lo_u32": 4.31, "v_mul_u32_u24": 4.27,
+    "v_bfe_u32": 4.28, "v_bfi_b32": 4.28, "v_perm_b32": 4.27, "v_cmp_le_u32_e64": 4.52,
+    "v_add_co_u32_e64": 4.56, "v_addc_co_u32_e64": 4.57, "v_sub_co_u32_e64": 4.57, "v_subb_co_u32_e64": 4.57,
+    "v_mov_b32_dpp": 4.3,
+}
+
+
+def cycles(lines):
+    tot, unknown = 0.0, {}
+    for l in lines:
+        if not l.startswith("v_"):
+            continue
+        op = l.split()[0]
+        if op not in COST:
+            unknown[op] = unknown.get(op, 0) + 1
+            tot += 4.3
+        else:
+            tot += COST[op]
+    return tot, unknown
+
+
+def main():
+    import gen_pbs_kernel as P
+    import gen_tw_kernel as T
+    tabs = T.load_tables()
+    out = {}
+    for name, body in (("fwd", T.gen_fwd(tabs)), ("inv", T.gen_inv(tabs))):
+        out[name], unk = cycles(body.lines)
+        out[name + "_valu"] = body.nvalu
+        if unk:
+            out[name + "_unpriced"] = unk
+    b = P.gen_pbs(tabs)
+    out["pbs_step"], unk = cycles(b.lines)
+    out["pbs_step_valu"] = b.nvalu
+    if unk:
+        out["pbs_step_unpriced"] = unk
+    print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()
