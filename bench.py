@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-pbs", action="store_true", help="skip the config-4 PBS leg")
     ap.add_argument("--pbs-batch", type=int, default=PBS_BATCH)
     ap.add_argument("--pbs-steps", type=int, default=3)
+    ap.add_argument("--pbs-global", type=int, default=65536, help="config 5 global batch (N > 1 only)")
     # rehearsal of the multi-rank path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--same-device", action="store_true")
@@ -196,8 +197,72 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
         },
         "cpu_baseline": None,
     }
+    if dist is not None:
+        res["sharded"] = bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk)
     del key
     return res
+
+
+def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk):
+    """Config 5: one global batch of PBS (default 65,536) held on the root, scattered over the ranks,
+    bootstrapped, gathered back (strong scaling).  The transfers are grouped point-to-point sends from
+    the root (multi_gpu.scatter_batch / gather_batch: RCCL over xGMI, the root feeding each peer over
+    its own link); the key broadcast is timed once, outside the steady state."""
+    mg = eng.multi_gpu
+    n_lwe, G, K = PBS_N_LWE, args.pbs_global, args.pbs_steps
+    gloo = args.dist_backend == "gloo"  # rehearsal: gloo point-to-point needs host tensors
+    tdev = torch.device("cpu") if gloo else dev
+    a, b = mg.shard_bounds(G, world, rank)
+    mine = b - a
+    # key broadcast from the root (replicated read-only state, SURVEY.md 8e)
+    kb = bsk.to(tdev)
+    barrier()
+    t0 = time.perf_counter()
+    mg.broadcast_(kb, src=0)
+    torch.cuda.synchronize()
+    barrier()
+    bcast_s = mg.max_over_ranks(time.perf_counter() - t0, None if gloo else dev)
+    del kb
+    lwe_all = out_all = None
+    if rank == 0:
+        lwe_all = torch.empty((G, n_lwe + 1), dtype=torch.int64, device=dev)
+        eng.fill_uniform(lwe_all, SEED + 50, 0)
+        lwe_all = lwe_all.to(tdev)
+        out_all = torch.empty((G, N + 1), dtype=torch.int64, device=tdev)
+    shard_in = torch.empty((mine, n_lwe + 1), dtype=torch.int64, device=tdev)
+    shard_out = torch.empty((mine, N + 1), dtype=torch.int64, device=dev)
+    work_in = shard_in if not gloo else torch.empty((mine, n_lwe + 1), dtype=torch.int64, device=dev)
+
+    def step(transfer):
+        if transfer:
+            mg.scatter_batch(lwe_all, shard_in, src=0)
+            if gloo:
+                work_in.copy_(shard_in)
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(work_in, shard_out, lut, key)
+        if transfer:
+            mg.gather_batch(shard_out if not gloo else shard_out.cpu(), out_all, dst=0)
+
+    step(True)
+    torch.cuda.synchronize()
+    times = {}
+    for transfer in (False, True):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step(transfer)
+        torch.cuda.synchronize()
+        barrier()
+        times[transfer] = mg.max_over_ranks(time.perf_counter() - t0, None if gloo else dev)
+    return {"metric": "PBS/sec, one global batch sharded over the GPUs (config 5)",
+            "value": G * K / times[False], "unit": "PBS/s", "scaling": "strong",
+            "value_with_scatter_gather": G * K / times[True],
+            "ms_per_step": times[False] / K * 1e3, "ms_per_step_with_scatter_gather": times[True] / K * 1e3,
+            "key_broadcast_ms": bcast_s * 1e3,
+            "config": {"global_batch": G, "n_gpus": world, "shard": [a, b],
+                       "transfer": "gloo via host (rehearsal)" if gloo else
+                                   "RCCL grouped send/recv from rank 0 (xGMI)",
+                       "scatter_bytes": G * (n_lwe + 1) * 8, "gather_bytes": G * (N + 1) * 8}}
 
 
 def bench_ext_product(args, eng, torch, dev, world, barrier):
