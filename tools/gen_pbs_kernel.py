@@ -33,8 +33,8 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_tw_kernel as T  # noqa: E402
-from gen_tw_kernel import (JUNK, SG0, Addr, Body, MulSlot, Seg, X, free_blocks_except, gmul,  # noqa: E402
-                           pv)
+from gen_tw_kernel import (JUNK, SG0, Addr, Body, MulSlot, Seg, X, free_blocks_except,  # noqa: E402
+                           minus_eps, pv)
 
 ACC = 128
 VOFF = 192
@@ -190,17 +190,53 @@ def rotate_decompose(B):
         sched(B, sg)
 
 
-def add_canon(sg, m, a, b):
-    """a <- a + b mod p (both canonical), temps from multiply slot m."""
-    alo, ahi, _ = a
-    blo, bhi, _ = b
-    v, P, c = m.v, m.P, m.c
-    sg.add(f"v_add_co_u32_e64 {v[0]}, {c[0]}, {alo}, {blo}", [alo, blo], [v[0], c[0]])
-    sg.add(f"v_addc_co_u32_e64 {v[1]}, {c[1]}, {ahi}, {bhi}, {c[0]}", [ahi, bhi, c[0]], [v[1], c[1]])
-    sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, -1, 1, {P[0]}", [P[0]], [P[1], c[0]])
-    sg.add(f"s_or_b64 {c[0]}, {c[0]}, {c[1]}", [c[0], c[1]], [c[0], "scc"], "salu")
-    sg.add(f"v_cndmask_b32_e64 {alo}, {v[0]}, {v[2]}, {c[0]}", [v[0], v[2], c[0]], [alo])
-    sg.add(f"v_cndmask_b32_e64 {ahi}, {v[1]}, {v[3]}, {c[0]}", [v[1], v[3], c[0]], [ahi])
+def prod128(sg, ms, x, wlo, whi):
+    """Full 128-bit x * w (x, w < 2^64) in multiply slot ms: low 64 bits in (A0, C0) = ms.v[0], ms.v[4],
+    high 64 bits in the PB pair (ms.v[2:3]).  The slot's Z1h / Z2h must hold 0 (set once per MAC)."""
+    xlo, xhi, _ = x
+    v, P = ms.v, ms.P
+    PA, PB, PC, PD, Z1, Z2 = P
+    A1, B0, B1, C1, Z1l, Z2l = v[1], v[2], v[3], v[5], v[8], v[10]
+    sg.add(f"v_mad_u64_u32 {PA}, {JUNK}, {xlo}, {wlo}, 0", [xlo, wlo], [PA, JUNK])             # A = xl wl
+    sg.add(f"v_mov_b32 {Z1l}, {A1}", [A1], [Z1l])
+    sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {xlo}, {whi}, {Z1}", [xlo, whi, Z1], [PB, JUNK])      # B = xl wh + A1
+    sg.add(f"v_mov_b32 {Z2l}, {B0}", [B0], [Z2l])
+    sg.add(f"v_mov_b32 {Z1l}, {B1}", [B1], [Z1l])
+    sg.add(f"v_mad_u64_u32 {PC}, {JUNK}, {xhi}, {wlo}, {Z2}", [xhi, wlo, Z2], [PC, JUNK])      # C = xh wl + B0
+    sg.add(f"v_mad_u64_u32 {PD}, {JUNK}, {xhi}, {whi}, {Z1}", [xhi, whi, Z1], [PD, JUNK])      # D = xh wh + B1
+    sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {C1}, 1, {PD}", [C1, PD], [PB, JUNK])                # H = D + C1
+
+
+def mac2(sg, m1, m2, x, g1, p, g2):
+    """x <- (x * g1 + p * g2) mod p, canonical, with ONE reduction: both 128-bit products are summed
+    exactly (carry c out of bit 128; 2^128 = -2^32 mod p), then reduced as in gmul:
+    L + H0 * EPS - H1 - c * 2^32 (2^64 = EPS, 2^96 = -1).  33 VALU instead of 2 x 17 + 5."""
+    prod128(sg, m1, x, *g1)
+    prod128(sg, m2, p, *g2)
+    a, b = m1.v, m2.v
+    ca, cb = m1.c[0], m1.c[1]
+    cs = m2.c[0]
+    # (s0, s1, s2, s3) = (A0, C0, H) + (A0', C0', H'), carry out of bit 128 in cs
+    sg.add(f"v_add_co_u32_e64 {a[0]}, {cs}, {a[0]}, {b[0]}", [a[0], b[0]], [a[0], cs])
+    sg.add(f"v_addc_co_u32_e64 {a[4]}, {cs}, {a[4]}, {b[4]}, {cs}", [a[4], b[4], cs], [a[4], cs])
+    sg.add(f"v_addc_co_u32_e64 {a[2]}, {cs}, {a[2]}, {b[2]}, {cs}", [a[2], b[2], cs], [a[2], cs])
+    sg.add(f"v_addc_co_u32_e64 {a[3]}, {cs}, {a[3]}, {b[3]}, {cs}", [a[3], b[3], cs], [a[3], cs])
+    c2 = a[6]
+    sg.add(f"v_cndmask_b32_e64 {c2}, 0, 1, {cs}", [cs], [c2])
+    # T = (s0, s1) - (s3 + c * 2^32); a borrow adds p (T - EPS mod 2^64, no second wrap: T >= 2^64 - 2^33)
+    T = m2.P[3]
+    t0, t1 = b[6], b[7]
+    sg.add(f"v_sub_co_u32_e64 {t0}, {ca}, {a[0]}, {a[3]}", [a[0], a[3]], [t0, ca])
+    sg.add(f"v_subb_co_u32_e64 {t1}, {cb}, {a[4]}, {c2}, {ca}", [a[4], c2, ca], [t1, cb])
+    minus_eps(sg, b[10], cb, T)
+    # R = T + s2 * EPS, U = R + EPS; canonical result = (carry(R) | carry(U)) ? U : R
+    PA, PC = m1.P[0], m1.P[2]
+    sg.add(f"v_mad_u64_u32 {PA}, {ca}, {a[2]}, -1, {T}", [a[2], T], [PA, ca])
+    sg.add(f"v_mad_u64_u32 {PC}, {cb}, -1, 1, {PA}", [PA], [PC, cb])
+    sg.add(f"s_or_b64 {cb}, {cb}, {ca}", [cb, ca], [cb, "scc"], "salu")
+    xlo, xhi, _ = x
+    sg.add(f"v_cndmask_b32_e64 {xlo}, {a[0]}, {a[4]}, {cb}", [a[0], a[4], cb], [xlo])
+    sg.add(f"v_cndmask_b32_e64 {xhi}, {a[1]}, {a[5]}, {cb}", [a[1], a[5], cb], [xhi])
 
 
 def mac(B, dmap):
@@ -211,6 +247,8 @@ def mac(B, dmap):
     for b in free:
         regs += list(range(b, b + 8))
     ms = [MulSlot(regs[12 * i], SG0 + 6 * i) for i in range(4)]
+    # the zero high halves of the product addends, set once for the whole MAC (prod128)
+    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
     for c in range(8):
         B.raw(*[f"ds_read_b64 {pv(PBUF + 2 * k)}, v{V_PX} offset:{512 * (4 * c + k)}" for k in range(4)],
               f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt(0)")
@@ -221,9 +259,8 @@ def mac(B, dmap):
             m1, m2 = ms[(2 * k) % 4], ms[(2 * k + 1) % 4]
             x = X(dmap, r)
             pl, ph = f"v{PBUF + 2 * k}", f"v{PBUF + 2 * k + 1}"
-            gmul(sg, m1, x, f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}", x[0], x[1])
-            gmul(sg, m2, (pl, ph, pv(PBUF + 2 * k)), f"v{gb + 8 + 2 * k}", f"v{gb + 9 + 2 * k}", pl, ph)
-            add_canon(sg, m1, x, (pl, ph, pv(PBUF + 2 * k)))
+            mac2(sg, m1, m2, x, (f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}"), (pl, ph, pv(PBUF + 2 * k)),
+                 (f"v{gb + 8 + 2 * k}", f"v{gb + 9 + 2 * k}"))
         sched(B, sg)
         if c + 2 < 8:
             B.raw(*gload(c + 2))

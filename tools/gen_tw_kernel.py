@@ -345,14 +345,16 @@ def gs(sg, sl, a, b, S, ac=False, bc=False):
     return True
 
 
-def gmul(sg, ms, x, wlo, whi, olo, ohi):
-    """o = x * w canonical (x semi, w canonical), general 64x64 multiply (17 VALU)."""
+def gmul(sg, ms, x, wlo, whi, olo, ohi, zero_hi=True):
+    """o = x * w canonical (x semi, w canonical), general 64x64 multiply (17 VALU; 15 with
+    zero_hi=False, when the caller keeps the slot's Z1h / Z2h at 0 across a run of multiplies)."""
     xlo, xhi, _ = x
     v, P, c = ms.v, ms.P, ms.c
     PA, PB, PC, PD, Z1, Z2 = P
     A0, A1, B0, B1, C0, C1, D0, D1, Z1l, Z1h, Z2l, Z2h = v
-    sg.add(f"v_mov_b32 {Z1h}, 0", [], [Z1h])
-    sg.add(f"v_mov_b32 {Z2h}, 0", [], [Z2h])
+    if zero_hi:
+        sg.add(f"v_mov_b32 {Z1h}, 0", [], [Z1h])
+        sg.add(f"v_mov_b32 {Z2h}, 0", [], [Z2h])
     sg.add(f"v_mad_u64_u32 {PA}, {JUNK}, {xlo}, {wlo}, 0", [xlo, wlo], [PA, JUNK])
     sg.add(f"v_mov_b32 {Z1l}, {A1}", [A1], [Z1l])
     sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {xlo}, {whi}, {Z1}", [xlo, whi, Z1], [PB, JUNK])
@@ -428,14 +430,14 @@ class Body:
             op.idx = i
         self.out(sg.schedule())
 
-    def mulrows(self, dmap, rows, wregs, mslots):
+    def mulrows(self, dmap, rows, wregs, mslots, zero_hi=True):
         """x[r] = x[r] * w (general), w in wregs[k] (pair base)."""
         sg = Seg()
         for k, r in enumerate(rows):
             ms = mslots[k % len(mslots)]
             x = X(dmap, r)
             wb = wregs[k]
-            gmul(sg, ms, x, f"v{wb}", f"v{wb + 1}", x[0], x[1])
+            gmul(sg, ms, x, f"v{wb}", f"v{wb + 1}", x[0], x[1], zero_hi)
         for i, op in enumerate(sg.ops):
             op.idx = i
         self.out(sg.schedule())
@@ -677,10 +679,11 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
         return dmap
     # twist: 4 batches of 8 rows, table rows in v8..v23, 3 multiply slots in v24..v59
     ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
+    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])  # Z1h / Z2h for all 32 multiplies
     for bt in range(4):
         rows = list(range(8 * bt, 8 * bt + 8))
         B.raw(*[ad.tw_load(bt, k, 8 + 2 * k) for k in range(8)], ad.tw_wait)
-        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms)
+        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms, zero_hi=False)
     if stop == "twist":
         return dmap
     dmap = t1(B, dmap, 8, 64, ad)
@@ -728,10 +731,11 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR):
     for b in free:
         regs += list(range(b, b + 8))
     ms = [MulSlot(regs[16 + 12 * i], SG0 + 6 * i) for i in range((len(regs) - 16) // 12)]
+    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])  # Z1h / Z2h for all 32 multiplies
     for bt in range(4):
         rows = list(range(8 * bt, 8 * bt + 8))
         B.raw(*[ad.tw_load(bt, k, regs[2 * k]) for k in range(8)], ad.tw_wait)
-        B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms)
+        B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms, zero_hi=False)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
