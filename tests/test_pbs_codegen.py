@@ -70,3 +70,29 @@ def test_emulated_ext_product_matches_oracle(oracle, cmux):
     else:
         want = ctx.ext_product(out, ggsw, glwe, 1, 23, 1, bnf=True)
     assert np.array_equal(o.reshape(-1), want)
+
+
+@pytest.mark.parametrize("base_log", [23, 10, 31, 1])
+def test_emulated_decomposition_corners(oracle, base_log):
+    """The level-1 decomposition of the generated body on the rounding corners: the one unbalanced tie
+    (top B+1 bits = 1 0..0, i.e. x in [2^63, 2^63 + 2^(63-B))), the balanced tie just below it, the
+    extremes, and both neighbours of every corner; external product vs the oracle, bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_emu
+    plan, tf, ti = _tables(oracle)
+    n_inv = int(plan.n_inv)
+    ti_norm = [v * n_inv % P for v in ti[:N]] + ti[N:]
+    ctx = oracle.NttContext(N)
+    rnd = random.Random(base_log)
+    q = 1 << (63 - base_log)
+    corners = [1 << 63, (1 << 63) + 1, (1 << 63) + q - 1, (1 << 63) + q, (1 << 63) - 1, (1 << 63) - q,
+               (1 << 63) - q - 1, 0, 1, 2**64 - 1, 2**64 - q, q - 1, q, (1 << 62), (1 << 62) - 1]
+    vals = []
+    for c in corners:
+        vals += [(c + d) % 2**64 for d in (-1, 0, 1)]
+    glwe = np.array((vals * (2 * N // len(vals) + 1))[: 2 * N], dtype=np.uint64)
+    rnd.shuffle(glwe)
+    ggsw = np.array([rnd.randrange(P) for _ in range(4 * N)], dtype=np.uint64)
+    out = np.array([rnd.getrandbits(64) for _ in range(2 * N)], dtype=np.uint64)
+    _, o = asm_emu.run_ext(HDR, glwe, out, ggsw, tf + ti + ti_norm, base_log, False)
+    assert np.array_equal(o.reshape(-1), ctx.ext_product(out, ggsw, glwe, 1, base_log, 1, bnf=True))

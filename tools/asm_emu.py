@@ -174,6 +174,19 @@ class Wave:
         x, off, w = self.src32(a[1]), self.src32(a[2]) & np.uint64(31), self.src32(a[3]) & np.uint64(31)
         self.wv(self.vreg(a[0]), (x >> off) & ((np.uint64(1) << w) - np.uint64(1)))
 
+    def op_v_bfe_i32(self, a):
+        x, off, w = self.src32(a[1]), self.src32(a[2]) & np.uint64(31), self.src32(a[3]) & np.uint64(31)
+        f = ((x >> off) & ((np.uint64(1) << w) - np.uint64(1))).astype(np.int64)
+        sign = (f >> (w.astype(np.int64) - 1)) & 1
+        f = np.where((w > 0) & (sign == 1), f - (np.int64(1) << w.astype(np.int64)), f)
+        self.wv(self.vreg(a[0]), f.astype(np.uint64) & M32)
+
+    def op_v_sub_u32(self, a):
+        self.wv(self.vreg(a[0]), (self.src32(a[1]) - self.src32(a[2])) & M32)
+
+    def op_v_cmp_eq_u32_e64(self, a):
+        self.set_mask(a[0], self.src32(a[1]) == self.src32(a[2]))
+
     def op_v_cmp_le_u32_e64(self, a):
         self.set_mask(a[0], self.src32(a[1]) <= self.src32(a[2]))
 

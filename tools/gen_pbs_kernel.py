@@ -79,7 +79,7 @@ def prologue(B):
           # base-log constants: 31 - B, B - 1, 2^(B-1), 2^32 - 2^B + 1
           f"s_sub_u32 s{S_SH}, 31, %[bl]",
           f"s_lshl_b32 s{S_HALF}, 1, %[bl]",
-          f"s_sub_u32 s{S_K1}, 1, s{S_HALF}",
+          f"s_mov_b32 s{S_K1}, s{S_HALF}",
           f"s_sub_u32 s{S_BM1}, %[bl], 1",
           f"s_lshr_b32 s{S_HALF}, s{S_HALF}, 1",
           f"s_mov_b32 s{S_HLO}, 0x80000000",
@@ -135,22 +135,22 @@ def slots_at(bases):
 def decompose(sg, sl, xl, xh):
     """Level-1 signed decomposition of the native u64 (xl, xh) in place (closest representable +
     one balanced digit, decomposer.rs:156-185 + iter.rs:131-151), mapped into [0, p) (ntt64.rs:231-238).
-    With one level the digit equals the balanced state: res = round(x / 2^(64-B)) mod 2^B, minus 2^B
-    when the balancing bit is set."""
+    With t = the top B + 1 bits of x (rounding bit last) the reference's digit is
+    sext_B(((t + 1) >> 1) mod 2^B), except t == 2^B (res == 2^(B-1) with a clear rounding bit, the
+    one tie that is not balanced), where it is +2^(B-1) = -sext_B(...).  The signed digit d becomes
+    d mod p as the sign-extended pair (d, d >> 31) plus (-15 [d < 0]) * 0x11111111 = -EPS [d < 0]."""
     v, c = sl.v, sl.c
-    t, res, u, w, ln, hn = v[1], v[2], v[3], v[4], v[5], v[6]
+    t, s, nd, m = v[1], v[2], v[3], v[4]
     sg.add(f"v_lshrrev_b32 {t}, s{S_SH}, {xh}", [xh], [t])
-    sg.add(f"v_add_u32 {res}, 1, {t}", [t], [res])
-    sg.add(f"v_bfe_u32 {res}, {res}, 1, %[bl]", [res], [res])
-    sg.add(f"v_add_u32 {u}, -1, {res}", [res], [u])
-    sg.add(f"v_lshlrev_b32 {w}, s{S_BM1}, {t}", [t], [w])
-    sg.add(f"v_or_b32 {u}, {u}, {w}", [u, w], [u])
-    sg.add(f"v_and_b32 {u}, {u}, {res}", [u, res], [u])
-    sg.add(f"v_cmp_le_u32_e64 {c[2]}, s{S_HALF}, {u}", [u], [c[2]])
-    sg.add(f"v_add_co_u32_e64 {ln}, {c[0]}, s{S_K1}, {res}", [res], [ln, c[0]])
-    sg.add(f"v_addc_co_u32_e64 {hn}, {JUNK}, -2, 0, {c[0]}", [c[0]], [hn, JUNK])
-    sg.add(f"v_cndmask_b32_e64 {xl}, {res}, {ln}, {c[2]}", [res, ln, c[2]], [xl])
-    sg.add(f"v_cndmask_b32_e64 {xh}, 0, {hn}, {c[2]}", [hn, c[2]], [xh])
+    sg.add(f"v_add_u32 {s}, 1, {t}", [t], [s])
+    sg.add(f"v_bfe_i32 {xl}, {s}, 1, %[bl]", [s], [xl])
+    sg.add(f"v_cmp_eq_u32_e64 {c[2]}, s{S_K1}, {t}", [t], [c[2]])
+    sg.add(f"v_sub_u32 {nd}, 0, {xl}", [xl], [nd])
+    sg.add(f"v_cndmask_b32_e64 {xl}, {xl}, {nd}, {c[2]}", [xl, nd, c[2]], [xl])
+    sg.add(f"v_ashrrev_i32 {xh}, 31, {xl}", [xl], [xh])
+    sg.add(f"v_and_b32 {m}, -15, {xh}", [xh], [m])
+    xp = pv(int(xl[1:]))
+    sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
 
 
 def rotate_decompose(B):

@@ -20,7 +20,7 @@ COST = {  # cycles per wave-instruction (tools/valu_probe.hip on MI355X)
     "v_add3_u32": 4.26, "v_alignbit_b32": 4.30, "v_cndmask_b32_e64": 4.31, "v_mad_u64_u32": 4.56,
     "v_mad_i64_i32": 4.56, "v_lshl_add_u64": 4.22, "v_mov_b64": 4.21, "v_lshrrev_b64": 4.24,
     "v_lshlrev_b64": 4.24, "v_mul_hi_u32": 4.29, "v_mul_lo_u32": 4.31, "v_mul_u32_u24": 4.27,
-    "v_bfe_u32": 4.28, "v_bfi_b32": 4.28, "v_perm_b32": 4.27, "v_cmp_le_u32_e64": 4.52,
+    "v_bfe_u32": 4.28, "v_bfe_i32": 4.28, "v_cmp_eq_u32_e64": 4.52, "v_bfi_b32": 4.28, "v_perm_b32": 4.27, "v_cmp_le_u32_e64": 4.52,
     "v_add_co_u32_e64": 4.56, "v_addc_co_u32_e64": 4.57, "v_sub_co_u32_e64": 4.57, "v_subb_co_u32_e64": 4.57,
     "v_mov_b32_dpp": 4.3,
 }
