@@ -337,6 +337,70 @@ def bench_keyswitch(args, eng, torch, dev, world, barrier):
                          "note": "digit pass + i8 MFMA GEMM (8 byte planes) per step"}}
 
 
+def bench_ks_pbs(args, eng, torch, dev, world, barrier):
+    """The shortint KS-PBS order end to end on one stream: big LWE (k N + 1 = 2049) -> keyswitch
+    (2048 -> 918, B 2^4, 4 levels) -> BNF PBS (n = 918) -> big LWE, both keys resident."""
+    KS, M = eng.lwe_keyswitch, eng.ntt64_pbs
+    batch, n_lwe = args.pbs_batch, PBS_N_LWE
+    ksk = torch.empty((KS_IN, KS_LEVEL, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ksk, SEED + 40, 0)
+    kkey = KS.LweKeyswitchKey(ksk, KS_BASE_LOG, KS_LEVEL)
+    del ksk
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    bsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 10, SOLINAS_P)
+    bkey = M.NttBootstrapKey(plan, bsk, PBS_BASE_LOG, PBS_LEVEL, M.BNF)
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 11, 0)
+    big = torch.empty((batch, KS_IN + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(big, SEED + 42, 0)
+    small = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+
+    def run():
+        KS.keyswitch_lwe_ciphertext(kkey, big, small)
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(small, out, lut, bkey)
+
+    run()
+    torch.cuda.synchronize()
+    K = args.pbs_steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    del bkey, kkey
+    return {"metric": "KS-PBS/sec (keyswitch then PBS, PARAM_MESSAGE_2_CARRY_2 shape)",
+            "value": world * batch * K / el, "unit": "KS-PBS/s", "ms_per_step": el / K * 1e3, "steps": K,
+            "config": {"workload": "keyswitch_lwe_ciphertext 2048 -> 918 (B 2^4, L 4) then "
+                                   "programmable_bootstrap_ntt64_bnf (n 918, N 2048, B 2^23, L 1), one stream",
+                       "batch_per_gpu": batch}}
+
+
+def cpu_baseline_ks(seconds: float):
+    """Oracle restatement of keyswitch_lwe_ciphertext_native_mod_compatible, OpenMP over ciphertexts."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    ksk = O.fill_uniform(SEED + 40, 0, KS_IN * KS_LEVEL * (PBS_N_LWE + 1))
+    sample = threads * 4
+    lwe = O.fill_uniform(SEED + 41, 0, sample * (KS_IN + 1)).reshape(sample, KS_IN + 1)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.lwe_keyswitch(ksk, lwe, PBS_N_LWE, KS_BASE_LOG, KS_LEVEL, threads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": reps * sample / el, "unit": "KS/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {sample} keyswitches 2048 -> 918 (B 2^4, L 4) in {el:.1f}s, restatement of "
+                      f"lwe_keyswitch.rs:137-227, OpenMP {threads} threads"}
+
+
 def load_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*/pmc_traffic.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -367,6 +431,10 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     global SIMDS
     SIMDS = torch.cuda.get_device_properties(dev).multi_processor_count * 4
+    # every leg runs on a dedicated stream: on the legacy default stream each dependent launch costs
+    # ~5 us more (tools/graph_probe.py: 150 vs ~160 us per fwd+inv step)
+    work = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(work)
 
     plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
     batch = args.batch
@@ -409,6 +477,25 @@ def main():
     e2.record()
     torch.cuda.synchronize()
     fwd_ms = e0.elapsed_time(e1) / K
+    # the same K steps launched as one hipGraph (captured outside the timed region): what a pipeline
+    # that replays a fixed transform sequence gets; reported beside, not instead of, the per-call rate
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=work):
+        for k in range(K):
+            plan.fwd(buf)
+            plan.inv(buf)
+    graph.replay()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    graph.replay()
+    torch.cuda.synchronize()
+    barrier()
+    graph_el = time.perf_counter() - t0
+    if dist is not None:
+        graph_el = eng.multi_gpu.max_over_ranks(graph_el, dev)
+    del graph
     inv_ms = e1.elapsed_time(e2) / K
     dom_ms = max(fwd_ms, inv_ms)
     dom = "fwd" if fwd_ms >= inv_ms else "inv"
@@ -438,6 +525,8 @@ def main():
             "parallelism": f"independent shards x{world} (no data-path collective)",
         },
         "kernels": {"fwd_ms": fwd_ms, "inv_ms": inv_ms},
+        "graph_replay": {"value": world * batch * K / graph_el, "ms_per_step": graph_el / K * 1e3,
+                         "note": "the K timed steps captured as one hipGraph and replayed once"},
         # the binding limit: integer VALU issue (SIMD cycles per launch at the peak clock vs measured)
         "valu_bound": {
             kind: {"issue_cycles_per_poly": VALU_CYCLES[kind],
@@ -461,13 +550,12 @@ def main():
         out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
-        ks_ms, pbs_ms = out["keyswitch"]["ms_per_step"], out["pbs"]["ms_per_step"]
-        out["ks_pbs"] = {"metric": "KS-PBS/sec (keyswitch then PBS, PARAM_MESSAGE_2_CARRY_2 shape)",
-                         "value": world * args.pbs_batch / ((ks_ms + pbs_ms) * 1e-3), "unit": "KS-PBS/s"}
+        out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_pbs:
             out["pbs"]["cpu_baseline"] = cpu_baseline_pbs(min(args.cpu_seconds, 10.0))
+            out["keyswitch"]["cpu_baseline"] = cpu_baseline_ks(min(args.cpu_seconds, 5.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
