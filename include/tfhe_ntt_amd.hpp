@@ -161,6 +161,93 @@ class Plan {
 };
 
 }  // namespace prime64
+
+// ---- core_crypto consumers (tfhe/src/core_crypto, device pointers, async on `stream`) ----------
+// The reference works on one ciphertext per call; every function here takes a leading batch.
+// Layouts as in tfhe_ntt_amd.h.  Variants: MI_NTT64_SOLINAS / MI_NTT64_BNF.
+namespace core_crypto {
+
+// algorithms/lwe_bootstrap_key_conversion.rs:294-365 (Raw: normalize = false)
+inline void convert_standard_lwe_bootstrap_key_to_ntt64(const prime64::Plan& plan, const uint64_t* bsk_std,
+                                                        uint64_t* bsk_ntt, size_t n_polys, unsigned in_modulus_width,
+                                                        bool normalize, void* stream = nullptr) {
+  check(mi_bsk_to_ntt64(plan.raw(), bsk_std, bsk_ntt, n_polys, in_modulus_width, normalize ? 1 : 0, stream));
+}
+
+// ntt64_pbs.rs:553-663 / ntt64_bnf_pbs.rs:541-681: out[b] += GGSW (.) glwe[b]
+inline void add_external_product_ntt64_assign(const prime64::Plan& plan, uint64_t* out, const uint64_t* glwe,
+                                              const uint64_t* ggsw_ntt, int base_log, int level, size_t batch,
+                                              int variant, void* stream = nullptr) {
+  check(mi_ext_product_ntt64_batch(plan.raw(), out, glwe, ggsw_ntt, 1, base_log, level, batch, variant, stream));
+}
+
+// ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705 (ct1 is left holding ct1 - ct0, as the reference)
+inline void cmux_ntt64_assign(const prime64::Plan& plan, uint64_t* ct0, uint64_t* ct1, const uint64_t* ggsw_ntt,
+                              int base_log, int level, size_t batch, int variant, void* stream = nullptr) {
+  check(mi_cmux_ntt64_batch(plan.raw(), ct0, ct1, ggsw_ntt, 1, base_log, level, batch, variant, stream));
+}
+
+// An NTT-domain bootstrap key bound to a plan (entities/ntt_lwe_bootstrap_key.rs); move-only.
+class NttBootstrapKey {
+ public:
+  NttBootstrapKey(const prime64::Plan& plan, const uint64_t* bsk_ntt, size_t n_lwe, int base_log, int level,
+                  int variant)
+      : n_lwe_(n_lwe), variant_(variant) {
+    check(mi_pbs_ntt64_key_create(plan.raw(), bsk_ntt, n_lwe, 1, base_log, level, variant, &raw_));
+  }
+  NttBootstrapKey(NttBootstrapKey&& o) noexcept
+      : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_), variant_(o.variant_) {}
+  NttBootstrapKey(const NttBootstrapKey&) = delete;
+  NttBootstrapKey& operator=(const NttBootstrapKey&) = delete;
+  ~NttBootstrapKey() {
+    if (raw_) (void)mi_pbs_ntt64_key_destroy(raw_);
+  }
+  const mi_pbs_ntt64_key* raw() const noexcept { return raw_; }
+  size_t input_lwe_dimension() const noexcept { return n_lwe_; }
+  int variant() const noexcept { return variant_; }
+
+ private:
+  mi_pbs_ntt64_key* raw_ = nullptr;
+  size_t n_lwe_;
+  int variant_;
+};
+
+// programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized (ntt64_pbs.rs:482-538,
+// ntt64_bnf_pbs.rs:469-540): lwe_out[b] (k N + 1) = PBS(lwe_in[b] (n + 1)) with the accumulator `lut`
+inline void programmable_bootstrap_ntt64_lwe_ciphertext(const NttBootstrapKey& key, const uint64_t* lwe_in,
+                                                        uint64_t* lwe_out, const uint64_t* lut, size_t batch,
+                                                        int ms_mode = MI_MS_STANDARD, void* stream = nullptr) {
+  check(mi_pbs_ntt64_batch(key.raw(), lwe_out, lwe_in, lut, batch, ms_mode, stream));
+}
+
+// entities/lwe_keyswitch_key.rs + algorithms/lwe_keyswitch.rs:103-227 (native modulus); move-only
+class LweKeyswitchKey {
+ public:
+  LweKeyswitchKey(const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device = 0)
+      : in_(in_dim), out_(out_dim) {
+    check(mi_lwe_ksk_create(ksk, in_dim, out_dim, base_log, level, device, &raw_));
+  }
+  LweKeyswitchKey(LweKeyswitchKey&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), in_(o.in_), out_(o.out_) {}
+  LweKeyswitchKey(const LweKeyswitchKey&) = delete;
+  LweKeyswitchKey& operator=(const LweKeyswitchKey&) = delete;
+  ~LweKeyswitchKey() {
+    if (raw_) (void)mi_lwe_ksk_destroy(raw_);
+  }
+  const mi_lwe_ksk* raw() const noexcept { return raw_; }
+  size_t input_key_lwe_dimension() const noexcept { return in_; }
+  size_t output_key_lwe_dimension() const noexcept { return out_; }
+
+ private:
+  mi_lwe_ksk* raw_ = nullptr;
+  size_t in_, out_;
+};
+
+inline void keyswitch_lwe_ciphertext(const LweKeyswitchKey& key, const uint64_t* lwe_in, uint64_t* lwe_out,
+                                     size_t batch, void* stream = nullptr) {
+  check(mi_lwe_keyswitch_batch(key.raw(), lwe_out, lwe_in, batch, stream));
+}
+
+}  // namespace core_crypto
 }  // namespace tfhe_ntt_amd
 
 // The staging buffer uses the HIP runtime directly (the only HIP dependency of this header).

@@ -1,0 +1,140 @@
+// test_core_crypto.cpp — the C++ core_crypto mirror (include/tfhe_ntt_amd.hpp, namespace core_crypto)
+// against the CPU oracle (oracle/ks_oracle.c, pbs_oracle.c: restatements of the reference, linked
+// here only as the checker), bit for bit, on seeded random keys and ciphertexts:
+//   convert_standard_lwe_bootstrap_key_to_ntt64   lwe_bootstrap_key_conversion.rs:294-365 (Raw)
+//   add_external_product_ntt64_assign (BNF)        ntt64_bnf_pbs.rs:541-681
+//   programmable_bootstrap_ntt64_lwe_ciphertext    ntt64_bnf_pbs.rs:469-540 (standard modulus switch)
+//   keyswitch_lwe_ciphertext                       lwe_keyswitch.rs:137-227 (2048 -> 918, B 2^4, L 4)
+// Needs a HIP device.  Build: make -C tests/cpp.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "tfhe_ntt_amd.hpp"
+
+extern "C" {
+#include "../../oracle/ks_oracle.h"
+#include "../../oracle/ntt_oracle.h"
+#include "../../oracle/pbs_oracle.h"
+}
+
+namespace cc = tfhe_ntt_amd::core_crypto;
+using tfhe_ntt_amd::prime64::Plan;
+
+static int g_failures = 0;
+#define EXPECT(cond)                                                                        \
+  do {                                                                                      \
+    if (!(cond)) {                                                                          \
+      std::fprintf(stderr, "%s:%d: expectation failed: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failures;                                                                         \
+    }                                                                                       \
+  } while (0)
+
+static const uint64_t P = 0xFFFFFFFF00000001ull;
+static const size_t N = 2048;
+
+struct Dev {  // a device copy of a host vector
+  uint64_t* p = nullptr;
+  size_t n = 0;
+  explicit Dev(const std::vector<uint64_t>& h) : n(h.size()) {
+    if (hipMalloc(reinterpret_cast<void**>(&p), n * 8) != hipSuccess ||
+        hipMemcpy(p, h.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess)
+      throw std::runtime_error("device copy failed");
+  }
+  explicit Dev(size_t count) : n(count) {
+    if (hipMalloc(reinterpret_cast<void**>(&p), n * 8) != hipSuccess || hipMemset(p, 0, n * 8) != hipSuccess)
+      throw std::runtime_error("device allocation failed");
+  }
+  ~Dev() { (void)hipFree(p); }
+  std::vector<uint64_t> host() const {
+    std::vector<uint64_t> h(n);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h.data(), p, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      throw std::runtime_error("device read failed");
+    return h;
+  }
+};
+
+static std::vector<uint64_t> uniform(uint64_t seed, uint64_t p, size_t count) {
+  std::vector<uint64_t> v(count);
+  ora_fill_uniform(seed, p, v.data(), count);
+  return v;
+}
+
+int main() {
+  std::vector<uint64_t> twid(N), itwid(N);
+  uint64_t n_inv = 0;
+  EXPECT(ora_plan_init(N, P, twid.data(), itwid.data(), &n_inv));
+  const ora_ntt_tables tabs{N, P, twid.data(), itwid.data(), n_inv};
+  auto plan = Plan::try_new(N, P);
+  EXPECT(plan.has_value());
+  if (!plan) return 1;
+
+  // key conversion (Raw) of a native-modulus standard key, n_lwe = 16
+  const size_t n_lwe = 16, polys = n_lwe * 4;
+  const auto bsk_std = uniform(101, 0, polys * N);
+  std::vector<uint64_t> bsk_ref(polys * N);
+  ora_bsk_to_ntt(&tabs, bsk_std.data(), bsk_ref.data(), polys, 64, 0);
+  Dev d_std(bsk_std), d_ntt(polys * N);
+  cc::convert_standard_lwe_bootstrap_key_to_ntt64(*plan, d_std.p, d_ntt.p, polys, 64, false);
+  EXPECT(d_ntt.host() == bsk_ref);
+
+  // external product, BNF, level 1, base 2^23, batch 2
+  {
+    const size_t batch = 2;
+    const auto ggsw = uniform(102, P, 4 * N), glwe = uniform(103, 0, batch * 2 * N), out = uniform(104, 0, batch * 2 * N);
+    std::vector<uint64_t> want(out);
+    for (size_t b = 0; b < batch; ++b)
+      ora_ext_product_bnf(&tabs, 1, 23, 1, want.data() + b * 2 * N, ggsw.data(), glwe.data() + b * 2 * N);
+    Dev d_g(ggsw), d_in(glwe), d_out(out);
+    cc::add_external_product_ntt64_assign(*plan, d_out.p, d_in.p, d_g.p, 23, 1, batch, MI_NTT64_BNF);
+    EXPECT(d_out.host() == want);
+  }
+
+  // PBS, BNF, level 1, base 2^23, batch 3, on the converted key
+  {
+    const size_t batch = 3;
+    const auto lut = uniform(105, 0, 2 * N), lwe = uniform(106, 0, batch * (n_lwe + 1));
+    std::vector<uint64_t> want(batch * (N + 1));
+    for (size_t b = 0; b < batch; ++b)
+      ora_pbs_bnf(&tabs, 1, 23, 1, want.data() + b * (N + 1), lwe.data() + b * (n_lwe + 1), lut.data(),
+                  bsk_ref.data(), n_lwe);
+    cc::NttBootstrapKey key(*plan, d_ntt.p, n_lwe, 23, 1, MI_NTT64_BNF);
+    Dev d_lut(lut), d_lwe(lwe), d_out(batch * (N + 1));
+    cc::programmable_bootstrap_ntt64_lwe_ciphertext(key, d_lwe.p, d_out.p, d_lut.p, batch);
+    EXPECT(d_out.host() == want);
+  }
+
+  // keyswitch 2048 -> 918, base 2^4, 4 levels (PARAM_MESSAGE_2_CARRY_2), batch 5
+  {
+    const size_t in_dim = 2048, out_dim = 918, batch = 5;
+    const int bl = 4, lv = 4;
+    const auto ksk = uniform(107, 0, in_dim * lv * (out_dim + 1)), lwe = uniform(108, 0, batch * (in_dim + 1));
+    std::vector<uint64_t> want(batch * (out_dim + 1));
+    ora_lwe_keyswitch_batch(ksk.data(), in_dim, out_dim, bl, lv, lwe.data(), want.data(), batch, 4);
+    Dev d_ksk(ksk), d_lwe(lwe), d_out(batch * (out_dim + 1));
+    cc::LweKeyswitchKey key(d_ksk.p, in_dim, out_dim, bl, lv);
+    cc::keyswitch_lwe_ciphertext(key, d_lwe.p, d_out.p, batch);
+    EXPECT(d_out.host() == want);
+  }
+
+  // errors surface as tfhe_ntt_amd::Error with the C status (base_log * level >= 64)
+  {
+    bool threw = false;
+    try {
+      Dev d(8 * 8 * 11);
+      cc::LweKeyswitchKey bad(d.p, 8, 10, 8, 8);
+    } catch (const tfhe_ntt_amd::Error& e) {
+      threw = e.status() == MI_ERR_INVALID_ARG;
+    }
+    EXPECT(threw);
+  }
+
+  if (g_failures) {
+    std::fprintf(stderr, "%d expectation(s) failed\n", g_failures);
+    return 1;
+  }
+  std::printf("test_core_crypto: all tests passed\n");
+  return 0;
+}

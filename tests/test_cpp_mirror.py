@@ -48,3 +48,13 @@ def test_mirror_reference_suite_on_gpu():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "all tests passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_core_crypto_mirror_on_gpu():
+    """C++ core_crypto mirror (key conversion, external product, PBS, keyswitch) vs the oracle."""
+    exe = os.path.join(CPP, "test_core_crypto")
+    assert os.path.exists(exe), "tests/cpp/test_core_crypto must be built beforehand (__graft_entry__.build())"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "all tests passed" in r.stdout
