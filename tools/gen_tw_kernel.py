@@ -712,7 +712,7 @@ def gen_fwd(tabs, stop=None):
     if stop:
         B.raw(*store_raw(dmap))
         return B
-    B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    B.raw(*store_rows(dmap, S_GB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
 
 
@@ -758,7 +758,7 @@ def gen_inv(tabs, stop=None):
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     dmap = inv_core(B, tabs, dmap)
-    B.raw(*store_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    B.raw(*store_rows(dmap, S_GB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
 
 
