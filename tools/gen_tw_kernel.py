@@ -510,6 +510,7 @@ class Addr:
     def __init__(self, tw_load, **regs):
         self.tw_load = tw_load    # (batch bt, row k, dst pair base) -> load line of table row 8 bt + k
         self.tw_wait = "s_waitcnt vmcnt(0)"
+        self.tw_wait_n = lambda n: f"s_waitcnt vmcnt({n})"   # at most n younger table loads outstanding
         # (dst pair base, table entry k) -> load line of the lane's pair-stage twiddle k (+16 odd lanes)
         self.lw_load = lambda dst, k: f"global_load_dwordx2 {pv(dst)}, {self.lwo}, {self.lw} offset:{8 * k}"
         self.__dict__.update(regs)
@@ -669,6 +670,21 @@ def store_raw(dmap):
     return store_rows(dmap, S_GB) + ["s_waitcnt vmcnt(0)"]
 
 
+def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None):
+    """x[r] *= table row r (general multiplies) for the 32 registers, in 4 batches of 8 rows; the next
+    batch's 8 table rows are loaded into the other buffer before this batch multiplies, so the table
+    latency (L2 or LDS) hides behind the multiplies.  The slots' zero addend halves are set once."""
+    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
+    buf = (lambda i, k: bufs[i] + 2 * k) if contiguous else (lambda i, k: regs[16 * i + 2 * k])
+    B.raw(*[ad.tw_load(0, k, buf(0, k)) for k in range(8)])
+    for bt in range(4):
+        if bt + 1 < 4:
+            B.raw(*[ad.tw_load(bt + 1, k, buf((bt + 1) % 2, k)) for k in range(8)], ad.tw_wait_n(8))
+        else:
+            B.raw(ad.tw_wait)
+        B.mulrows(dmap, list(range(8 * bt, 8 * bt + 8)), [buf(bt % 2, k) for k in range(8)], ms, zero_hi=False)
+
+
 def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
     """Forward transform of the W0 data in dmap (must be v64..v127); returns the output dmap (W0,
     canonical).  With `stop`, returns early (debug bodies)."""
@@ -677,13 +693,9 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
         B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
     if stop == "g1":
         return dmap
-    # twist: 4 batches of 8 rows, table rows in v8..v23, 3 multiply slots in v24..v59
-    ms = [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(3)]
-    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])  # Z1h / Z2h for all 32 multiplies
-    for bt in range(4):
-        rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[ad.tw_load(bt, k, 8 + 2 * k) for k in range(8)], ad.tw_wait)
-        B.mulrows(dmap, rows, [8 + 2 * k for k in range(8)], ms, zero_hi=False)
+    # twist: 4 batches of 8 rows; table rows double-buffered in v8..v23 / v48..v63 (batch bt + 1
+    # loads while batch bt multiplies), 2 multiply slots in v24..v47
+    twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)])
     if stop == "twist":
         return dmap
     dmap = t1(B, dmap, 8, 64, ad)
@@ -730,12 +742,9 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR):
     regs = []
     for b in free:
         regs += list(range(b, b + 8))
-    ms = [MulSlot(regs[16 + 12 * i], SG0 + 6 * i) for i in range((len(regs) - 16) // 12)]
-    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])  # Z1h / Z2h for all 32 multiplies
-    for bt in range(4):
-        rows = list(range(8 * bt, 8 * bt + 8))
-        B.raw(*[ad.tw_load(bt, k, regs[2 * k]) for k in range(8)], ad.tw_wait)
-        B.mulrows(dmap, rows, [regs[2 * k] for k in range(8)], ms, zero_hi=False)
+    assert len(regs) >= 56, len(regs)
+    twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(regs[32 + 12 * i], SG0 + 6 * i) for i in range(2)],
+               contiguous=False, regs=regs)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
@@ -775,6 +784,7 @@ PIPE_SGPR_CLOBBER = SGPR_CLOBBER + list(range(94, 100))
 LDS_ADDR = Addr(lambda bt, k, dst: f"ds_read_b64 {pv(dst)}, %[twl] offset:{512 * (8 * bt + k)}",
                 **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r")})
 LDS_ADDR.tw_wait = "s_waitcnt lgkmcnt(0)"
+LDS_ADDR.tw_wait_n = lambda n: f"s_waitcnt lgkmcnt({n})"
 # pair-stage table: 32 entries after the 2048 twist rows; lane parity selects entries 16..31
 LDS_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, %[lwl] offset:{8 * k}"
 
