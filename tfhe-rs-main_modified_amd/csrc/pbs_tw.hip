@@ -54,6 +54,13 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
   return total_half - (u64)(total_hed / 2) - (1ull << (64u - LOG_MOD - 1u));
 }
 
+// The lane-pair twiddles of the forward and inverse transforms (tab[N..N+31], tab[2N+32+..]: the
+// same for the plain and the N^-1-folded inverse tables) into LDS, read by the body's pair stage.
+__device__ __forceinline__ void load_lane_pair_tables(u64* lwtab, const u64* __restrict__ tab, int t) {
+  if (t < 64) lwtab[t] = t < 32 ? tab[N + t] : tab[2 * N + 32 + (t - 32)];
+  __syncthreads();
+}
+
 // lwe_in: batch x (n+1); lut: 2 x N; bsk: n x 2 x 2 x N (NTT domain, N^-1 folded in);
 // tab: [fwd twist (N) | fwd lane-pair twiddles (32) | inverse twist (N) | inverse lane-pair (32) | ...].
 __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
@@ -61,12 +68,14 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
                                                      uint32_t n_lwe, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab, int centered) {
   __shared__ u64 buf[2 * N];
+  __shared__ u64 lwtab[64];
   const int t = threadIdx.x;
   const uint32_t lane = t & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;  // uniform per workgroup
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
+  load_lane_pair_tables(lwtab, tab, t);  // ends with a workgroup barrier
   u64 body_corr = 0;
   if (centered) body_corr = centered_body_correction(lwe, n_lwe, t, buf);
 
@@ -82,7 +91,8 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   MI_PBS_BODY_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [lut_lo] "s"(lut_lo), [lut_hi] "s"(lut_hi),
                      [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi), [gpar_lo] "s"(gpar_lo),
                      [gpar_hi] "s"(gpar_hi), [lwe_lo] "s"(lwe_lo), [lwe_hi] "s"(lwe_hi), [n] "s"(n_lwe),
-                     [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log));
+                     [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log),
+                     [LW] "s"((uint32_t)(uintptr_t)lwtab));
   // buf[w N + e] = acc_w[e].  Final rotation by -ms(b) (ntt64_bnf_pbs.rs:262-270), then sample
   // extraction at nth = 0 (glwe_sample_extraction.rs:89-160): out[0] = A'[0], out[j] = -A'[N - j].
   const u64* acc = buf + w * N;
@@ -111,10 +121,12 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
                                                      const u64* __restrict__ ggsw, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab) {
   __shared__ u64 buf[2 * N];
+  __shared__ u64 lwtab[64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;
+  load_lane_pair_tables(lwtab, tab, threadIdx.x);
   const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
   u64* o = out + ((size_t)b * 2 + w) * N;
   u64* g = glwe + ((size_t)b * 2 + w) * N;
@@ -129,12 +141,12 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
     MI_PBS_BODY_CMUX_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
                             [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
                             [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
-                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log));
+                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
   else
     MI_PBS_BODY_EXT_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
                            [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
                            [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
-                           [tab_hi] "s"(tab_hi), [bl] "s"(base_log));
+                           [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
 }
 
 }  // namespace pbstw

@@ -392,6 +392,16 @@ def run_body(hdr, name, poly, twist_tab, fwd=True):
     return data
 
 
+def _lds_with_lane_pair_tables(tab, N):
+    """Workgroup LDS as pbs_tw.hip lays it out: 2 x N exchange buffers, then the 32 forward and 32
+    inverse lane-pair twiddles (tab[N:N+32], tab[N+32+N : N+32+N+32])."""
+    lds = np.zeros(2 * N + 64, dtype=np.uint64)
+    t = np.array(tab, dtype=np.uint64)
+    lds[2 * N:2 * N + 32] = t[N:N + 32]
+    lds[2 * N + 32:2 * N + 64] = t[2 * N + 32:2 * N + 64]
+    return lds
+
+
 def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
     """Emulate the 2-wave workgroup of the blind-rotation body (tools/gen_pbs_kernel.py) on one LWE
     ciphertext.  bsk: n x 2 x 2 x N NTT-domain key (N^-1 folded in), tab: the plan's twist tables
@@ -400,7 +410,7 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
     LB, UB, KB, TB = 0x100000000, 0x200000000, 0x300000000, 0x400000000
     mem = {LB: np.array(lwe, dtype=np.uint64), UB: np.array(lut, dtype=np.uint64).reshape(-1),
            KB: np.array(bsk, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
-    lds = np.zeros(2 * N, dtype=np.uint64)
+    lds = _lds_with_lane_pair_tables(tab, N)
     lines = body_lines(hdr, name, "MI_PBS_BODY_")
     waves = []
     for w in range(2):
@@ -409,7 +419,7 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
                "gown_lo": str((KB + 3 * w * N * 8) & 0xFFFFFFFF), "gown_hi": str((KB + 3 * w * N * 8) >> 32),
                "gpar_lo": str((KB + (2 - w) * N * 8) & 0xFFFFFFFF), "gpar_hi": str((KB + (2 - w) * N * 8) >> 32),
                "lwe_lo": str(LB & 0xFFFFFFFF), "lwe_hi": str(LB >> 32), "n": str(n_lwe),
-               "tab_lo": str(TB & 0xFFFFFFFF), "tab_hi": str(TB >> 32), "bl": str(base_log)}
+               "tab_lo": str(TB & 0xFFFFFFFF), "tab_hi": str(TB >> 32), "bl": str(base_log), "LW": str(2 * N * 8)}
         wv = Wave(ops, mem, lds=lds)
         wv.v[0] = np.arange(LANES, dtype=np.uint64)
         wv.load(lines)
@@ -422,7 +432,7 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
                     next(waves[k])
                 except StopIteration:
                     live[k] = False
-    return lds.reshape(2, N).copy()
+    return lds[:2 * N].reshape(2, N).copy()
 
 
 def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
@@ -433,7 +443,7 @@ def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
     g = np.array(glwe, dtype=np.uint64).reshape(-1).copy()
     o = np.array(out, dtype=np.uint64).reshape(-1).copy()
     mem = {GB: g, OB: o, KB: np.array(ggsw, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
-    lds = np.zeros(2 * N, dtype=np.uint64)
+    lds = _lds_with_lane_pair_tables(tab, N)
     lines = body_lines(hdr, "cmux_bnf_l1" if cmux else "ext_bnf_l1", "MI_PBS_BODY_")
     waves = []
     for w in range(2):
@@ -444,7 +454,7 @@ def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
                "out_lo": lo(OB + w * N * 8), "out_hi": hi(OB + w * N * 8),
                "gown_lo": lo(KB + 3 * w * N * 8), "gown_hi": hi(KB + 3 * w * N * 8),
                "gpar_lo": lo(KB + (2 - w) * N * 8), "gpar_hi": hi(KB + (2 - w) * N * 8),
-               "tab_lo": lo(TB), "tab_hi": hi(TB), "bl": str(base_log)}
+               "tab_lo": lo(TB), "tab_hi": hi(TB), "bl": str(base_log), "LW": str(2 * N * 8)}
         wv = Wave(ops, mem, lds=lds)
         wv.v[0] = np.arange(LANES, dtype=np.uint64)
         wv.load(lines)

@@ -60,6 +60,12 @@ def addr_for(tab):
 
 
 FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
+# the lane-pair twiddles (32 forward + 32 inverse) live in the workgroup's LDS (copied by pbs_tw.hip at
+# kernel start): 4 lookups per step at LDS instead of L2 latency.  V_LWL = table base + 128 * (lane & 1).
+V_LWL = 248
+FWD_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
+INV_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
+FWD_ADDR.lw_wait = INV_ADDR.lw_wait = "s_waitcnt lgkmcnt(0)"
 
 
 def sched(B, sg):
@@ -104,7 +110,8 @@ def prologue(B):
           "v_lshrrev_b32 v15, 5, %[lane]", "v_xor_b32 v15, %[lane], v15", "v_lshlrev_b32 v15, 3, v15",
           f"v_add_u32 v{V_T2R}, %[S], v15",
           "v_add_u32 v16, v12, v9", "v_lshlrev_b32 v16, 3, v16", f"v_add_u32 v{V_T4W}, %[S], v16",
-          f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}")
+          f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}",
+          f"v_lshlrev_b32 v{V_LWL}, 7, v9", f"v_add_u32 v{V_LWL}, %[LW], v{V_LWL}")
 
 
 def load_rows(dst, base):

@@ -513,6 +513,7 @@ class Addr:
         self.tw_wait_n = lambda n: f"s_waitcnt vmcnt({n})"   # at most n younger table loads outstanding
         # (dst pair base, table entry k) -> load line of the lane's pair-stage twiddle k (+16 odd lanes)
         self.lw_load = lambda dst, k: f"global_load_dwordx2 {pv(dst)}, {self.lwo}, {self.lw} offset:{8 * k}"
+        self.lw_wait = None   # wait after the lane-pair twiddle loads (None: tw_wait)
         self.__dict__.update(regs)
 
 
@@ -635,7 +636,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR):
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
     for half in range(2):
         ks = list(range(8 * half, 8 * half + 8))
-        B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in enumerate(ks)], ad.tw_wait, "s_nop 1")
+        B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in enumerate(ks)], ad.lw_wait or ad.tw_wait, "s_nop 1")
         sg = Seg()
         for i, k in enumerate(ks):
             tmp = [f"v{r}" for r in tmps[i % 2]]
