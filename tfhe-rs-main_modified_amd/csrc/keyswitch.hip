@@ -13,12 +13,18 @@
 // signed bytes e_s (d = sum_s e_s 256^s) against key rows pre-shifted by 8s, so the GEMM depth is
 // K = in_dim * level * nd and |S_t| <= K * 128 * 128 < 2^31 for K < 2^17 (checked at key creation).
 //   * ksk_prepare_kernel (once per key): u64 key -> byte planes in MFMA B-fragment order
-//     [col tile][k block][plane][lane] x 16 B, zero-padded to 16-column / 64-digit tiles;
+//     [column group of GN tiles][k block][tile][plane][lane] x 16 B (one contiguous block per k step),
+//     zero-padded to whole column groups / 64-digit blocks;
 //   * ks_digits_kernel (per batch): decomposition of every mask element into int8 digits in A-fragment
-//     order [row tile][k block][lane] x 16 B (padded rows and digits are 0);
-//   * ks_gemm_kernel: one wave = 4 row tiles x 1 column tile x 8 planes = 32 accumulators of 16x16 i32;
-//     operands stream straight from global memory in fragment order (1 KiB coalesced per fragment),
-//     the 4 waves of a workgroup share the digit fragments through L1/L2; epilogue writes u64 outputs.
+//     order [row group of GM tiles][k block][tile][lane] x 16 B (padded rows and digits are 0);
+//   * ks_gemm_kernel: one 4-wave workgroup per CU computes a 256-row x 32-column block (x 8 planes):
+//     each k step's 16 + 16 KiB of fragments are copied global -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4) into a 3-buffer ring two steps ahead of the MFMAs (counted vmcnt + raw
+//     s_barrier, so the copies stay in flight across barriers); fragment reads are inline-asm
+//     ds_read_b128 so the compiler does not drain the ring before them.  Each wave owns 4 row tiles x 2
+//     column tiles x 8 planes = 64 accumulators of 16x16 i32 (256 AGPRs, one wave per SIMD).  Blocks
+//     are mapped XCD-aware: the workgroups one XCD runs together cover 8 row groups x 4 column groups,
+//     so the fragments they share are re-read from that XCD's L2.
 // Fragment maps (gfx950): lane l holds row/column (l & 15) of the tile and the 16 consecutive k of
 // group l >> 4 — the same k map for A and B, so the k order inside a block does not matter; C/D:
 // col = l & 15, row = 4 (l >> 4) + reg (cdna_hip_programming.md §3).
@@ -80,18 +86,30 @@ __device__ __forceinline__ uint4 pack16(const int8_t (&b)[16]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// frag[((ct * KB + kb) * 8 + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
-// column 16 ct + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
+// Workgroup block = WAVE_R x WAVE_C waves, each owning 4 row tiles x 2 column tiles (x 8 planes).
+// 4 x 1 (256 rows x 32 columns) moves 32 KiB per k step for 256 MFMAs, 2 x 2 (128 x 64) 40 KiB: the B
+// side carries 8 planes, so tall blocks stage fewer bytes per MFMA.
+static constexpr int WAVE_R = 4, WAVE_C = 1;
+static constexpr int GM = 4 * WAVE_R;  // row tiles (of 16) per workgroup block
+static constexpr int GN = 2 * WAVE_C;  // column tiles (of 16) per workgroup block
+static constexpr int A_STEP = GM * 64;      // uint4 per k step of a row group
+static constexpr int B_STEP = GN * 8 * 64;  // uint4 per k step of a column group
+static constexpr int A_PIECES = GM / 4;      // 1 KiB LDS-DMA pieces per wave and k step
+static constexpr int B_PIECES = GN * 8 / 4;
+static constexpr int PIECES = A_PIECES + B_PIECES;
+
+// frag[(((cg * KB + kb) * GN + ci) * 8 + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
+// column 16 (GN cg + ci) + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
 // (in_dim blocks of `level` LWEs) shifted left by 8 s.
 __global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ frag, const u64* __restrict__ ksk,
                                                           Shape s) {
-  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;
+  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;  // CT is a multiple of GN
   for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t lane = idx & 63, t = (idx >> 6) & 7;
-    const uint64_t rest = idx >> 9;
-    const uint32_t kb = rest % s.KB, ct = rest / s.KB;
-    const uint32_t col = ct * 16 + (lane & 15);
+    const uint32_t lane = idx & 63, t = (idx >> 6) & 7, ci = (idx >> 9) % GN;
+    const uint64_t rest = idx / (512 * GN);
+    const uint32_t kb = rest % s.KB, cg = rest / s.KB;
+    const uint32_t col = (cg * GN + ci) * 16 + (lane & 15);
     int8_t b[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -104,92 +122,181 @@ __global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ fr
   }
 }
 
-// afrag[(mt * KB + kb) * 64 + lane] = digits k = 64 kb + 16 (lane >> 4) + j of ciphertext
-// 16 mt + (lane & 15); rows >= batch and k >= K are zero.
+// afrag[((mg * KB + kb) * GM + mi) * 64 + lane] = digits k = 64 kb + 16 (lane >> 4) + j of ciphertext
+// 16 (GM mg + mi) + (lane & 15); rows >= batch and k >= K are zero.
 __global__ __launch_bounds__(256) void ks_digits_kernel(uint4* __restrict__ afrag, const u64* __restrict__ lwe_in,
                                                         uint32_t batch, uint32_t rows, Shape s) {
   const uint64_t total = (uint64_t)rows * s.KB * 4;
   for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t g = idx & 3;
-    const uint32_t kb = (idx >> 2) % s.KB;
-    const uint32_t row = (uint32_t)((idx >> 2) / s.KB);
+    // idx walks afrag in storage order (coalesced 1 KiB stores per wave); a wave reads 16 rows x 128 B
+    const uint32_t lane = idx & 63, g = lane >> 4;
+    const uint64_t piece = idx >> 6;  // (mg * KB + kb) * GM + mi
+    const uint32_t mi = piece % GM, kb = (piece / GM) % s.KB, mg = (uint32_t)(piece / GM / s.KB);
+    const uint32_t row = (mg * GM + mi) * 16 + (lane & 15);
     int8_t b[16];
     const u64* x = lwe_in + (uint64_t)row * (s.in_dim + 1);
-    uint32_t cur_i = 0xFFFFFFFFu, cur_li = 0;
+    const int bl = (int)s.base_log, lv = (int)s.level;
+    // digit column k = (i * level + li) * nd + sb, walked incrementally: 3 divisions per thread, not 3 per
+    // digit; terms come least significant first (iter.rs:103-119)
+    const uint32_t k0 = kb * 64 + 16 * g, kd0 = k0 / s.nd;
+    uint32_t sb = k0 - kd0 * s.nd, i = kd0 / s.level, li = kd0 - i * s.level;
+    const bool live = row < batch;
     u64 state = 0;
     int d = 0;
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t k = kb * 64 + 16 * g + j;
-      int8_t e = 0;
-      if (row < batch && k < s.K) {
-        const uint32_t kd = k / s.nd, i = kd / s.level, li = kd % s.level;
-        if (i != cur_i) {
-          state = decomp_init(x[i], (int)s.base_log, (int)s.level);
-          cur_i = i;
-          cur_li = 0;
-        }
-        while (cur_li <= li) {  // terms come least significant first (iter.rs:103-119)
-          d = decompose_one((int)s.base_log, state);
-          ++cur_li;
-        }
-        e = signed_byte((u64)(int64_t)d, (int)(k % s.nd));
-      }
-      b[j] = e;
+    if (live && k0 < s.K) {  // the state after terms 0..li of coefficient i
+      state = decomp_init(x[i], bl, lv);
+      for (uint32_t u = 0; u <= li; ++u) d = decompose_one(bl, state);
     }
-    const uint32_t mt = row >> 4, lane = (row & 15) + 16 * g;
-    afrag[((uint64_t)mt * s.KB + kb) * 64 + lane] = pack16(b);
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t k = k0 + j;
+      const bool on = live && k + 1 < s.K;
+      b[j] = (live && k < s.K) ? signed_byte((u64)(int64_t)d, (int)sb) : 0;
+      if (++sb == s.nd) {  // next decomposition term
+        sb = 0;
+        if (++li == s.level) {  // next mask coefficient
+          li = 0;
+          ++i;
+          if (on) state = decomp_init(x[i], bl, lv);
+        }
+        if (on) d = decompose_one(bl, state);
+      }
+    }
+    afrag[idx] = pack16(b);
   }
 }
 
-static constexpr int MT_W = 4;  // row tiles per wave
-static constexpr int WAVES = 4;  // column tiles per workgroup
+// Block t of the launch order -> (row group, column group): XCD x (workgroups x, x + 8, ... are dispatched
+// to the same XCD) takes the contiguous range [x * per, (x + 1) * per) of an order that walks 8 row groups
+// inside each column group, so the ~32 blocks an XCD holds at once share 4 column groups' key fragments.
+__device__ __forceinline__ bool ks_block(uint32_t bid, uint32_t n_mg, uint32_t n_cg, uint32_t& mg, uint32_t& cg) {
+  const uint32_t n_rb = (n_mg + 7) / 8, tiles = n_rb * 8 * n_cg, per = (tiles + 7) / 8;
+  const uint32_t t = (bid & 7) * per + (bid >> 3);
+  if (t >= tiles) return false;
+  const uint32_t rb = t / (8 * n_cg), w = t % (8 * n_cg);
+  cg = w / 8;
+  mg = rb * 8 + w % 8;
+  return mg < n_mg;
+}
 
-__global__ __launch_bounds__(64 * WAVES) void ks_gemm_kernel(u64* __restrict__ out, const u64* __restrict__ lwe_in,
-                                                             const uint4* __restrict__ afrag,
-                                                             const uint4* __restrict__ bfrag, uint32_t batch,
-                                                             Shape s) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t ct = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (ct >= s.CT) return;  // whole wave; no barriers in this kernel
-  const uint32_t mt0 = blockIdx.y * MT_W;
-  const uint4* A = afrag + (uint64_t)mt0 * s.KB * 64 + lane;
-  const uint4* B = bfrag + (uint64_t)ct * s.KB * 8 * 64 + lane;
-  i32x4 acc[MT_W][8];
+__device__ __forceinline__ i32x4 frag(const uint4* p) {
+  const uint4 x = *p;
+  return i32x4{(int)x.x, (int)x.y, (int)x.z, (int)x.w};
+}
+
+__global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, const u64* __restrict__ lwe_in,
+                                                         const uint4* __restrict__ afrag,
+                                                         const uint4* __restrict__ bfrag, uint32_t batch,
+                                                         uint32_t n_mg, Shape s) {
+  // three stage buffers (A pieces, then B pieces): LDS-DMA runs two k steps ahead
+  __shared__ uint4 lds[3][A_STEP + B_STEP];
+  uint32_t mg, cg;
+  if (!ks_block(blockIdx.x, n_mg, s.CT / GN, mg, cg)) return;  // whole workgroup, before any barrier
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w / WAVE_C, wc = w % WAVE_C;
+  // LDS-DMA staging: wave w copies A pieces [A_PIECES w, A_PIECES (w + 1)) and the same share of the B
+  // pieces of each k step (a piece = one tile-plane's 64 lanes x 16 B, written lane-linearly, which is
+  // the fragment order).
+  const uint4* ga = afrag + (uint64_t)mg * s.KB * A_STEP + (A_PIECES * w) * 64 + lane;
+  const uint4* gb = bfrag + (uint64_t)cg * s.KB * B_STEP + (B_PIECES * w) * 64 + lane;
+  auto stage = [&](uint32_t kb, uint32_t buf) {
 #pragma unroll
-  for (int m = 0; m < MT_W; ++m)
+    for (int q = 0; q < A_PIECES; ++q)
+      __builtin_amdgcn_global_load_lds(ga + (uint64_t)kb * A_STEP + q * 64, &lds[buf][(A_PIECES * w + q) * 64], 16,
+                                       0, 0);
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[m][t] = i32x4{0, 0, 0, 0};
+    for (int q = 0; q < B_PIECES; ++q)
+      __builtin_amdgcn_global_load_lds(gb + (uint64_t)kb * B_STEP + q * 64,
+                                       &lds[buf][A_STEP + (B_PIECES * w + q) * 64], 16, 0, 0);
+  };
+  i32x4 acc[4][2][8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[m][c][t] = i32x4{0, 0, 0, 0};
+  // this lane's fragment addresses in buffer 0 (buffer b adds b * BUF_BYTES)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)&lds[0][0];
+  const uint32_t a_addr = lds0 + ((wr * 4) * 64 + lane) * 16;
+  const uint32_t b_addr = lds0 + (A_STEP + (wc * 2 * 8) * 64 + lane) * 16;
+  constexpr uint32_t BUF_BYTES = (A_STEP + B_STEP) * 16;
+  stage(0, 0);
+  if (s.KB > 1) stage(1, 1);
+  if (s.KB > 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint32_t cur = 0;
   for (uint32_t kb = 0; kb < s.KB; ++kb) {
-    uint4 a[MT_W], b[8];
+    // Fragment reads in inline asm: the compiler cannot tell the stage buffers apart and would wait for
+    // every LDS-DMA in flight before its own ds_reads.  A + the first column tile's planes are waited for
+    // at once; the second tile's planes land while the first 32 MFMAs run.
+    const uint32_t ao = a_addr + cur * BUF_BYTES, bo = b_addr + cur * BUF_BYTES;
+    i32x4 av0, av1, av2, av3, p0, p1, p2, p3, p4, p5, p6, p7, q0, q1, q2, q3, q4, q5, q6, q7;
+    asm volatile(
+        "ds_read_b128 %0, %12\n\tds_read_b128 %1, %12 offset:1024\n\t"
+        "ds_read_b128 %2, %12 offset:2048\n\tds_read_b128 %3, %12 offset:3072\n\t"
+        "ds_read_b128 %4, %13\n\tds_read_b128 %5, %13 offset:1024\n\t"
+        "ds_read_b128 %6, %13 offset:2048\n\tds_read_b128 %7, %13 offset:3072\n\t"
+        "ds_read_b128 %8, %13 offset:4096\n\tds_read_b128 %9, %13 offset:5120\n\t"
+        "ds_read_b128 %10, %13 offset:6144\n\tds_read_b128 %11, %13 offset:7168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(av0), "=&v"(av1), "=&v"(av2), "=&v"(av3), "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "=&v"(p4),
+          "=&v"(p5), "=&v"(p6), "=&v"(p7)
+        : "v"(ao), "v"(bo));
+    asm volatile(
+        "ds_read_b128 %0, %8 offset:8192\n\tds_read_b128 %1, %8 offset:9216\n\t"
+        "ds_read_b128 %2, %8 offset:10240\n\tds_read_b128 %3, %8 offset:11264\n\t"
+        "ds_read_b128 %4, %8 offset:12288\n\tds_read_b128 %5, %8 offset:13312\n\t"
+        "ds_read_b128 %6, %8 offset:14336\n\tds_read_b128 %7, %8 offset:15360"
+        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5), "=&v"(q6), "=&v"(q7)
+        : "v"(bo));
+    const bool more = kb + 2 < s.KB;
+    const uint32_t nxt = cur == 0 ? 2 : cur - 1;  // (kb + 2) % 3: last read in step kb - 1, before the barrier
+    if (more) stage(kb + 2, nxt);
+    const i32x4 av[4] = {av0, av1, av2, av3};
+    const i32x4 b0[8] = {p0, p1, p2, p3, p4, p5, p6, p7};
 #pragma unroll
-    for (int m = 0; m < MT_W; ++m) a[m] = A[((uint64_t)m * s.KB + kb) * 64];
+    for (int t = 0; t < 8; ++t)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) b[t] = B[((uint64_t)kb * 8 + t) * 64];
+      for (int m = 0; m < 4; ++m) acc[m][0][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], b0[t], acc[m][0][t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // the first tile's MFMAs stay ahead of the wait for the second's planes
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7));
+    const i32x4 b1[8] = {q0, q1, q2, q3, q4, q5, q6, q7};
 #pragma unroll
-    for (int m = 0; m < MT_W; ++m) {
-      const i32x4 av = {(int)a[m].x, (int)a[m].y, (int)a[m].z, (int)a[m].w};
+    for (int t = 0; t < 8; ++t)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const i32x4 bv = {(int)b[t].x, (int)b[t].y, (int)b[t].z, (int)b[t].w};
-        acc[m][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[m][t], 0, 0, 0);
-      }
-    }
+      for (int m = 0; m < 4; ++m) acc[m][1][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], b1[t], acc[m][1][t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs ahead of the wait: they are what covers the DMA
+    // this wave's pieces of step kb + 1 have landed (the PIECES newest, step kb + 2's, may stay in
+    // flight), then the barrier makes everyone's visible
+    if (more)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    cur = cur == 2 ? 0 : cur + 1;
   }
-  const uint32_t col = ct * 16 + (lane & 15);
-  if (col >= s.out_size) return;
-  const bool is_body = col == s.out_size - 1;
 #pragma unroll
-  for (int m = 0; m < MT_W; ++m) {
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t col = (cg * GN + wc * 2 + c) * 16 + (lane & 15);
+    if (col >= s.out_size) continue;
+    const bool is_body = col == s.out_size - 1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t row = (mt0 + m) * 16 + 4 * (lane >> 4) + r;
-      if (row >= batch) continue;
-      u64 v = 0;
+    for (int m = 0; m < 4; ++m) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) v += (u64)(int64_t)acc[m][t][r] << (8 * t);
-      const u64 base = is_body ? lwe_in[(uint64_t)row * (s.in_dim + 1) + s.in_dim] : 0;
-      out[(uint64_t)row * s.out_size + col] = base - v;
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t row = (mg * GM + wr * 4 + m) * 16 + 4 * (lane >> 4) + r;
+        if (row >= batch) continue;
+        u64 v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v += (u64)(int64_t)acc[m][c][t][r] << (8 * t);
+        const u64 base = is_body ? lwe_in[(uint64_t)row * (s.in_dim + 1) + s.in_dim] : 0;
+        out[(uint64_t)row * s.out_size + col] = base - v;
+      }
     }
   }
 }
@@ -207,7 +314,7 @@ static ks::Shape ks_shape(size_t in_dim, size_t out_dim, int base_log, int level
   s.nd = (uint32_t)ks_digit_bytes_per_term(base_log);
   s.K = (uint32_t)(in_dim * (size_t)level * s.nd);
   s.KB = (s.K + 63) / 64;
-  s.CT = (s.out_size + 15) / 16;
+  s.CT = (s.out_size + 16 * ks::GN - 1) / (16 * ks::GN) * ks::GN;  // whole column groups
   return s;
 }
 
@@ -218,7 +325,7 @@ size_t ks_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level) {
 
 size_t ks_digit_bytes(size_t in_dim, int base_log, int level, size_t batch) {
   const size_t kb = (in_dim * (size_t)level * (size_t)ks_digit_bytes_per_term(base_log) + 63) / 64;
-  const size_t rows = (batch + 16 * ks::MT_W - 1) / (16 * ks::MT_W) * 16 * ks::MT_W;
+  const size_t rows = (batch + 16 * ks::GM - 1) / (16 * ks::GM) * 16 * ks::GM;
   return rows * kb * 64;
 }
 
@@ -235,16 +342,18 @@ hipError_t launch_keyswitch(uint64_t* out, const uint64_t* lwe_in, const void* f
                             size_t in_dim, size_t out_dim, int base_log, int level, hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
-  const uint32_t rows = (uint32_t)((batch + 16 * ks::MT_W - 1) / (16 * ks::MT_W) * 16 * ks::MT_W);
+  const uint32_t rows = (uint32_t)((batch + 16 * ks::GM - 1) / (16 * ks::GM) * 16 * ks::GM);
   const uint64_t total = (uint64_t)rows * s.KB * 4;
   const unsigned dgrid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
   hipLaunchKernelGGL(ks::ks_digits_kernel, dim3(dgrid), dim3(256), 0, st, (uint4*)digits, lwe_in, (uint32_t)batch,
                      rows, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const dim3 grid((s.CT + ks::WAVES - 1) / ks::WAVES, rows / (16 * ks::MT_W));
-  hipLaunchKernelGGL(ks::ks_gemm_kernel, grid, dim3(64 * ks::WAVES), 0, st, out, lwe_in, (const uint4*)digits,
-                     (const uint4*)frag, (uint32_t)batch, s);
+  const uint32_t n_mg = rows / (16 * ks::GM), n_cg = s.CT / ks::GN;
+  const uint32_t tiles = (n_mg + 7) / 8 * 8 * n_cg;
+  const unsigned grid = 8 * ((tiles + 7) / 8);
+  hipLaunchKernelGGL(ks::ks_gemm_kernel, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
+                     (const uint4*)frag, (uint32_t)batch, n_mg, s);
   return hipGetLastError();
 }
 
