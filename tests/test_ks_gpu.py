@@ -41,6 +41,8 @@ def run_ks(engine, ksk, lwe, base_log, level):
     (33, 17, 10, 2, 64),        # digits wider than a signed byte: 2 bytes per digit
     (40, 25, 15, 4, 3),         # 15-bit base: 2 bytes per digit
     (20, 12, 21, 3, 17),        # 21-bit base: 3 bytes per digit
+    (512, 300, 4, 4, 520),      # 3 row groups of 256 (last ragged) x 10 column groups of 32
+    (48, 40, 4, 4, 300),        # odd number of k blocks (K = 192 -> 3), 2 row groups, padded columns
 ])
 def test_keyswitch_matches_oracle(engine, oracle, in_dim, out_dim, base_log, level, batch):
     g = H.rng(in_dim * 7 + out_dim + base_log)

@@ -198,15 +198,19 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
   // the fragment order).
   const uint4* ga = afrag + (uint64_t)mg * s.KB * A_STEP + (A_PIECES * w) * 64 + lane;
   const uint4* gb = bfrag + (uint64_t)cg * s.KB * B_STEP + (B_PIECES * w) * 64 + lane;
-  auto stage = [&](uint32_t kb, uint32_t buf) {
+  // quarter `part` of this wave's pieces of step kb into stage buffer `buf`
+  static_assert(PIECES % 4 == 0, "pieces are issued in quarters");
+  auto dma = [&](uint32_t kb, uint32_t buf, int part) {
 #pragma unroll
-    for (int q = 0; q < A_PIECES; ++q)
-      __builtin_amdgcn_global_load_lds(ga + (uint64_t)kb * A_STEP + q * 64, &lds[buf][(A_PIECES * w + q) * 64], 16,
-                                       0, 0);
-#pragma unroll
-    for (int q = 0; q < B_PIECES; ++q)
-      __builtin_amdgcn_global_load_lds(gb + (uint64_t)kb * B_STEP + q * 64,
-                                       &lds[buf][A_STEP + (B_PIECES * w + q) * 64], 16, 0, 0);
+    for (int u = 0; u < PIECES / 4; ++u) {
+      const int q = part * (PIECES / 4) + u;
+      if (q < A_PIECES)
+        __builtin_amdgcn_global_load_lds(ga + (uint64_t)kb * A_STEP + q * 64, &lds[buf][(A_PIECES * w + q) * 64],
+                                         16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(gb + (uint64_t)kb * B_STEP + (q - A_PIECES) * 64,
+                                         &lds[buf][A_STEP + (B_PIECES * w + q - A_PIECES) * 64], 16, 0, 0);
+    }
   };
   i32x4 acc[4][2][8];
 #pragma unroll
@@ -220,66 +224,80 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
   const uint32_t a_addr = lds0 + ((wr * 4) * 64 + lane) * 16;
   const uint32_t b_addr = lds0 + (A_STEP + (wc * 2 * 8) * 64 + lane) * 16;
   constexpr uint32_t BUF_BYTES = (A_STEP + B_STEP) * 16;
-  stage(0, 0);
-  if (s.KB > 1) stage(1, 1);
-  if (s.KB > 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  uint32_t cur = 0;
-  for (uint32_t kb = 0; kb < s.KB; ++kb) {
-    // Fragment reads in inline asm: the compiler cannot tell the stage buffers apart and would wait for
-    // every LDS-DMA in flight before its own ds_reads.  A + the first column tile's planes are waited for
-    // at once; the second tile's planes land while the first 32 MFMAs run.
-    const uint32_t ao = a_addr + cur * BUF_BYTES, bo = b_addr + cur * BUF_BYTES;
-    i32x4 av0, av1, av2, av3, p0, p1, p2, p3, p4, p5, p6, p7, q0, q1, q2, q3, q4, q5, q6, q7;
+  // Fragment reads are inline asm: the compiler cannot tell the stage buffers apart and would drain
+  // every LDS-DMA in flight (vmcnt(0)) before its own ds_reads; lgkm_wait retires them.
+  auto rd_a = [&](uint32_t buf, i32x4(&A)[4]) {
+    const uint32_t ao = a_addr + buf * BUF_BYTES;
     asm volatile(
-        "ds_read_b128 %0, %12\n\tds_read_b128 %1, %12 offset:1024\n\t"
-        "ds_read_b128 %2, %12 offset:2048\n\tds_read_b128 %3, %12 offset:3072\n\t"
-        "ds_read_b128 %4, %13\n\tds_read_b128 %5, %13 offset:1024\n\t"
-        "ds_read_b128 %6, %13 offset:2048\n\tds_read_b128 %7, %13 offset:3072\n\t"
-        "ds_read_b128 %8, %13 offset:4096\n\tds_read_b128 %9, %13 offset:5120\n\t"
-        "ds_read_b128 %10, %13 offset:6144\n\tds_read_b128 %11, %13 offset:7168\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(av0), "=&v"(av1), "=&v"(av2), "=&v"(av3), "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "=&v"(p4),
-          "=&v"(p5), "=&v"(p6), "=&v"(p7)
-        : "v"(ao), "v"(bo));
-    asm volatile(
-        "ds_read_b128 %0, %8 offset:8192\n\tds_read_b128 %1, %8 offset:9216\n\t"
-        "ds_read_b128 %2, %8 offset:10240\n\tds_read_b128 %3, %8 offset:11264\n\t"
-        "ds_read_b128 %4, %8 offset:12288\n\tds_read_b128 %5, %8 offset:13312\n\t"
-        "ds_read_b128 %6, %8 offset:14336\n\tds_read_b128 %7, %8 offset:15360"
-        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3), "=&v"(q4), "=&v"(q5), "=&v"(q6), "=&v"(q7)
-        : "v"(bo));
-    const bool more = kb + 2 < s.KB;
-    const uint32_t nxt = cur == 0 ? 2 : cur - 1;  // (kb + 2) % 3: last read in step kb - 1, before the barrier
-    if (more) stage(kb + 2, nxt);
-    const i32x4 av[4] = {av0, av1, av2, av3};
-    const i32x4 b0[8] = {p0, p1, p2, p3, p4, p5, p6, p7};
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc[m][0][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], b0[t], acc[m][0][t], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);  // the first tile's MFMAs stay ahead of the wait for the second's planes
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
+        "ds_read_b128 %3, %4 offset:3072"
+        : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3])
+        : "v"(ao));
+  };
+  auto rd_b = [&](uint32_t buf, int j, i32x4& Bj) {  // plane t of column tile c, j = 8 c + t
+    const uint32_t bo = b_addr + buf * BUF_BYTES + 1024 * j;
+    asm volatile("ds_read_b128 %0, %1" : "=&v"(Bj) : "v"(bo));
+  };
+  auto lgkm_wait = [&](i32x4(&A)[4], i32x4(&Bf)[16]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6), "+v"(q7));
-    const i32x4 b1[8] = {q0, q1, q2, q3, q4, q5, q6, q7};
+                 : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(Bf[0]), "+v"(Bf[1]), "+v"(Bf[2]),
+                   "+v"(Bf[3]), "+v"(Bf[4]), "+v"(Bf[5]), "+v"(Bf[6]), "+v"(Bf[7]), "+v"(Bf[8]), "+v"(Bf[9]),
+                   "+v"(Bf[10]), "+v"(Bf[11]), "+v"(Bf[12]), "+v"(Bf[13]), "+v"(Bf[14]), "+v"(Bf[15]));
+  };
+  // prologue: steps 0..2 in flight; steps 0 and 1 landed; step 0's fragments in (A, Bf); a barrier so
+  // that nobody's step-3 DMA overwrites buffer 0 before every wave has read it
+  // (a copy of a step past the end is clamped to the last step: redundant but harmless, and it keeps
+  // exactly PIECES copies per step in flight, so every wait below is the same counted vmcnt)
+  const uint32_t last = s.KB - 1;
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+  for (int p = 0; p < 4; ++p) dma(0, 0, p);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) acc[m][1][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[m], b1[t], acc[m][1][t], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs ahead of the wait: they are what covers the DMA
-    // this wave's pieces of step kb + 1 have landed (the PIECES newest, step kb + 2's, may stay in
-    // flight), then the barrier makes everyone's visible
-    if (more)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int p = 0; p < 4; ++p) dma(1 < last ? 1 : last, 1, p);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) dma(2 < last ? 2 : last, 2, p);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+  __builtin_amdgcn_s_barrier();
+  i32x4 A[4], NA[4], Bf[16];
+  rd_a(0, A);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rd_b(0, j, Bf[j]);
+  lgkm_wait(A, Bf);
+  __builtin_amdgcn_s_barrier();
+  // Step kb: 16 groups of 4 MFMAs, group j on plane fragment Bf[j] (j = 8 c + t) and the 4 row tiles A.
+  // Behind group j the wave refills Bf[j] with step kb + 1's fragment (just freed), reads step kb + 1's
+  // A into NA behind group 0, and issues a quarter of step kb + 3's LDS-DMA into the buffer step kb
+  // occupied behind groups 1, 3, 5, 7 (an MFMA leaves half its cycles to other issue).  Step kb + 2's
+  // copy is in flight throughout; the closing wait retires it and the barrier publishes it.
+  uint32_t buf = 0;
+  for (uint32_t kb = 0; kb < s.KB; ++kb) {
+    const uint32_t nbuf = buf == 2 ? 0 : buf + 1, src = kb + 3 < last ? kb + 3 : last;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = j >> 3, t = j & 7;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {  // accumulators pinned to AGPRs ("+a"): fragments keep the VGPRs
+        if (j == 0 && m == 0)  // A was just copied by VALU: 2 wait states before an MFMA reads it
+          asm("s_nop 1\n\tv_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][c][t]) : "v"(A[m]), "v"(Bf[j]));
+        else
+          asm("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][c][t]) : "v"(A[m]), "v"(Bf[j]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (j == 0) rd_a(nbuf, NA);  // in the last step these read a stale buffer: unused
+      rd_b(nbuf, j, Bf[j]);
+      if ((j & 1) && j < 8) dma(src, buf, j >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lgkm_wait(NA, Bf);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) A[m] = NA[m];
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    cur = cur == 2 ? 0 : cur + 1;
+    buf = nbuf;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
+  // the compiler does not know the asm above holds MFMAs: 12 wait states before it reads their results
+  asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const uint32_t col = (cg * GN + wc * 2 + c) * 16 + (lane & 15);
