@@ -97,6 +97,7 @@ static constexpr int B_STEP = GN * 8 * 64;  // uint4 per k step of a column grou
 static constexpr int A_PIECES = GM / 4;      // 1 KiB LDS-DMA pieces per wave and k step
 static constexpr int B_PIECES = GN * 8 / 4;
 static constexpr int PIECES = A_PIECES + B_PIECES;
+static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 measured no faster
 
 // frag[(((cg * KB + kb) * GN + ci) * 8 + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
 // column 16 (GN cg + ci) + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
@@ -188,8 +189,10 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
                                                          const uint4* __restrict__ afrag,
                                                          const uint4* __restrict__ bfrag, uint32_t batch,
                                                          uint32_t n_mg, Shape s) {
-  // three stage buffers (A pieces, then B pieces): LDS-DMA runs two k steps ahead
-  __shared__ uint4 lds[3][A_STEP + B_STEP];
+  // NBUF stage buffers (A pieces, then B pieces) of 32 KiB: while step kb multiplies, step kb + 1 is
+  // read into registers and steps kb + 2 .. kb + NBUF are in flight (deep enough to cover the L2 /
+  // MALL latency at the per-CU byte rate one step of MFMAs needs)
+  __shared__ uint4 lds[NBUF][A_STEP + B_STEP];
   uint32_t mg, cg;
   if (!ks_block(blockIdx.x, n_mg, s.CT / GN, mg, cg)) return;  // whole workgroup, before any barrier
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w / WAVE_C, wc = w % WAVE_C;
@@ -245,17 +248,18 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
                    "+v"(Bf[10]), "+v"(Bf[11]), "+v"(Bf[12]), "+v"(Bf[13]), "+v"(Bf[14]), "+v"(Bf[15]));
   };
   // prologue: steps 0..2 in flight; steps 0 and 1 landed; step 0's fragments in (A, Bf); a barrier so
-  // that nobody's step-3 DMA overwrites buffer 0 before every wave has read it
+  // that nobody's step-NBUF DMA overwrites buffer 0 before every wave has read it
   // (a copy of a step past the end is clamped to the last step: redundant but harmless, and it keeps
   // exactly PIECES copies per step in flight, so every wait below is the same counted vmcnt)
   const uint32_t last = s.KB - 1;
 #pragma unroll
   for (int p = 0; p < 4; ++p) dma(0, 0, p);
 #pragma unroll
-  for (int p = 0; p < 4; ++p) dma(1 < last ? 1 : last, 1, p);
+  for (uint32_t b = 1; b < NBUF; ++b) {
 #pragma unroll
-  for (int p = 0; p < 4; ++p) dma(2 < last ? 2 : last, 2, p);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    for (int p = 0; p < 4; ++p) dma(b < last ? b : last, b, p);
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * PIECES) : "memory");  // steps 0 and 1 landed
   __builtin_amdgcn_s_barrier();
   i32x4 A[4], NA[4], Bf[16];
   rd_a(0, A);
@@ -265,12 +269,12 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
   __builtin_amdgcn_s_barrier();
   // Step kb: 16 groups of 4 MFMAs, group j on plane fragment Bf[j] (j = 8 c + t) and the 4 row tiles A.
   // Behind group j the wave refills Bf[j] with step kb + 1's fragment (just freed), reads step kb + 1's
-  // A into NA behind group 0, and issues a quarter of step kb + 3's LDS-DMA into the buffer step kb
+  // A into NA behind group 0, and issues a quarter of step kb + NBUF's LDS-DMA into the buffer step kb
   // occupied behind groups 1, 3, 5, 7 (an MFMA leaves half its cycles to other issue).  Step kb + 2's
   // copy is in flight throughout; the closing wait retires it and the barrier publishes it.
   uint32_t buf = 0;
   for (uint32_t kb = 0; kb < s.KB; ++kb) {
-    const uint32_t nbuf = buf == 2 ? 0 : buf + 1, src = kb + 3 < last ? kb + 3 : last;
+    const uint32_t nbuf = (buf + 1) % NBUF, src = kb + NBUF < last ? kb + NBUF : last;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int c = j >> 3, t = j & 7;
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
     lgkm_wait(NA, Bf);
 #pragma unroll
     for (int m = 0; m < 4; ++m) A[m] = NA[m];
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * PIECES) : "memory");  // step kb + 2 landed
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     buf = nbuf;
