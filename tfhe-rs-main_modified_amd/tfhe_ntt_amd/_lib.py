@@ -79,6 +79,21 @@ _SIGS = {
 _lib = None
 
 
+def _init_torch_device_runtime() -> None:
+    """Bring torch's HIP context up before the engine's first HIP call.
+
+    torch ships its own libamdhip64; the engine links /opt/rocm's.  Measured on the MI355X: either
+    runtime fully initialised first is fine, but after a bare ``torch.cuda.is_available()`` (which
+    pytest collection and most scripts call) the engine's first ``hipSetDevice`` fails.  Completing
+    torch's initialisation here removes that order dependence.  No device -> nothing to do."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
@@ -86,6 +101,7 @@ def lib() -> ctypes.CDLL:
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `make -C tfhe-rs-main_modified_amd` "
                 "(there is no CPU fallback for the HIP engine)")
+        _init_torch_device_runtime()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)

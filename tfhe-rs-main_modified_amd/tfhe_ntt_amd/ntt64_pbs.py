@@ -136,6 +136,32 @@ class NttBootstrapKey:
     def output_lwe_size(self) -> int:
         return self.glwe_dimension * self.polynomial_size + 1
 
+    def serialize(self) -> bytes:
+        """``bincode::serialize`` bytes of the reference's NttLweBootstrapKey (``ntt_bsk_format``); the
+        ciphertext modulus field is native (0) for ``BNF`` and the Solinas prime for ``SOLINAS``."""
+        from .ntt_bsk_format import serialize_ntt_bsk
+        mod = 0 if self.variant == BNF else self.plan.modulus()
+        return serialize_ntt_bsk(self.bsk.detach().cpu().numpy(), self.polynomial_size, self.glwe_dimension + 1,
+                                 self.level, self.base_log, mod)
+
+    @classmethod
+    def deserialize(cls, plan, buf: bytes, device=None):
+        """Loads serialised key bytes into HBM (one copy) and binds them to ``plan``; the variant follows
+        the stored ciphertext modulus (native -> BNF, the plan's prime -> SOLINAS)."""
+        import numpy as np
+        import torch
+        from .ntt_bsk_format import NttBskFormatError, deserialize_ntt_bsk
+        data, f = deserialize_ntt_bsk(buf)
+        if f["polynomial_size"] != plan.ntt_size():
+            raise NttBskFormatError(f"key polynomial size {f['polynomial_size']} != plan size {plan.ntt_size()}")
+        if f["ciphertext_modulus"] not in (0, plan.modulus()):
+            raise NttBskFormatError(f"key ciphertext modulus {f['ciphertext_modulus']} is neither native nor the "
+                                    "plan's prime")
+        variant = BNF if f["ciphertext_modulus"] == 0 else SOLINAS
+        dev = device if device is not None else torch.device("cuda", plan.device)
+        bsk = torch.from_numpy(data.view(np.int64)).to(dev)
+        return cls(plan, bsk, f["decomposition_base_log"], f["decomposition_level_count"], variant)
+
 
 def _pbs(key, lwe_in, lwe_out, accumulator, ms_mode):
     n_in = key.input_lwe_dimension + 1
