@@ -21,6 +21,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <vector>
 
 #include "tfhe_ntt_amd.h"
 
@@ -245,6 +246,63 @@ class LweKeyswitchKey {
 inline void keyswitch_lwe_ciphertext(const LweKeyswitchKey& key, const uint64_t* lwe_in, uint64_t* lwe_out,
                                      size_t batch, void* stream = nullptr) {
   check(mi_lwe_keyswitch_batch(key.raw(), lwe_out, lwe_in, batch, stream));
+}
+
+// On-disk NTT bootstrap key: the bytes bincode 1.3 writes for NttLweBootstrapKey<ABox<[u64]>>
+// (entities/ntt_lwe_bootstrap_key.rs:26-33, entities/ntt_ggsw_ciphertext_list.rs:21-31,
+// commons/ciphertext_modulus.rs:48-93): u64 count, count u64 elements (n_lwe, level, k+1, k+1, N),
+// then polynomial_size, glwe_size, level, base_log as u64, the modulus as u128 (0 = native 2^64) and
+// scalar_bits = 64 as u64, all little-endian.  Same layout as tfhe_ntt_amd/ntt_bsk_format.py.
+struct NttBskFields {
+  uint64_t polynomial_size = 0, glwe_size = 0, level = 0, base_log = 0;
+  uint64_t modulus_lo = 0, modulus_hi = 0;  // u128 ciphertext modulus
+  uint64_t input_lwe_dimension = 0;
+};
+
+namespace detail {
+inline void put_u64(std::vector<uint8_t>& out, uint64_t v) {
+  for (int i = 0; i < 8; ++i) out.push_back(static_cast<uint8_t>(v >> (8 * i)));
+}
+inline uint64_t get_u64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = v << 8 | p[i];
+  return v;
+}
+}  // namespace detail
+
+inline std::vector<uint8_t> serialize_ntt_bsk(const uint64_t* data, size_t count, const NttBskFields& f) {
+  const uint64_t ggsw = f.level * f.glwe_size * f.glwe_size * f.polynomial_size;
+  if (ggsw == 0 || count % ggsw) throw std::invalid_argument("NTT BSK: data is not a whole number of GGSWs");
+  std::vector<uint8_t> out;
+  out.reserve(8 + 8 * count + 56);
+  detail::put_u64(out, count);
+  for (size_t i = 0; i < count; ++i) detail::put_u64(out, data[i]);
+  for (uint64_t v : {f.polynomial_size, f.glwe_size, f.level, f.base_log, f.modulus_lo, f.modulus_hi, uint64_t{64}})
+    detail::put_u64(out, v);
+  return out;
+}
+
+// Throws std::invalid_argument on truncated / trailing bytes, scalar_bits != 64 (the reference's
+// TryFrom<SerializableCiphertextModulus> error) or a data length that is not a whole number of GGSWs.
+inline NttBskFields deserialize_ntt_bsk(const uint8_t* buf, size_t len, std::vector<uint64_t>& data) {
+  if (len < 8) throw std::invalid_argument("NTT BSK: truncated");
+  const uint64_t count = detail::get_u64(buf);
+  if (count > (len - 8) / 8 || len != 8 + 8 * count + 56) throw std::invalid_argument("NTT BSK: length mismatch");
+  const uint8_t* t = buf + 8 + 8 * count;
+  NttBskFields f;
+  f.polynomial_size = detail::get_u64(t);
+  f.glwe_size = detail::get_u64(t + 8);
+  f.level = detail::get_u64(t + 16);
+  f.base_log = detail::get_u64(t + 24);
+  f.modulus_lo = detail::get_u64(t + 32);
+  f.modulus_hi = detail::get_u64(t + 40);
+  if (detail::get_u64(t + 48) != 64) throw std::invalid_argument("NTT BSK: scalar_bits != 64");
+  const uint64_t ggsw = f.level * f.glwe_size * f.glwe_size * f.polynomial_size;
+  if (ggsw == 0 || count % ggsw) throw std::invalid_argument("NTT BSK: data is not a whole number of GGSWs");
+  f.input_lwe_dimension = count / ggsw;
+  data.resize(count);
+  for (uint64_t i = 0; i < count; ++i) data[i] = detail::get_u64(buf + 8 + 8 * i);
+  return f;
 }
 
 }  // namespace core_crypto

@@ -97,3 +97,26 @@ def test_deserialized_key_bootstraps_identically(engine, bnf):
         run(dev(lwe), out, dev(lut), k)
         outs.append(out.cpu().numpy())
     assert np.array_equal(outs[0], outs[1])
+
+
+def _cpp_tool():
+    import os
+    import subprocess
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp")
+    subprocess.run(["make", "-C", d, "-s", "bsk_format_tool"], check=True)
+    return os.path.join(d, "bsk_format_tool")
+
+
+def test_cpp_mirror_reads_and_writes_the_same_bytes():
+    """include/tfhe_ntt_amd.hpp serialize_ntt_bsk / deserialize_ntt_bsk agree byte for byte with the
+    Python mirror (CPU only: the C++ serialiser is header-only)."""
+    import subprocess
+    tool = _cpp_tool()
+    key = _key(H.rng(12), n_lwe=4, level=3, glwe=2, n=64)
+    buf = F.serialize_ntt_bsk(key, 64, 2, 3, 7, P)
+    r = subprocess.run([tool], input=buf, capture_output=True, check=True)
+    assert r.stdout == buf
+    assert r.stderr.split() == [b"64", b"2", b"3", b"7", b"4"]
+    bad = buf[:-8] + struct.pack("<Q", 32)
+    r = subprocess.run([tool], input=bad, capture_output=True)
+    assert r.returncode == 3 and b"scalar_bits" in r.stderr
