@@ -16,6 +16,10 @@ the PARAM_MESSAGE_2_CARRY_2 shape (n=918, k=1, N=2048, base 2^23, l=1, native 2^
 through the BNF NTT algorithm, ntt64_bnf_pbs.rs:469-540), one fused kernel launch.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-pbs]
+
+``--gpus N`` with N > 1 outside a torch.distributed launch re-launches this script under
+``python -m torch.distributed.run --nproc-per-node N`` (as a child process, before anything touches the
+GPU) and exits with its status; inside a launch, WORLD_SIZE must equal N.
 """
 import argparse
 import json
@@ -44,14 +48,16 @@ PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults keep every GPU leg busy for seconds (the NTT leg ~1.6 s), so a sampler outside the process
+    # sees the work, while the whole run stays well under a minute of GPU time
+    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-pbs", action="store_true", help="skip the config-4 PBS leg")
     ap.add_argument("--pbs-batch", type=int, default=PBS_BATCH)
-    ap.add_argument("--pbs-steps", type=int, default=3)
+    ap.add_argument("--pbs-steps", type=int, default=10)
     ap.add_argument("--pbs-global", type=int, default=65536, help="config 5 global batch (N > 1 only)")
     # rehearsal of the multi-rank path on a 1-GPU box: every rank on cuda:0, gloo instead of RCCL
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -278,7 +284,7 @@ def bench_ext_product(args, eng, torch, dev, world, barrier):
     run = lambda: M.add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, PBS_BASE_LOG, 1)
     run()
     torch.cuda.synchronize()
-    K = max(3, args.steps // 5)
+    K = max(3, args.steps // 20)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -313,7 +319,7 @@ def bench_keyswitch(args, eng, torch, dev, world, barrier):
     run = lambda: KS.keyswitch_lwe_ciphertext(key, lwe, out)
     run()
     torch.cuda.synchronize()
-    K = max(5, args.steps)
+    K = max(5, args.steps // 10)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
@@ -412,12 +418,31 @@ def load_traffic():
         return None
 
 
+def relaunch_distributed(n: int) -> int:
+    """One process per GPU: run this script under torch.distributed.run with N ranks (a child process;
+    this process has not touched the GPU) and return its exit status."""
+    import socket
+    import subprocess
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     import torch
     import tfhe_ntt_amd as eng
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -452,55 +477,41 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
+    # HIP events on the launching stream (`work`, torch's current stream, which the plan launches on)
+    # bracket the timed region itself: their interval / (2 K) is the average duration of the 2 K timed
+    # launches, gaps included (no event sits between launches: each would add its own dependency point)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(work)
     for k in range(K):
         plan.fwd(buf)
         plan.inv(buf)
+    ev1.record(work)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         elapsed = eng.multi_gpu.max_over_ranks(elapsed, dev)
+    launch_ms = ev0.elapsed_time(ev1) / (2 * K)
 
-    # per-kernel durations, outside the timed loop: HIP events around K back-to-back launches of one
-    # kernel (an event between every launch would add its own ~6-10 us barrier to each interval).
-    # The plan launches on torch's current stream, which is what these events record on.
+    # per-direction split (informational), from a separate loop of back-to-back launches of one kernel;
+    # the roofline below uses the timed launches
+    split_k = min(K, 500)
     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    e0.record()
-    for k in range(K):
+    e0.record(work)
+    for k in range(split_k):
         plan.fwd(buf)
-    e1.record()
-    for k in range(K):
+    e1.record(work)
+    for k in range(split_k):
         plan.inv(buf)
-    e2.record()
+    e2.record(work)
     torch.cuda.synchronize()
-    fwd_ms = e0.elapsed_time(e1) / K
-    # the same K steps launched as one hipGraph (captured outside the timed region): what a pipeline
-    # that replays a fixed transform sequence gets; reported beside, not instead of, the per-call rate
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=work):
-        for k in range(K):
-            plan.fwd(buf)
-            plan.inv(buf)
-    graph.replay()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    graph.replay()
-    torch.cuda.synchronize()
-    barrier()
-    graph_el = time.perf_counter() - t0
-    if dist is not None:
-        graph_el = eng.multi_gpu.max_over_ranks(graph_el, dev)
-    del graph
-    inv_ms = e1.elapsed_time(e2) / K
-    dom_ms = max(fwd_ms, inv_ms)
-    dom = "fwd" if fwd_ms >= inv_ms else "inv"
+    fwd_ms = e0.elapsed_time(e1) / split_k
+    inv_ms = e1.elapsed_time(e2) / split_k
     bytes_launch = batch * BYTES_PER_POLY_PASS
-    achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
+    achieved = bytes_launch / (launch_ms * 1e-3) / 1e9
 
     units = world * batch * K
     value = units / elapsed
@@ -524,9 +535,9 @@ def main():
             "global_batch": batch * world,
             "parallelism": f"independent shards x{world} (no data-path collective)",
         },
-        "kernels": {"fwd_ms": fwd_ms, "inv_ms": inv_ms},
-        "graph_replay": {"value": world * batch * K / graph_el, "ms_per_step": graph_el / K * 1e3,
-                         "note": "the K timed steps captured as one hipGraph and replayed once"},
+        "kernels": {"timed_launch_ms": launch_ms, "fwd_ms": fwd_ms, "inv_ms": inv_ms,
+                    "note": "timed_launch_ms: HIP events around the timed region / (2 K launches); "
+                            f"fwd_ms / inv_ms: {split_k} back-to-back launches of one direction after it"},
         # the binding limit: integer VALU issue (SIMD cycles per launch at the peak clock vs measured)
         "valu_bound": {
             kind: {"issue_cycles_per_poly": VALU_CYCLES[kind],
@@ -536,7 +547,7 @@ def main():
             for kind, ms in (("fwd", fwd_ms), ("inv", inv_ms))},
         "roofline": {
             "bound": "hbm",
-            "kernel": f"ntt {dom}",
+            "kernel": "ntt_tw_body_kernel fwd / inv (average over the 2 K timed launches)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

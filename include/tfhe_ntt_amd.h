@@ -46,6 +46,13 @@ const char *mi_last_error_message(void);
 int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan **out_plan);
 int mi_ntt64_plan_destroy(mi_ntt64_plan *plan);
 
+/* The process-wide plan cache of Ntt64::new (tfhe/src/core_crypto/commons/math/ntt/ntt64.rs:27-79):
+ * one immutable plan per (n, p, device), built on first use (concurrent first callers build it once)
+ * and shared by every later caller and thread; later lookups are a read-locked map probe.  Cached
+ * plans live until process exit, as the reference's static PLANS map; mi_ntt64_plan_destroy on one
+ * is a no-op.  Same status codes as mi_ntt64_plan_create (the reference panics where it is None). */
+int mi_ntt64_plan_cached(size_t n, uint64_t p, int device, const mi_ntt64_plan **out_plan);
+
 /* Plan::ntt_size / Plan::modulus (prime64.rs:870-878); also the device the plan lives on. */
 int mi_ntt64_plan_info(const mi_ntt64_plan *plan, size_t *n, uint64_t *p, int *device);
 
@@ -129,9 +136,50 @@ int mi_cmux_ntt64_batch(const mi_ntt64_plan *plan, uint64_t *ct0, uint64_t *ct1,
  * both orders give identical values.  MI_NTT64_SOLINAS keys are referenced, not copied (the caller
  * keeps `bsk_ntt` alive).  Replaces the reference's PodStack scratch (ntt64_pbs.rs:705-751). */
 typedef struct mi_pbs_ntt64_key mi_pbs_ntt64_key;
+/* The BNF preparation runs on `stream` (the stream that produced bsk_ntt) and synchronises it before
+ * returning. */
 int mi_pbs_ntt64_key_create(const mi_ntt64_plan *plan, const uint64_t *bsk_ntt, size_t n_lwe, int k, int base_log,
-                            int level, int variant, mi_pbs_ntt64_key **out_key);
+                            int level, int variant, void *stream, mi_pbs_ntt64_key **out_key);
 int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key *key);
+/* n_lwe, k, base_log, level, variant of a key (any pointer may be NULL). */
+int mi_pbs_ntt64_key_info(const mi_pbs_ntt64_key *key, size_t *n_lwe, int *k, int *base_log, int *level,
+                          int *variant);
+
+/* ---- On-disk NTT bootstrap key (entities/ntt_lwe_bootstrap_key.rs:26-33) -----------------------
+ * MI_NTT_BSK_PLAIN     = bincode::serialize(&NttLweBootstrapKey<ABox<[u64]>>) (bincode 1.3, fixint,
+ *                        little-endian): u64 count, count u64 (n_lwe, level, k+1, k+1, N NTT-domain
+ *                        coefficients), polynomial_size, glwe_size, level, base_log as u64, the
+ *                        SerializableCiphertextModulus (u128 modulus, u64 scalar_bits = 64).
+ * MI_NTT_BSK_VERSIONED = bincode of key.versionize() (tfhe-versionable; the type has no `Named` impl,
+ *                        so this is its whole versioned form): u32 1 (NttLweBootstrapKeyVersions::V1),
+ *                        u32 1 (NttGgswCiphertextListVersions::V1), the data sequence, then every scalar
+ *                        field behind its own u32 version tag 0 (PolynomialSizeVersions::V0, ...,
+ *                        SerializableCiphertextModulusVersions::V0).
+ * An NTT key's modulus is the NTT prime for both PBS variants (ntt64_bnf_pbs.rs:44-94; Ntt64::new
+ * asserts a custom modulus, ntt64.rs:38); whether the values are Raw (BNF) or Normalize (Solinas) is not
+ * stored, so loaders take the variant explicitly. */
+typedef enum mi_ntt_bsk_format { MI_NTT_BSK_PLAIN = 0, MI_NTT_BSK_VERSIONED = 1 } mi_ntt_bsk_format;
+typedef struct mi_ntt_bsk_header {
+    uint64_t polynomial_size, glwe_size, level, base_log;
+    uint64_t modulus_lo, modulus_hi; /* u128 ciphertext modulus (0 = native 2^64)                   */
+    uint64_t input_lwe_dimension;    /* count / (level * glwe_size^2 * polynomial_size)              */
+    uint64_t count;                  /* u64 elements of the key data                                 */
+    uint64_t data_offset;            /* byte offset of the first element in the serialised buffer    */
+} mi_ntt_bsk_header;
+/* Parses and validates `len` bytes (truncated / trailing bytes, unknown version tags, scalar_bits != 64
+ * as the reference's TryFrom<SerializableCiphertextModulus>, a modulus above 2^64, data that is not a
+ * whole number of GGSWs, size fields whose product overflows): MI_ERR_INVALID_ARG with the reason in
+ * mi_last_error_message.  A modulus of 2^64 is canonicalised to 0 (native), as TryFrom does. */
+int mi_ntt_bsk_parse(const uint8_t *bytes, size_t len, int format, mi_ntt_bsk_header *out);
+/* Bytes `mi_ntt_bsk_write` produces for header `h` (h->count elements; data_offset ignored). */
+int mi_ntt_bsk_serialized_size(const mi_ntt_bsk_header *h, int format, size_t *out_len);
+/* Serialises host `data` (h->count u64) into `out` (exactly the serialized size). */
+int mi_ntt_bsk_write(const mi_ntt_bsk_header *h, const uint64_t *data, int format, uint8_t *out, size_t out_len);
+/* Loads serialised key bytes (host memory) straight into HBM on the plan's device (one host-to-device
+ * copy on `stream`, no re-layout) and makes a PBS key of `variant` that owns the upload: the stored
+ * polynomial size must equal the plan's, glwe_size 2, and the modulus the plan's prime. */
+int mi_pbs_ntt64_key_load(const mi_ntt64_plan *plan, const uint8_t *bytes, size_t len, int format, int variant,
+                          void *stream, mi_pbs_ntt64_key **out_key);
 
 /* Batched programmable bootstrap: lwe_out[b] = SampleExtract_0(BlindRotate(lut, lwe_in[b])).
  * programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized (ntt64_bnf_pbs.rs:469-540) or
@@ -139,6 +187,44 @@ int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key *key);
  * lwe_in: batch x (n_lwe + 1) u64; lut: one GLWE shared by the batch; lwe_out: batch x (k*N + 1). */
 int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
+
+/* ---- Multi-GPU helpers (single process, several devices) ----------------------------------------
+ * The analogue of the CUDA backend's helper_multi_gpu (backends/tfhe-cuda-backend/cuda/src/utils/
+ * helper_multi_gpu.cu:10-98, helper_multi_gpu.cuh:150-265) for a host that drives several GPUs from one
+ * process (as tfhe-rs's CudaStreams do).  Bootstraps and transforms are independent, so the data path has
+ * no collective: batches are split contiguously (the first total % count devices take one more; with
+ * fewer units than devices the first `total` take one each), read-only state is broadcast once and LWE
+ * batches are scattered from / gathered to the first device with peer-to-peer copies (xGMI links on
+ * MI355X).  A device may appear more than once in a set (e.g. {0, 0} rehearses the split on one GPU).
+ * All copies are asynchronous: ordered after `stream` (on devices[0]) and, for gather / PBS, `stream`
+ * is ordered after them. */
+typedef struct mi_multi_gpu mi_multi_gpu;
+/* cuda_setup_multi_gpu (helper_multi_gpu.cu:11-40): enables peer access between devices[0] and every other
+ * device of the set, and creates one non-blocking stream per entry. */
+int mi_multi_gpu_create(const int *devices, int count, mi_multi_gpu **out);
+int mi_multi_gpu_destroy(mi_multi_gpu *m);
+int mi_multi_gpu_count(const mi_multi_gpu *m, int *count);
+/* device and stream (hipStream_t as void*) of entry `index` (either pointer may be NULL) */
+int mi_multi_gpu_info(const mi_multi_gpu *m, int index, int *device, void **stream);
+int mi_multi_gpu_synchronize(const mi_multi_gpu *m);
+/* get_active_gpu_count (helper_multi_gpu.cu:42-49): min(ceil(num_inputs / 12), gpu_count), at least 1 */
+int mi_multi_gpu_active_count(uint32_t num_inputs, uint32_t gpu_count, uint32_t *out);
+/* get_gpu_offset / get_num_inputs_on_gpu (helper_multi_gpu.cu:51-98): entry `index`'s [offset, offset + n) */
+int mi_multi_gpu_shard(size_t total, int index, int count, size_t *offset, size_t *n);
+/* dsts[i] (on devices[i]) <- `bytes` at src (devices[0]); an entry equal to src is skipped */
+int mi_multi_gpu_broadcast(mi_multi_gpu *m, const void *src, void *const *dsts, size_t bytes, void *stream);
+/* multi_gpu_scatter_lwe_async, trivial index: dsts[i] <- shard i of `total` units of unit_bytes at src */
+int mi_multi_gpu_scatter(mi_multi_gpu *m, const void *src, void *const *dsts, size_t total, size_t unit_bytes,
+                         void *stream);
+/* multi_gpu_gather_lwe_async, trivial index: shard i of dst (devices[0]) <- srcs[i] */
+int mi_multi_gpu_gather(mi_multi_gpu *m, void *dst, const void *const *srcs, size_t total, size_t unit_bytes,
+                        void *stream);
+/* Batched PBS over the device set: scatter lwe_in (devices[0]), mi_pbs_ntt64_batch on every device with
+ * keys[i] / luts[i] (bound to devices[i], same shape), gather into lwe_out (devices[0]).  Shard 0 runs in
+ * place on `stream`; the others use stream-ordered scratch on their device. */
+int mi_pbs_ntt64_multi_gpu(mi_multi_gpu *m, const mi_pbs_ntt64_key *const *keys, uint64_t *lwe_out,
+                           const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
+                           void *stream);
 
 /* ---- prime32::Plan (tfhe-ntt/src/prime32.rs:632-1025) ----------------------------------------
  * The same negacyclic transform and pointwise ops on u32 buffers for a prime p < 2^32.  try_new
@@ -194,12 +280,13 @@ int mi_native_polymul_batch(const mi_native_plan *plan, void *prod, const void *
  * mi_lwe_ksk_create takes the reference's LweKeyswitchKey layout as a device pointer: in_dim blocks of
  * `level` LWE ciphertexts of out_dim + 1 u64, levels stored as generate_lwe_keyswitch_key writes them
  * (lwe_keyswitch_key_generation.rs:169-199), and prepares a private device copy (the caller's buffer
- * may be freed afterwards).  MI_ERR_INVALID_ARG where SignedDecomposer::new would assert
+ * may be freed afterwards; the preparation runs on `stream`, the stream that produced `ksk`, and synchronises
+ * it).  MI_ERR_INVALID_ARG where SignedDecomposer::new would assert
  * (base_log * level >= 64); MI_ERR_UNSUPPORTED when in_dim * level * ceil((base_log + 1) / 8) >= 2^17
  * (beyond the exact int32 accumulation of the int8 matrix-core path). */
 typedef struct mi_lwe_ksk mi_lwe_ksk;
 int mi_lwe_ksk_create(const uint64_t *ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device,
-                      mi_lwe_ksk **out_key);
+                      void *stream, mi_lwe_ksk **out_key);
 int mi_lwe_ksk_destroy(mi_lwe_ksk *key);
 int mi_lwe_ksk_info(const mi_lwe_ksk *key, size_t *in_dim, size_t *out_dim, int *base_log, int *level);
 /* keyswitch_lwe_ciphertext_native_mod_compatible (lwe_keyswitch.rs:137-227) over a batch:

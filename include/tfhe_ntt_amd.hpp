@@ -17,6 +17,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -191,10 +192,21 @@ inline void cmux_ntt64_assign(const prime64::Plan& plan, uint64_t* ct0, uint64_t
 // An NTT-domain bootstrap key bound to a plan (entities/ntt_lwe_bootstrap_key.rs); move-only.
 class NttBootstrapKey {
  public:
+  // `stream`: the stream that produced bsk_ntt (the BNF preparation is ordered after it)
   NttBootstrapKey(const prime64::Plan& plan, const uint64_t* bsk_ntt, size_t n_lwe, int base_log, int level,
-                  int variant)
+                  int variant, void* stream = nullptr)
       : n_lwe_(n_lwe), variant_(variant) {
-    check(mi_pbs_ntt64_key_create(plan.raw(), bsk_ntt, n_lwe, 1, base_log, level, variant, &raw_));
+    check(mi_pbs_ntt64_key_create(plan.raw(), bsk_ntt, n_lwe, 1, base_log, level, variant, stream, &raw_));
+  }
+  // Serialised key bytes (MI_NTT_BSK_PLAIN / MI_NTT_BSK_VERSIONED) loaded straight into HBM
+  // (mi_pbs_ntt64_key_load); `variant` is explicit: Raw (BNF) and Normalize (Solinas) keys store the same fields.
+  static NttBootstrapKey load(const prime64::Plan& plan, const uint8_t* bytes, size_t len, int variant,
+                              int format = MI_NTT_BSK_PLAIN, void* stream = nullptr) {
+    mi_pbs_ntt64_key* raw = nullptr;
+    check(mi_pbs_ntt64_key_load(plan.raw(), bytes, len, format, variant, stream, &raw));
+    size_t n_lwe = 0;
+    check(mi_pbs_ntt64_key_info(raw, &n_lwe, nullptr, nullptr, nullptr, nullptr));
+    return NttBootstrapKey(raw, n_lwe, variant);
   }
   NttBootstrapKey(NttBootstrapKey&& o) noexcept
       : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_), variant_(o.variant_) {}
@@ -208,6 +220,7 @@ class NttBootstrapKey {
   int variant() const noexcept { return variant_; }
 
  private:
+  NttBootstrapKey(mi_pbs_ntt64_key* raw, size_t n_lwe, int variant) : raw_(raw), n_lwe_(n_lwe), variant_(variant) {}
   mi_pbs_ntt64_key* raw_ = nullptr;
   size_t n_lwe_;
   int variant_;
@@ -224,9 +237,10 @@ inline void programmable_bootstrap_ntt64_lwe_ciphertext(const NttBootstrapKey& k
 // entities/lwe_keyswitch_key.rs + algorithms/lwe_keyswitch.rs:103-227 (native modulus); move-only
 class LweKeyswitchKey {
  public:
-  LweKeyswitchKey(const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device = 0)
+  LweKeyswitchKey(const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device = 0,
+                  void* stream = nullptr)
       : in_(in_dim), out_(out_dim) {
-    check(mi_lwe_ksk_create(ksk, in_dim, out_dim, base_log, level, device, &raw_));
+    check(mi_lwe_ksk_create(ksk, in_dim, out_dim, base_log, level, device, stream, &raw_));
   }
   LweKeyswitchKey(LweKeyswitchKey&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), in_(o.in_), out_(o.out_) {}
   LweKeyswitchKey(const LweKeyswitchKey&) = delete;
@@ -248,60 +262,33 @@ inline void keyswitch_lwe_ciphertext(const LweKeyswitchKey& key, const uint64_t*
   check(mi_lwe_keyswitch_batch(key.raw(), lwe_out, lwe_in, batch, stream));
 }
 
-// On-disk NTT bootstrap key: the bytes bincode 1.3 writes for NttLweBootstrapKey<ABox<[u64]>>
-// (entities/ntt_lwe_bootstrap_key.rs:26-33, entities/ntt_ggsw_ciphertext_list.rs:21-31,
-// commons/ciphertext_modulus.rs:48-93): u64 count, count u64 elements (n_lwe, level, k+1, k+1, N),
-// then polynomial_size, glwe_size, level, base_log as u64, the modulus as u128 (0 = native 2^64) and
-// scalar_bits = 64 as u64, all little-endian.  Same layout as tfhe_ntt_amd/ntt_bsk_format.py.
-struct NttBskFields {
-  uint64_t polynomial_size = 0, glwe_size = 0, level = 0, base_log = 0;
-  uint64_t modulus_lo = 0, modulus_hi = 0;  // u128 ciphertext modulus
-  uint64_t input_lwe_dimension = 0;
-};
+// On-disk NTT bootstrap key (entities/ntt_lwe_bootstrap_key.rs:26-33): plain bincode or the versioned
+// form, parsed and written by the library (mi_ntt_bsk_parse / mi_ntt_bsk_write, pure host code, no
+// device needed); the layouts are documented in include/tfhe_ntt_amd.h.  Same bytes as
+// tfhe_ntt_amd/ntt_bsk_format.py.
+using NttBskFields = mi_ntt_bsk_header;
 
-namespace detail {
-inline void put_u64(std::vector<uint8_t>& out, uint64_t v) {
-  for (int i = 0; i < 8; ++i) out.push_back(static_cast<uint8_t>(v >> (8 * i)));
-}
-inline uint64_t get_u64(const uint8_t* p) {
-  uint64_t v = 0;
-  for (int i = 7; i >= 0; --i) v = v << 8 | p[i];
-  return v;
-}
-}  // namespace detail
-
-inline std::vector<uint8_t> serialize_ntt_bsk(const uint64_t* data, size_t count, const NttBskFields& f) {
-  const uint64_t ggsw = f.level * f.glwe_size * f.glwe_size * f.polynomial_size;
-  if (ggsw == 0 || count % ggsw) throw std::invalid_argument("NTT BSK: data is not a whole number of GGSWs");
-  std::vector<uint8_t> out;
-  out.reserve(8 + 8 * count + 56);
-  detail::put_u64(out, count);
-  for (size_t i = 0; i < count; ++i) detail::put_u64(out, data[i]);
-  for (uint64_t v : {f.polynomial_size, f.glwe_size, f.level, f.base_log, f.modulus_lo, f.modulus_hi, uint64_t{64}})
-    detail::put_u64(out, v);
+inline std::vector<uint8_t> serialize_ntt_bsk(const uint64_t* data, size_t count, NttBskFields f,
+                                              int format = MI_NTT_BSK_PLAIN) {
+  f.count = count;
+  size_t len = 0;
+  check(mi_ntt_bsk_serialized_size(&f, format, &len));
+  std::vector<uint8_t> out(len);
+  const int st = mi_ntt_bsk_write(&f, data, format, out.data(), out.size());
+  if (st == MI_ERR_INVALID_ARG) throw std::invalid_argument(mi_last_error_message());
+  check(st);
   return out;
 }
 
-// Throws std::invalid_argument on truncated / trailing bytes, scalar_bits != 64 (the reference's
-// TryFrom<SerializableCiphertextModulus> error) or a data length that is not a whole number of GGSWs.
-inline NttBskFields deserialize_ntt_bsk(const uint8_t* buf, size_t len, std::vector<uint64_t>& data) {
-  if (len < 8) throw std::invalid_argument("NTT BSK: truncated");
-  const uint64_t count = detail::get_u64(buf);
-  if (count > (len - 8) / 8 || len != 8 + 8 * count + 56) throw std::invalid_argument("NTT BSK: length mismatch");
-  const uint8_t* t = buf + 8 + 8 * count;
-  NttBskFields f;
-  f.polynomial_size = detail::get_u64(t);
-  f.glwe_size = detail::get_u64(t + 8);
-  f.level = detail::get_u64(t + 16);
-  f.base_log = detail::get_u64(t + 24);
-  f.modulus_lo = detail::get_u64(t + 32);
-  f.modulus_hi = detail::get_u64(t + 40);
-  if (detail::get_u64(t + 48) != 64) throw std::invalid_argument("NTT BSK: scalar_bits != 64");
-  const uint64_t ggsw = f.level * f.glwe_size * f.glwe_size * f.polynomial_size;
-  if (ggsw == 0 || count % ggsw) throw std::invalid_argument("NTT BSK: data is not a whole number of GGSWs");
-  f.input_lwe_dimension = count / ggsw;
-  data.resize(count);
-  for (uint64_t i = 0; i < count; ++i) data[i] = detail::get_u64(buf + 8 + 8 * i);
+// Throws std::invalid_argument on malformed bytes (see mi_ntt_bsk_parse).
+inline NttBskFields deserialize_ntt_bsk(const uint8_t* buf, size_t len, std::vector<uint64_t>& data,
+                                        int format = MI_NTT_BSK_PLAIN) {
+  NttBskFields f{};
+  const int st = mi_ntt_bsk_parse(buf, len, format, &f);
+  if (st == MI_ERR_INVALID_ARG) throw std::invalid_argument(mi_last_error_message());
+  check(st);
+  data.resize(f.count);
+  if (f.count) std::memcpy(data.data(), buf + f.data_offset, f.count * sizeof(uint64_t));
   return f;
 }
 

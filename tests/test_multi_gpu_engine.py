@@ -1,0 +1,211 @@
+"""Config 5's split through the real engine.
+
+* CPU: the C-ABI shard arithmetic (``mi_multi_gpu_shard`` / ``_active_count``) equals the reference's
+  get_num_inputs_on_gpu / get_gpu_offset / get_active_gpu_count (helper_multi_gpu.cu:42-98, restated
+  below with its float ceil) and ``multi_gpu.shard_bounds``.
+* GPU, one process: ``DeviceSet([0, 0, 0])`` scatters a batch from entry 0, bootstraps every shard with the
+  real PBS and gathers it back (``mi_pbs_ntt64_multi_gpu``): identical to one launch and to the oracle.
+* GPU, two processes (world size 2, gloo, both ranks on cuda:0 — the one-GPU rehearsal of the RCCL path):
+  the root holds the global LWE batch and the key, broadcasts the key, scatters the batch, every rank runs
+  the real NTT and PBS on its shard, the root gathers; the gathered result equals the single-rank run and
+  the oracle.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import tfhe_helpers as H
+
+P = 0xFFFFFFFF00000001
+N = 2048
+
+
+def _ref_inputs_on_gpu(total, i, count):
+    """helper_multi_gpu.cu:66-98, restated as written (float ceil, cutoff)."""
+    if count > total:
+        return 1 if i < total else 0
+    if total % count == 0:
+        small = large = total // count
+        cutoff = 0
+    else:
+        y = math.ceil(total / count) * count - total
+        cutoff = count - y
+        small, large = total // count, math.ceil(total / count)
+    return large if i < cutoff else small
+
+
+def test_shard_arithmetic_matches_reference(engine):
+    mg = engine.multi_gpu
+    for total in (0, 1, 5, 8, 9, 4095, 4096, 65536, 65537):
+        for count in (1, 2, 3, 7, 8):
+            off = 0
+            for i in range(count):
+                n = _ref_inputs_on_gpu(total, i, count)
+                assert mg.lib_shard(total, i, count) == (off, off + n), (total, count, i)
+                if total >= count:
+                    assert mg.shard_bounds(total, count, i) == (off, off + n)
+                off += n
+    for num_inputs in (0, 1, 12, 13, 100, 10**6):
+        for g in (1, 2, 8):
+            assert mg.lib_active_count(num_inputs, g) == min(max(1, -(-num_inputs // 12)), g)
+    with pytest.raises(engine.MiError):
+        mg.lib_shard(10, 3, 3)
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64)).cuda()
+
+
+def _host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("entries,batch", [(2, 9), (3, 10), (3, 2)])
+def test_device_set_pbs_scatter_gather(engine, oracle, entries, batch):
+    import torch
+    M = engine.ntt64_pbs
+    g = H.rng(900 + entries + batch)
+    n_lwe = 20
+    plan = engine.Plan.try_new(N, P)
+    bsk = g.integers(0, P, size=(n_lwe, 1, 2, 2, N), dtype=np.uint64)
+    lut = H.uniform_u64(g, (2, N))
+    lwe = H.uniform_u64(g, (batch, n_lwe + 1))
+    key = M.NttBootstrapKey(plan, _dev(bsk), 23, 1, M.BNF)
+    ds = engine.multi_gpu.DeviceSet([0] * entries)
+    # scatter / gather round trip and broadcast
+    src = _dev(lwe)
+    shards = [torch.empty((b - a, n_lwe + 1), dtype=torch.int64, device="cuda") for a, b in
+              (ds.shard(batch, i) for i in range(entries))]
+    ds.scatter(src, shards)
+    back = torch.zeros_like(src)
+    ds.gather(back, shards)
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(back), lwe)
+    copies = [torch.zeros(2, N, dtype=torch.int64, device="cuda") for _ in range(entries)]
+    lt = _dev(lut)
+    ds.broadcast(lt, copies)
+    ds.synchronize()
+    assert all(np.array_equal(_host(c), lut) for c in copies)
+    # the multi-device PBS == one launch == the oracle
+    out_multi = torch.zeros((batch, N + 1), dtype=torch.int64, device="cuda")
+    ds.programmable_bootstrap([key] * entries, src, out_multi, copies)
+    out_one = torch.zeros_like(out_multi)
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(src, out_one, lt, key)
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(out_multi), _host(out_one))
+    ctx = oracle.NttContext(N)
+    assert np.array_equal(_host(out_multi)[-1], ctx.pbs(lwe[-1], lut.reshape(-1), bsk.reshape(-1), 1, 23, 1, bnf=True))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+GLOBAL_PBS, GLOBAL_POLYS, N_LWE = 11, 13, 24
+
+
+def _rank_main(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "tfhe-rs-main_modified_amd"), os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import tfhe_ntt_amd as eng
+        mg, M = eng.multi_gpu, eng.ntt64_pbs
+        torch.cuda.set_device(0)
+        plan = eng.Plan.try_new(N, P)
+        g = H.rng(4242)
+        # the root's state: key, LUT, global batches (host tensors: gloo moves host memory)
+        if rank == 0:
+            bsk = torch.from_numpy(g.integers(0, P, size=(N_LWE, 1, 2, 2, N), dtype=np.uint64).view(np.int64))
+            lut = torch.from_numpy(H.uniform_u64(g, (2, N)).view(np.int64))
+            lwe_all = torch.from_numpy(H.uniform_u64(g, (GLOBAL_PBS, N_LWE + 1)).view(np.int64))
+            polys_all = torch.from_numpy(g.integers(0, P, size=(GLOBAL_POLYS, N), dtype=np.uint64).view(np.int64))
+        else:
+            bsk = torch.zeros((N_LWE, 1, 2, 2, N), dtype=torch.int64)
+            lut = torch.zeros((2, N), dtype=torch.int64)
+            lwe_all = polys_all = None
+        mg.broadcast_(bsk)
+        mg.broadcast_(lut)
+        a, b = mg.shard_bounds(GLOBAL_PBS, world, rank)
+        lwe = torch.empty((b - a, N_LWE + 1), dtype=torch.int64)
+        mg.scatter_batch(lwe_all, lwe)
+        pa, pb = mg.shard_bounds(GLOBAL_POLYS, world, rank)
+        polys = torch.empty((pb - pa, N), dtype=torch.int64)
+        mg.scatter_batch(polys_all, polys)
+        # the real engine on this rank's shard
+        key = M.NttBootstrapKey(plan, bsk.cuda(), 23, 1, M.BNF)
+        out = torch.zeros((b - a, N + 1), dtype=torch.int64, device="cuda")
+        if b > a:
+            M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe.cuda(), out, lut.cuda(), key)
+        tp = polys.cuda()
+        if pb > pa:
+            plan.fwd(tp)
+        torch.cuda.synchronize()
+        out_all = torch.zeros((GLOBAL_PBS, N + 1), dtype=torch.int64) if rank == 0 else None
+        fwd_all = torch.zeros((GLOBAL_POLYS, N), dtype=torch.int64) if rank == 0 else None
+        mg.gather_batch(out.cpu(), out_all)
+        mg.gather_batch(tp.cpu(), fwd_all)
+        if rank == 0:
+            # single-rank reference run of the same global batches
+            one = torch.zeros((GLOBAL_PBS, N + 1), dtype=torch.int64, device="cuda")
+            M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe_all.cuda(), one, lut.cuda(), key)
+            tp1 = polys_all.cuda()
+            plan.fwd(tp1)
+            torch.cuda.synchronize()
+            assert torch.equal(out_all, one.cpu()), "sharded PBS != single-rank PBS"
+            assert torch.equal(fwd_all, tp1.cpu()), "sharded NTT != single-rank NTT"
+            np.save(os.environ["MI_MG_OUT"] + "_pbs.npy", out_all.numpy())
+            np.save(os.environ["MI_MG_OUT"] + "_fwd.npy", fwd_all.numpy())
+            np.save(os.environ["MI_MG_OUT"] + "_in.npy", lwe_all.numpy())
+            np.save(os.environ["MI_MG_OUT"] + "_polys.npy", polys_all.numpy())
+            np.save(os.environ["MI_MG_OUT"] + "_bsk.npy", bsk.numpy())
+            np.save(os.environ["MI_MG_OUT"] + "_lut.npy", lut.numpy())
+        q.put((rank, "ok"))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_real_engine(oracle, tmp_path):
+    import torch.multiprocessing as mp
+    os.environ["MI_MG_OUT"] = str(tmp_path / "mg")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    results = sorted(q.get(timeout=5) for _ in range(2))
+    assert not alive and results == [(0, "ok"), (1, "ok")], results
+    base = str(tmp_path / "mg")
+    out = np.load(base + "_pbs.npy").view(np.uint64)
+    lwe = np.load(base + "_in.npy").view(np.uint64)
+    bsk = np.load(base + "_bsk.npy").view(np.uint64)
+    lut = np.load(base + "_lut.npy").view(np.uint64)
+    want = oracle.NttContext(N).pbs_batch_bnf(lwe, lut.reshape(-1), bsk.reshape(-1), 1, 23, 1, threads=8)
+    assert np.array_equal(out, want)
+    polys = np.load(base + "_polys.npy").view(np.uint64)
+    assert np.array_equal(np.load(base + "_fwd.npy").view(np.uint64), oracle.Plan.try_new(N, P).fwd(polys))

@@ -53,13 +53,11 @@ def test_bsk_conversion(engine, plan, ctx, width, normalize):
     assert np.array_equal(host(d), want)
 
 
-@pytest.mark.parametrize("bnf,kernel", [(True, "default"), (True, "generic"), (False, "default")])
+@pytest.mark.parametrize("bnf", [True, False])
 @pytest.mark.parametrize("base_log,level", [(23, 1), (12, 2), (7, 3), (1, 1), (21, 3), (31, 1)])
-def test_external_product_parity(engine, plan, ctx, monkeypatch, bnf, kernel, base_log, level):
-    """BNF level 1 (base_log <= 31) runs on the twisted-transform kernel by default (pbs_tw.hip);
-    'generic' forces pbs_kernels.hip (MI_PBS_VARIANT=0)."""
-    if kernel == "generic":
-        monkeypatch.setenv("MI_PBS_VARIANT", "0")
+def test_external_product_parity(engine, plan, ctx, bnf, base_log, level):
+    """BNF level 1 (base_log <= 31) runs on the twisted-transform kernel (pbs_tw.hip), the other
+    shapes on the generic one (pbs_kernels.hip)."""
     q = 0 if bnf else P
     g = H.rng(base_log * 10 + level + 1000 * bnf)
     batch = 6
@@ -78,10 +76,8 @@ def test_external_product_parity(engine, plan, ctx, monkeypatch, bnf, kernel, ba
     assert np.array_equal(host(tg), glwe)  # input untouched
 
 
-@pytest.mark.parametrize("bnf,kernel", [(True, "default"), (True, "generic"), (False, "default")])
-def test_cmux_parity(engine, plan, ctx, monkeypatch, bnf, kernel):
-    if kernel == "generic":
-        monkeypatch.setenv("MI_PBS_VARIANT", "0")
+@pytest.mark.parametrize("bnf", [True, False])
+def test_cmux_parity(engine, plan, ctx, bnf):
     q = 0 if bnf else P
     g = H.rng(7 + bnf)
     batch, base_log, level = 5, 23, 1
@@ -130,13 +126,9 @@ def test_pbs_parity_random_key(engine, plan, ctx, oracle, bnf, centered, level, 
     assert np.array_equal(host(out), want)
 
 
-@pytest.mark.parametrize("kernel", ["twisted", "generic"])
-def test_pbs_parity_config4_shape(engine, plan, ctx, monkeypatch, kernel):
+def test_pbs_parity_config4_shape(engine, plan, ctx):
     """PARAM_MESSAGE_2_CARRY_2 shape (n = 918, beta = 2^23, l = 1, BNF) on a random key, vs the
-    multi-threaded oracle; both the twisted-transform kernel (default, pbs_tw.hip) and the generic
-    one (pbs_kernels.hip, MI_PBS_VARIANT=0)."""
-    if kernel == "generic":
-        monkeypatch.setenv("MI_PBS_VARIANT", "0")
+    multi-threaded oracle (twisted-transform kernel, pbs_tw.hip)."""
     g = H.rng(918)
     n_lwe, batch, base_log, level = 918, 48, 23, 1
     bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)

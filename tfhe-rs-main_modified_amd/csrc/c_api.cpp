@@ -8,75 +8,32 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
-#include "../../include/tfhe_ntt_amd.h"
-#include "host_math.hpp"
-#include "ntt64_launch.hpp"
+#include "c_api_internal.hpp"
 #include "ntt64_tw_tables.hpp"
 
-using mi::host::u128;
-using mi::host::u64;
+namespace mi {
+namespace capi {
+std::string& last_error() {
+  thread_local std::string msg;
+  return msg;
+}
+}  // namespace capi
+}  // namespace mi
 
-struct mi_ntt64_plan {
-  size_t n = 0;
-  int logn = 0;
-  u64 p = 0;
-  int device = 0;
-  bool goldilocks = false;
-  int variant = 0;
-  std::vector<u64> twid, inv_twid;  // canonical host tables (reference layout)
-  u64 n_inv = 0;
-  mi::MontParams mp;
-  u64 c_normalize = 0, c_man = 0, c_macc = 0;  // device constants of the pointwise ops
-  u64* d_twid = nullptr;
-  u64* d_inv_twid = nullptr;
-  // twisted N = 2048 Solinas transform (ntt64_tw.hip): rho_i^j and rho_i^-j, 64 i + j
-  u64* d_twist_f = nullptr;
-  u64* d_twist_i = nullptr;
-};
+using namespace mi::capi;
 
 namespace {
 
-thread_local std::string g_last_error;
-
-int fail(int status, const std::string& msg) {
-  g_last_error = msg;
-  return status;
-}
-
-int hip_fail(hipError_t e, const char* what) {
-  return fail(MI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-struct DeviceGuard {
-  int prev = -1;
-  bool ok = true;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
 u64 mont_form(u64 x, u64 p) { return (u64)(((u128)x << 64) % p); }
-
-// MI_NTT_VARIANT selects a kernel family for benchmarking (-1 / unset = the default choice).
-int env_variant() {
-  const char* v = std::getenv("MI_NTT_VARIANT");
-  return v ? std::atoi(v) : -1;
-}
-
-// MI_PBS_VARIANT=0 forces the generic PBS kernel (pbs_kernels.hip) where the twisted one applies.
-int env_pbs_variant() {
-  const char* v = std::getenv("MI_PBS_VARIANT");
-  return v ? std::atoi(v) : -1;
-}
 
 }  // namespace
 
@@ -95,7 +52,7 @@ const char* mi_status_string(int status) {
   }
 }
 
-const char* mi_last_error_message(void) { return g_last_error.c_str(); }
+const char* mi_last_error_message(void) { return last_error().c_str(); }
 
 int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_plan) {
   if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
@@ -115,7 +72,6 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   plan->p = p;
   plan->device = device;
   plan->goldilocks = (p == mi::host::SOLINAS_P);
-  plan->variant = env_variant();
 
   // prime64.rs:162-182: Solinas uses the hard-coded friendly root tower, other primes the
   // Tonelli-Shanks root.
@@ -221,14 +177,13 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
       }
     }
   }
-  // default kernel: the twisted shift-twiddle transform where it applies, else the window kernels
-  if (plan->variant < 0) plan->variant = plan->d_twist_f ? 4 : 0;
+  plan->twisted = plan->d_twist_f != nullptr;
   *out_plan = plan;
   return MI_OK;
 }
 
 int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
-  if (!plan) return MI_OK;
+  if (!plan || plan->cached) return MI_OK;
   {
     DeviceGuard g(plan->device);
     if (plan->d_twid) (void)hipFree(plan->d_twid);
@@ -236,6 +191,46 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
     if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);  // d_twist_i points into the same allocation
   }
   delete plan;
+  return MI_OK;
+}
+
+// Ntt64::new's PLANS map (ntt64.rs:27-79): a read-locked probe, then one slot per key built under its
+// own once-flag so concurrent first users of one (n, p, device) build it once and other keys are not
+// blocked behind that build.
+int mi_ntt64_plan_cached(size_t n, uint64_t p, int device, const mi_ntt64_plan** out_plan) {
+  if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
+  *out_plan = nullptr;
+  struct Slot {
+    std::once_flag once;
+    mi_ntt64_plan* plan = nullptr;
+    int status = MI_OK;
+    std::string error;
+  };
+  static std::shared_mutex mu;
+  static std::map<std::tuple<size_t, uint64_t, int>, std::unique_ptr<Slot>>* plans =
+      new std::map<std::tuple<size_t, uint64_t, int>, std::unique_ptr<Slot>>;  // never destroyed, like PLANS
+  const auto key = std::make_tuple(n, p, device);
+  Slot* slot = nullptr;
+  {
+    std::shared_lock<std::shared_mutex> rd(mu);
+    auto it = plans->find(key);
+    if (it != plans->end()) slot = it->second.get();
+  }
+  if (!slot) {
+    std::unique_lock<std::shared_mutex> wr(mu);
+    auto& ent = (*plans)[key];
+    if (!ent) ent.reset(new Slot);
+    slot = ent.get();
+  }
+  std::call_once(slot->once, [&] {
+    slot->status = mi_ntt64_plan_create(n, p, device, &slot->plan);
+    if (slot->status == MI_OK)
+      slot->plan->cached = true;
+    else
+      slot->error = last_error();
+  });
+  if (slot->status != MI_OK) return fail(slot->status, slot->error);
+  *out_plan = slot->plan;
   return MI_OK;
 }
 
@@ -264,14 +259,14 @@ static int check_batch(const mi_ntt64_plan* plan, const void* buf, size_t batch,
   return MI_OK;
 }
 
-// Variant routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan when its tables
-// exist (MI_NTT_VARIANT=4), else the register-window kernels.
+// Kernel routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan, else the
+// register-window kernels.  One kernel per plan shape; nothing in the environment changes it.
 static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride,
                                    hipStream_t s) {
-  if (plan->variant >= 4 && plan->variant <= 7 && plan->d_twist_f)
-    return mi::launch_ntt_tw(fwd, plan->variant, buf, batch, stride, fwd ? plan->d_twist_f : plan->d_twist_i, s);
-  return mi::launch_ntt(fwd, plan->logn, plan->variant >= 4 ? 0 : plan->variant, plan->goldilocks, plan->mp, buf,
-                        batch, stride, fwd ? plan->d_twid : plan->d_inv_twid, s);
+  if (plan->twisted)
+    return mi::launch_ntt_tw(fwd, buf, batch, stride, fwd ? plan->d_twist_f : plan->d_twist_i, s);
+  return mi::launch_ntt(fwd, plan->logn, plan->goldilocks, plan->mp, buf, batch, stride,
+                        fwd ? plan->d_twid : plan->d_inv_twid, s);
 }
 
 static int run_ntt(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride, void* stream) {
@@ -346,15 +341,9 @@ int mi_fill_uniform(uint64_t* buf, size_t count, uint64_t seed, uint64_t p, int 
 
 // ---- external product / PBS ------------------------------------------------------------------
 
-struct mi_pbs_ntt64_key {
-  const mi_ntt64_plan* plan = nullptr;
-  size_t n_lwe = 0;
-  int k = 1, base_log = 0, level = 0, variant = 0;
-  const u64* bsk = nullptr;  // what the kernel reads
-  u64* owned = nullptr;      // BNF: private copy with N^{-1} folded in
-};
+}  // extern "C"
 
-static int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant) {
+int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant) {
   if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
   if (variant != MI_NTT64_SOLINAS && variant != MI_NTT64_BNF) return fail(MI_ERR_INVALID_ARG, "unknown variant");
   if (level < 1 || base_log < 1 || base_log * level > 63)
@@ -365,10 +354,12 @@ static int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int l
   return MI_OK;
 }
 
+extern "C" {
+
 // the twisted-transform bodies (pbs_tw.hip) cover BNF, level 1, base_log <= 31 on the Solinas N = 2048
-// plan; MI_PBS_VARIANT=0 forces the generic kernels
+// plan; every other shape runs the generic kernels (pbs_kernels.hip)
 static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int base_log, int level) {
-  return variant == MI_NTT64_BNF && level == 1 && base_log <= 31 && plan->d_twist_f && env_pbs_variant() != 0;
+  return variant == MI_NTT64_BNF && level == 1 && base_log <= 31 && plan->twisted;
 }
 
 int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
@@ -422,8 +413,18 @@ int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1,
   return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
 }
 
+}  // extern "C"
+
+int mi::capi::prepare_bnf_key(const mi_ntt64_plan* plan, u64* dst, const u64* src, size_t count, hipStream_t stream) {
+  hipError_t e = mi::launch_scale(dst, src, count, plan->n_inv, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "bootstrap key normalisation");
+}
+
+extern "C" {
+
 int mi_pbs_ntt64_key_create(const mi_ntt64_plan* plan, const uint64_t* bsk_ntt, size_t n_lwe, int k, int base_log,
-                            int level, int variant, mi_pbs_ntt64_key** out_key) {
+                            int level, int variant, void* stream, mi_pbs_ntt64_key** out_key) {
   if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
   *out_key = nullptr;
   int st = check_pbs_shape(plan, k, base_log, level, variant);
@@ -446,12 +447,12 @@ int mi_pbs_ntt64_key_create(const mi_ntt64_plan* plan, const uint64_t* bsk_ntt, 
       delete key;
       return fail(MI_ERR_OOM, "bootstrap key copy allocation failed");
     }
-    hipError_t e = mi::launch_scale(key->owned, bsk_ntt, count, plan->n_inv, nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess) {
+    // ordered after the work that produced bsk_ntt on `stream` (the caller's stream)
+    st = prepare_bnf_key(plan, key->owned, bsk_ntt, count, (hipStream_t)stream);
+    if (st != MI_OK) {
       (void)hipFree(key->owned);
       delete key;
-      return hip_fail(e, "bootstrap key normalisation");
+      return st;
     }
     key->bsk = key->owned;
   }
@@ -729,7 +730,7 @@ struct mi_lwe_ksk {
 };
 
 int mi_lwe_ksk_create(const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int device,
-                      mi_lwe_ksk** out_key) {
+                      void* stream, mi_lwe_ksk** out_key) {
   if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
   *out_key = nullptr;
   if (!ksk) return fail(MI_ERR_INVALID_ARG, "ksk is NULL");
@@ -757,8 +758,9 @@ int mi_lwe_ksk_create(const uint64_t* ksk, size_t in_dim, size_t out_dim, int ba
     delete key;
     return fail(MI_ERR_OOM, "keyswitch key allocation failed");
   }
-  hipError_t e = mi::launch_ksk_prepare(key->frag, ksk, in_dim, out_dim, base_log, level, nullptr);
-  if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+  // ordered after the work that produced `ksk` on the caller's stream
+  hipError_t e = mi::launch_ksk_prepare(key->frag, ksk, in_dim, out_dim, base_log, level, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
   if (e != hipSuccess) {
     (void)hipFree(key->frag);
     delete key;

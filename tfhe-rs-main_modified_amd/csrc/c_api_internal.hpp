@@ -1,0 +1,76 @@
+// c_api_internal.hpp — state shared by the C-ABI translation units (c_api*.cpp): the opaque handle
+// structs of include/tfhe_ntt_amd.h and the error / device helpers.  Not part of the public surface.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/tfhe_ntt_amd.h"
+#include "host_math.hpp"
+#include "ntt64_launch.hpp"
+
+using mi::host::u128;
+using mi::host::u64;
+
+struct mi_ntt64_plan {
+  size_t n = 0;
+  int logn = 0;
+  u64 p = 0;
+  int device = 0;
+  bool goldilocks = false;
+  bool twisted = false;  // N = 2048 Solinas: the twisted shift-twiddle kernel (ntt64_tw.hip)
+  bool cached = false;   // owned by the process-wide plan cache (mi_ntt64_plan_cached); destroy is a no-op
+  std::vector<u64> twid, inv_twid;  // canonical host tables (reference layout)
+  u64 n_inv = 0;
+  mi::MontParams mp;
+  u64 c_normalize = 0, c_man = 0, c_macc = 0;  // device constants of the pointwise ops
+  u64* d_twid = nullptr;
+  u64* d_inv_twid = nullptr;
+  // twisted N = 2048 Solinas transform (ntt64_tw.hip): rho_i^j and rho_i^-j, 64 i + j
+  u64* d_twist_f = nullptr;
+  u64* d_twist_i = nullptr;
+};
+
+struct mi_pbs_ntt64_key {
+  const mi_ntt64_plan* plan = nullptr;
+  size_t n_lwe = 0;
+  int k = 1, base_log = 0, level = 0, variant = 0;
+  const u64* bsk = nullptr;  // what the kernel reads
+  u64* owned = nullptr;      // BNF: private copy with N^{-1} folded in; loaded keys: the uploaded bytes
+};
+
+namespace mi {
+namespace capi {
+
+std::string& last_error();
+
+inline int fail(int status, const std::string& msg) {
+  last_error() = msg;
+  return status;
+}
+
+inline int hip_fail(hipError_t e, const char* what) {
+  return fail(MI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// shared by mi_pbs_ntt64_key_create and mi_pbs_ntt64_key_load
+int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant);
+// BNF keys: N^{-1} folded into `dst` (dst may equal src); synchronises `stream`
+int prepare_bnf_key(const mi_ntt64_plan* plan, u64* dst, const u64* src, size_t count, hipStream_t stream);
+
+}  // namespace capi
+}  // namespace mi

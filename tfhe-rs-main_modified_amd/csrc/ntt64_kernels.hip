@@ -78,7 +78,7 @@ static hipError_t launch_window(IO* data, size_t batch, size_t stride, const u64
 }
 
 template <bool FWD, class Mod, class IO>
-static hipError_t dispatch(int logn, int variant, IO* data, size_t batch, size_t stride, const u64* tw,
+static hipError_t dispatch(int logn, IO* data, size_t batch, size_t stride, const u64* tw,
                            const Mod& mod, hipStream_t s) {
   switch (logn) {
     case 4: return launch_window<4, 3, FWD>(data, batch, stride, tw, mod, s);
@@ -88,9 +88,7 @@ static hipError_t dispatch(int logn, int variant, IO* data, size_t batch, size_t
     case 8: return launch_window<8, 3, FWD>(data, batch, stride, tw, mod, s);
     case 9: return launch_window<9, 3, FWD>(data, batch, stride, tw, mod, s);
     case 10: return launch_window<10, 3, FWD>(data, batch, stride, tw, mod, s);
-    case 11:
-      if (variant == 1) return launch_window<11, 4, FWD>(data, batch, stride, tw, mod, s);
-      return launch_window<11, 3, FWD>(data, batch, stride, tw, mod, s);
+    case 11: return launch_window<11, 3, FWD>(data, batch, stride, tw, mod, s);
     case 12: return launch_window<12, 3, FWD>(data, batch, stride, tw, mod, s);
     case 13: return launch_window<13, 3, FWD>(data, batch, stride, tw, mod, s);
     case 14: return launch_window<14, 4, FWD>(data, batch, stride, tw, mod, s);
@@ -98,27 +96,20 @@ static hipError_t dispatch(int logn, int variant, IO* data, size_t batch, size_t
   }
 }
 
-hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, u64* data,
-                      size_t batch, size_t stride, const u64* tw, hipStream_t s) {
+hipError_t launch_ntt(bool fwd, int logn, bool goldilocks, const MontParams& mp, u64* data, size_t batch,
+                      size_t stride, const u64* tw, hipStream_t s) {
   if (goldilocks) {
-    if (variant >= 2) {  // persistent software-pipelined path (ntt64_gl.hip)
-      const hipError_t e = launch_ntt_gl(fwd, logn, variant, data, batch, stride, tw, s);
-      if (e != hipErrorInvalidValue) return e;
-    }
     Goldilocks g;
-    return fwd ? dispatch<true>(logn, variant, data, batch, stride, tw, g, s)
-               : dispatch<false>(logn, variant, data, batch, stride, tw, g, s);
+    return fwd ? dispatch<true>(logn, data, batch, stride, tw, g, s) : dispatch<false>(logn, data, batch, stride, tw, g, s);
   }
   Montgomery m{mp.p, mp.pinv, mp.r2};
-  return fwd ? dispatch<true>(logn, variant, data, batch, stride, tw, m, s)
-             : dispatch<false>(logn, variant, data, batch, stride, tw, m, s);
+  return fwd ? dispatch<true>(logn, data, batch, stride, tw, m, s) : dispatch<false>(logn, data, batch, stride, tw, m, s);
 }
 
 hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* data, size_t batch, size_t stride,
                           const uint64_t* tw, hipStream_t s) {
   Montgomery m{mp.p, mp.pinv, mp.r2};
-  return fwd ? dispatch<true>(logn, 0, data, batch, stride, tw, m, s)
-             : dispatch<false>(logn, 0, data, batch, stride, tw, m, s);
+  return fwd ? dispatch<true>(logn, data, batch, stride, tw, m, s) : dispatch<false>(logn, data, batch, stride, tw, m, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -11,9 +11,9 @@ struct MontParams {
   uint64_t p = 0, pinv = 0, r2 = 0;
 };
 
-// Transform kernels.  `variant` selects an alternative register-window width where one is
-// compiled (0 = default).  `tw` points at the plan's device table (forward or inverse).
-hipError_t launch_ntt(bool fwd, int logn, int variant, bool goldilocks, const MontParams& mp, uint64_t* data,
+// Register-window transform kernels (ntt64_kernels.hip).  `tw` points at the plan's device table
+// (forward or inverse).
+hipError_t launch_ntt(bool fwd, int logn, bool goldilocks, const MontParams& mp, uint64_t* data,
                       size_t batch, size_t stride, const uint64_t* tw, hipStream_t s);
 
 // prime32 plans (u32 buffers, generic Montgomery arithmetic)
@@ -22,13 +22,9 @@ hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* da
 hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, const uint32_t* a, const uint32_t* b,
                                 size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
 
-// Goldilocks persistent kernels (ntt64_gl.hip); hipErrorInvalidValue when the size is not covered.
-hipError_t launch_ntt_gl(bool fwd, int logn, int variant, uint64_t* data, size_t batch, size_t stride,
-                         const uint64_t* tw, hipStream_t s);
-
 // Twisted shift-twiddle transform (ntt64_tw.hip): Solinas prime, N = 2048 only.  `twist` = the
 // plan's rho_i^j table (forward) or rho_i^-j table (inverse), 2048 u64 each.
-hipError_t launch_ntt_tw(bool fwd, int variant, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
+hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
                          hipStream_t s);
 
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])

@@ -41,6 +41,7 @@ _SIGS = {
     "mi_last_error_message": (ctypes.c_char_p, []),
     "mi_ntt64_plan_create": (_int, [_sz, _u64, _int, ctypes.POINTER(_vp)]),
     "mi_ntt64_plan_destroy": (_int, [_vp]),
+    "mi_ntt64_plan_cached": (_int, [_sz, _u64, _int, ctypes.POINTER(_vp)]),
     "mi_ntt64_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_u64), ctypes.POINTER(_int)]),
     "mi_ntt64_plan_twiddles": (_int, [_vp, _p64, _p64, _p64]),
     "mi_ntt64_fwd_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
@@ -54,9 +55,26 @@ _SIGS = {
     "mi_bsk_to_ntt64": (_int, [_vp, _vp, _vp, _sz, ctypes.c_uint, _int, _vp]),
     "mi_ext_product_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _int, _vp]),
     "mi_cmux_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _int, _vp]),
-    "mi_pbs_ntt64_key_create": (_int, [_vp, _vp, _sz, _int, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "mi_pbs_ntt64_key_create": (_int, [_vp, _vp, _sz, _int, _int, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_key_destroy": (_int, [_vp]),
+    "mi_pbs_ntt64_key_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int),
+                                     ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "mi_ntt_bsk_parse": (_int, [_vp, _sz, _int, _vp]),
+    "mi_ntt_bsk_serialized_size": (_int, [_vp, _int, ctypes.POINTER(_sz)]),
+    "mi_ntt_bsk_write": (_int, [_vp, _vp, _int, _vp, _sz]),
+    "mi_pbs_ntt64_key_load": (_int, [_vp, _vp, _sz, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_multi_gpu_create": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
+    "mi_multi_gpu_destroy": (_int, [_vp]),
+    "mi_multi_gpu_count": (_int, [_vp, ctypes.POINTER(_int)]),
+    "mi_multi_gpu_info": (_int, [_vp, _int, ctypes.POINTER(_int), ctypes.POINTER(_vp)]),
+    "mi_multi_gpu_synchronize": (_int, [_vp]),
+    "mi_multi_gpu_active_count": (_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
+    "mi_multi_gpu_shard": (_int, [_sz, _int, _int, ctypes.POINTER(_sz), ctypes.POINTER(_sz)]),
+    "mi_multi_gpu_broadcast": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_multi_gpu_scatter": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_multi_gpu_gather": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_pbs_ntt64_multi_gpu": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp]),
     "mi_ntt32_plan_create": (_int, [_sz, ctypes.c_uint32, _int, ctypes.POINTER(_vp)]),
     "mi_ntt32_plan_destroy": (_int, [_vp]),
     "mi_ntt32_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(_int)]),
@@ -69,12 +87,20 @@ _SIGS = {
     "mi_native_plan_destroy": (_int, [_vp]),
     "mi_native_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "mi_native_polymul_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
-    "mi_lwe_ksk_create": (_int, [_vp, _sz, _sz, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "mi_lwe_ksk_create": (_int, [_vp, _sz, _sz, _int, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_lwe_ksk_destroy": (_int, [_vp]),
     "mi_lwe_ksk_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_int),
                                ctypes.POINTER(_int)]),
     "mi_lwe_keyswitch_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
 }
+
+
+
+class NttBskHeader(ctypes.Structure):
+    """``mi_ntt_bsk_header`` (include/tfhe_ntt_amd.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("polynomial_size", "glwe_size", "level", "base_log", "modulus_lo",
+                                               "modulus_hi", "input_lwe_dimension", "count", "data_offset")]
+
 
 _lib = None
 

@@ -34,7 +34,7 @@ class LweKeyswitchKey:
         h = ctypes.c_void_p()
         check(lib().mi_lwe_ksk_create(_dev(ksk, "ksk"), self.input_key_lwe_dimension,
                                       self.output_key_lwe_dimension, base_log, level,
-                                      ksk.device.index or 0, ctypes.byref(h)))
+                                      ksk.device.index or 0, _stream(ksk), ctypes.byref(h)))
         self._h = h
 
     def __del__(self):

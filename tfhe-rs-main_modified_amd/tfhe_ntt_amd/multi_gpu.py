@@ -14,6 +14,10 @@ shard.  Collectives appear only at the edges, mirroring the CUDA backend's multi
                        (grouped point-to-point: xGMI is point-to-point, so the root talks to each
                        peer over its own link instead of a ring);
 * ``max_over_ranks`` — the benchmark's whole-job time.
+
+``DeviceSet`` is the single-process form of the same split over the C ABI (``mi_multi_gpu_*``): one host
+process driving several devices, as tfhe-rs's ``CudaStreams`` do — peer-to-peer scatter / gather /
+broadcast from the first device and a whole multi-GPU PBS (``mi_pbs_ntt64_multi_gpu``).
 """
 from __future__ import annotations
 
@@ -97,4 +101,115 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-__all__ = ["shard_bounds", "broadcast_", "scatter_batch", "gather_batch", "max_over_ranks"]
+class DeviceSet:
+    """A set of HIP devices with one stream each (``mi_multi_gpu``); entry 0 holds whole batches.  A device
+    may repeat (``DeviceSet([0, 0])`` rehearses the split on one GPU)."""
+
+    def __init__(self, devices):
+        import ctypes
+
+        from ._lib import check, lib
+        self.devices = [int(d) for d in devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        check(lib().mi_multi_gpu_create(ctypes.cast(arr, ctypes.c_void_p), len(self.devices), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                from ._lib import lib
+                lib().mi_multi_gpu_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def __len__(self):
+        return len(self.devices)
+
+    def shard(self, total: int, index: int):
+        """[offset, offset + n) of entry ``index`` (``mi_multi_gpu_shard``)."""
+        return lib_shard(total, index, len(self.devices))
+
+    @staticmethod
+    def _ptrs(ts):
+        import ctypes
+        return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+    @staticmethod
+    def _stream(t):
+        import ctypes
+
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def synchronize(self):
+        from ._lib import check, lib
+        check(lib().mi_multi_gpu_synchronize(self._h))
+
+    def broadcast(self, src, dsts):
+        import ctypes
+
+        from ._lib import check, lib
+        check(lib().mi_multi_gpu_broadcast(self._h, ctypes.c_void_p(src.data_ptr()), self._ptrs(dsts),
+                                           src.numel() * src.element_size(), self._stream(src)))
+
+    def scatter(self, src, dsts):
+        """``dsts[i]`` (on ``devices[i]``) <- shard i of ``src`` (leading dim = units, on ``devices[0]``)."""
+        import ctypes
+
+        from ._lib import check, lib
+        unit = src[0].numel() * src.element_size() if src.shape[0] else 0
+        check(lib().mi_multi_gpu_scatter(self._h, ctypes.c_void_p(src.data_ptr()), self._ptrs(dsts), src.shape[0],
+                                         unit, self._stream(src)))
+
+    def gather(self, dst, srcs):
+        import ctypes
+
+        from ._lib import check, lib
+        unit = dst[0].numel() * dst.element_size() if dst.shape[0] else 0
+        check(lib().mi_multi_gpu_gather(self._h, ctypes.c_void_p(dst.data_ptr()), self._ptrs(srcs), dst.shape[0],
+                                        unit, self._stream(dst)))
+
+    def programmable_bootstrap(self, keys, lwe_in, lwe_out, luts, ms_mode: int = 0):
+        """Batched PBS over the set (``mi_pbs_ntt64_multi_gpu``): ``keys[i]`` / ``luts[i]`` on ``devices[i]``,
+        ``lwe_in`` / ``lwe_out`` on ``devices[0]``; results land in ``lwe_out`` as one launch would."""
+        import ctypes
+
+        from ._lib import check, lib
+        if len(keys) != len(self.devices) or len(luts) != len(self.devices):
+            raise ValueError("one key and one LUT per device of the set")
+        k0 = keys[0]
+        n_in, n_out = k0.input_lwe_dimension + 1, k0.output_lwe_size()
+        batch = lwe_in.numel() // n_in
+        if lwe_in.shape[-1] != n_in or lwe_out.shape[-1] != n_out or lwe_out.numel() // n_out != batch:
+            raise ValueError("assertion failed: lwe shapes do not match the key")
+        kp = (ctypes.c_void_p * len(keys))(*[k._h.value for k in keys])
+        check(lib().mi_pbs_ntt64_multi_gpu(self._h, kp, ctypes.c_void_p(lwe_out.data_ptr()),
+                                           ctypes.c_void_p(lwe_in.data_ptr()), self._ptrs(luts), batch, ms_mode,
+                                           self._stream(lwe_out)))
+
+
+def lib_shard(total: int, index: int, count: int):
+    """``mi_multi_gpu_shard`` (get_gpu_offset / get_num_inputs_on_gpu, helper_multi_gpu.cu:51-98)."""
+    import ctypes
+
+    from ._lib import check, lib
+    off, n = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().mi_multi_gpu_shard(total, index, count, ctypes.byref(off), ctypes.byref(n)))
+    return off.value, off.value + n.value
+
+
+def lib_active_count(num_inputs: int, gpu_count: int) -> int:
+    """``mi_multi_gpu_active_count`` (get_active_gpu_count, helper_multi_gpu.cu:42-49)."""
+    import ctypes
+
+    from ._lib import check, lib
+    out = ctypes.c_uint32()
+    check(lib().mi_multi_gpu_active_count(num_inputs, gpu_count, ctypes.byref(out)))
+    return out.value
+
+
+__all__ = ["shard_bounds", "broadcast_", "scatter_batch", "gather_batch", "max_over_ranks", "DeviceSet",
+           "lib_shard", "lib_active_count"]

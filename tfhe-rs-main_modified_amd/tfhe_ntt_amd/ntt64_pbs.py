@@ -109,20 +109,24 @@ class NttBootstrapKey:
 
     ``bsk`` is the device tensor (n_lwe, level, k+1, k+1, N) produced by
     ``convert_standard_lwe_bootstrap_key_to_ntt64``: Raw for ``BNF`` (a private copy with N^-1
-    folded in is made once), Normalize for ``SOLINAS`` (referenced; keep the tensor alive)."""
+    folded in is made once, on the tensor's current stream), Normalize for ``SOLINAS`` (referenced;
+    keep the tensor alive)."""
 
     def __init__(self, plan, bsk, base_log: int, level: int, variant: int = BNF):
         n = plan.ntt_size()
         k = 1
         if bsk.dim() != 5 or tuple(bsk.shape[1:]) != (level, k + 1, k + 1, n):
             raise ValueError(f"assertion failed: bsk shape {tuple(bsk.shape)} != (n_lwe, {level}, 2, 2, {n})")
-        self.plan, self.bsk, self.base_log, self.level, self.variant = plan, bsk, base_log, level, variant
-        self.input_lwe_dimension = bsk.shape[0]
-        self.glwe_dimension, self.polynomial_size = k, n
+        self._bind(plan, bsk, int(bsk.shape[0]), k, base_log, level, variant)
         h = ctypes.c_void_p()
         check(lib().mi_pbs_ntt64_key_create(plan.handle, _dev(bsk, "bsk"), self.input_lwe_dimension, k, base_log,
-                                            level, variant, ctypes.byref(h)))
+                                            level, variant, _stream(bsk), ctypes.byref(h)))
         self._h = h
+
+    def _bind(self, plan, bsk, n_lwe, k, base_log, level, variant):
+        self.plan, self.bsk, self.base_log, self.level, self.variant = plan, bsk, base_log, level, variant
+        self.input_lwe_dimension = n_lwe
+        self.glwe_dimension, self.polynomial_size = k, plan.ntt_size()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -136,28 +140,48 @@ class NttBootstrapKey:
     def output_lwe_size(self) -> int:
         return self.glwe_dimension * self.polynomial_size + 1
 
-    def serialize(self) -> bytes:
-        """``bincode::serialize`` bytes of the reference's NttLweBootstrapKey (``ntt_bsk_format``); the
-        ciphertext modulus field is native (0) for ``BNF`` and the Solinas prime for ``SOLINAS``."""
+    def serialize(self, versioned: bool = False) -> bytes:
+        """Bytes of the reference's NttLweBootstrapKey (``ntt_bsk_format``: ``bincode::serialize`` or, with
+        ``versioned``, bincode of ``versionize()``).  The ciphertext modulus is the plan's NTT prime for
+        both variants, as the reference stores it (ntt64_bnf_pbs.rs:44-94).  Needs the source tensor
+        (keys made by ``load`` own only their device copy)."""
         from .ntt_bsk_format import serialize_ntt_bsk
-        mod = 0 if self.variant == BNF else self.plan.modulus()
+        if self.bsk is None:
+            raise ValueError("key was loaded from bytes; serialise the original bytes instead")
         return serialize_ntt_bsk(self.bsk.detach().cpu().numpy(), self.polynomial_size, self.glwe_dimension + 1,
-                                 self.level, self.base_log, mod)
+                                 self.level, self.base_log, self.plan.modulus(), versioned)
 
     @classmethod
-    def deserialize(cls, plan, buf: bytes, device=None):
-        """Loads serialised key bytes into HBM (one copy) and binds them to ``plan``; the variant follows
-        the stored ciphertext modulus (native -> BNF, the plan's prime -> SOLINAS)."""
+    def load(cls, plan, buf: bytes, variant: int, versioned: bool = False, stream=None):
+        """Serialised key bytes straight into HBM through the C ABI loader (``mi_pbs_ntt64_key_load``: one
+        host-to-device copy, no re-layout).  ``variant`` is explicit because Raw (BNF) and Normalize
+        (Solinas) keys store the same fields; the stored modulus must be the plan's prime."""
+        import torch
+        buf = bytes(buf)
+        h = ctypes.c_void_p()
+        s = stream if stream is not None else torch.cuda.current_stream(torch.device("cuda", plan.device))
+        check(lib().mi_pbs_ntt64_key_load(plan.handle, buf, len(buf), int(bool(versioned)), variant,
+                                          ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
+        n_lwe, k, bl, lv, var = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().mi_pbs_ntt64_key_info(h, ctypes.byref(n_lwe), ctypes.byref(k), ctypes.byref(bl), ctypes.byref(lv),
+                                          ctypes.byref(var)))
+        key = cls.__new__(cls)
+        key._bind(plan, None, n_lwe.value, k.value, bl.value, lv.value, var.value)
+        key._h = h
+        return key
+
+    @classmethod
+    def deserialize(cls, plan, buf: bytes, variant: int, versioned: bool = False, device=None):
+        """Parses the bytes on the host (``ntt_bsk_format``), uploads the key tensor and binds it to ``plan``
+        (the key keeps the tensor, so it can be re-serialised).  ``variant`` as in ``load``."""
         import numpy as np
         import torch
         from .ntt_bsk_format import NttBskFormatError, deserialize_ntt_bsk
-        data, f = deserialize_ntt_bsk(buf)
+        data, f = deserialize_ntt_bsk(buf, versioned)
         if f["polynomial_size"] != plan.ntt_size():
             raise NttBskFormatError(f"key polynomial size {f['polynomial_size']} != plan size {plan.ntt_size()}")
-        if f["ciphertext_modulus"] not in (0, plan.modulus()):
-            raise NttBskFormatError(f"key ciphertext modulus {f['ciphertext_modulus']} is neither native nor the "
-                                    "plan's prime")
-        variant = BNF if f["ciphertext_modulus"] == 0 else SOLINAS
+        if f["ciphertext_modulus"] != plan.modulus():
+            raise NttBskFormatError(f"key ciphertext modulus {f['ciphertext_modulus']} is not the plan's NTT prime")
         dev = device if device is not None else torch.device("cuda", plan.device)
         bsk = torch.from_numpy(data.view(np.int64)).to(dev)
         return cls(plan, bsk, f["decomposition_base_log"], f["decomposition_level_count"], variant)

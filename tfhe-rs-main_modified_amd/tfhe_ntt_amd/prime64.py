@@ -35,10 +35,10 @@ def _is_torch(x) -> bool:
 class Plan:
     """Negacyclic NTT plan for a 64-bit prime, living on one HIP device."""
 
-    __slots__ = ("_h", "_n", "_p", "_device")
+    __slots__ = ("_h", "_n", "_p", "_device", "_cached")
 
-    def __init__(self, handle, n: int, p: int, device: int):
-        self._h, self._n, self._p, self._device = handle, n, p, device
+    def __init__(self, handle, n: int, p: int, device: int, cached: bool = False):
+        self._h, self._n, self._p, self._device, self._cached = handle, n, p, device, cached
 
     # -- construction ------------------------------------------------------------------
     @classmethod
@@ -50,9 +50,17 @@ class Plan:
         check(st)
         return cls(h, polynomial_size, modulus, device)
 
+    @classmethod
+    def cached(cls, polynomial_size: int, modulus: int, device: int = 0) -> "Plan":
+        """The shared plan of ``Ntt64::new`` (ntt64.rs:27-79): one plan per (N, p, device) for the whole
+        process, built on first use; raises where the reference panics (no plan for (N, p))."""
+        h = ctypes.c_void_p()
+        check(lib().mi_ntt64_plan_cached(polynomial_size, modulus, device, ctypes.byref(h)))
+        return cls(h, polynomial_size, modulus, device, cached=True)
+
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and not getattr(self, "_cached", False):
             try:
                 lib().mi_ntt64_plan_destroy(h)
             except Exception:

@@ -772,62 +772,6 @@ def gen_inv(tabs, stop=None):
     return B
 
 
-# ------------------------------------------------------------------------------------------------
-# Persistent, software-pipelined variant (ntt64_tw.hip ntt_tw_pipe_kernel): each wave walks the
-# polynomials poly0, poly0 + step, ... < batch; the next polynomial's 32 rows are loaded into
-# v128..v191 while the current one is transformed, so HBM latency is exposed once per wave instead
-# of once per polynomial.  The twist / pair-stage tables live in LDS (copied once per workgroup), so
-# the body issues no global load besides the prefetch and vmcnt only ever counts prefetch + stores.
-VPF = 128                                   # prefetch rows v128..v191
-S_NXT, S_BAT, S_STP, S_SB, S_GD = 94, 95, 96, 97, 98   # s98:99 data base
-PIPE_SGPR_CLOBBER = SGPR_CLOBBER + list(range(94, 100))
-
-LDS_ADDR = Addr(lambda bt, k, dst: f"ds_read_b64 {pv(dst)}, %[twl] offset:{512 * (8 * bt + k)}",
-                **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r")})
-LDS_ADDR.tw_wait = "s_waitcnt lgkmcnt(0)"
-LDS_ADDR.tw_wait_n = lambda n: f"s_waitcnt lgkmcnt({n})"
-# pair-stage table: 32 entries after the 2048 twist rows; lane parity selects entries 16..31
-LDS_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, %[lwl] offset:{8 * k}"
-
-
-def poly_bases(dst):
-    """s[dst .. dst+7] = data base + s_NXT * stride_bytes + 4096 m (m = 0..3)."""
-    return [f"s_mul_i32 s{dst}, s{S_NXT}, s{S_SB}", f"s_mul_hi_u32 s{dst + 1}, s{S_NXT}, s{S_SB}",
-            f"s_add_u32 s{dst}, s{dst}, s{S_GD}", f"s_addc_u32 s{dst + 1}, s{dst + 1}, s{S_GD + 1}"] + \
-        [l for m in range(1, 4) for l in (f"s_add_u32 s{dst + 2 * m}, s{dst}, {4096 * m}",
-                                          f"s_addc_u32 s{dst + 2 * m + 1}, s{dst + 1}, 0")]
-
-
-def gen_pipe(tabs, fwd):
-    B = Body(tabs)
-    dmap = [64 + 2 * r for r in range(32)]
-    pf = [VPF + 2 * r for r in range(32)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
-    B.raw(f"s_mov_b32 s{S_NXT}, %[p0]", f"s_mov_b32 s{S_BAT}, %[batch]", f"s_mov_b32 s{S_STP}, %[step]",
-          f"s_mov_b32 s{S_SB}, %[sb]", f"s_mov_b32 s{S_GD}, %[g_lo]", f"s_mov_b32 s{S_GD + 1}, %[g_hi]")
-    B.raw(*poly_bases(S_GB), *load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    B.raw(".Ltw_top_%=:",
-          f"s_add_u32 s{S_NXT}, s{S_NXT}, s{S_STP}", f"s_cmp_lt_u32 s{S_NXT}, s{S_BAT}",
-          "s_cbranch_scc0 .Ltw_nopf_%=",
-          *poly_bases(S_TB), *load_rows(pf, S_TB), ".Ltw_nopf_%=:")
-    out = fwd_core(B, tabs, dmap, LDS_ADDR) if fwd else inv_core(B, tabs, dmap, LDS_ADDR)
-    B.raw(*store_rows(out, S_GB), f"s_cmp_lt_u32 s{S_NXT}, s{S_BAT}", "s_cbranch_scc0 .Ltw_end_%=",
-          "s_waitcnt vmcnt(32)")
-    B.raw(*[f"v_mov_b64 {pv(d)}, {pv(p)}" for d, p in zip(dmap, pf)])
-    B.raw(*[f"s_mov_b64 s[{S_GB + 2 * m}:{S_GB + 2 * m + 1}], s[{S_TB + 2 * m}:{S_TB + 2 * m + 1}]" for m in range(4)],
-          "s_branch .Ltw_top_%=", ".Ltw_end_%=:", "s_waitcnt vmcnt(0)")
-    return B
-
-
-def emit_pipe(name, body):
-    clob = [f'"v{i}"' for i in range(VLO, VPF + 64)] + [f'"s{i}"' for i in PIPE_SGPR_CLOBBER] + ['"scc"', '"memory"']
-    return (f"// {name}: {body.nvalu} VALU per polynomial (incl. 32 v_mov_b64), {len(body.lines)} lines\n"
-            f"#define MI_TW_PIPE_{name.upper()}(...) asm volatile(\\\n" +
-            "\\\n".join(f'      "{l}\\n"' for l in body.lines) +
-            f"\\\n      :: __VA_ARGS__ \\\n      : {', '.join(clob)})\n")
-
-
 def emit(name, body, ops_in):
     clob = [f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
     text = "\n".join(f'      "{l}\\n"' for l in body.lines)
@@ -839,19 +783,12 @@ def emit(name, body, ops_in):
 
 def main():
     tabs = load_tables()
-    if len(sys.argv) > 1 and sys.argv[1] == "debug":
-        print("#pragma once")
-        for st in ("g1", "twist", "t1", "cyc", "last"):
-            print(emit("fwd_" + st, gen_fwd(tabs, st), None))
-        return
     f, i = gen_fwd(tabs), gen_inv(tabs)
     print("// GENERATED by tools/gen_tw_kernel.py — do not edit.  Whole-data-path asm bodies of the twisted")
     print("// N = 2048 Goldilocks transform (ntt64_tw.hip).  Owns v8..v127, s20..s31 + s36..s93, exec (restored).")
     print("#pragma once")
     print(emit("fwd", f, None))
     print(emit("inv", i, None))
-    print(emit_pipe("fwd", gen_pipe(tabs, True)))
-    print(emit_pipe("inv", gen_pipe(tabs, False)))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 

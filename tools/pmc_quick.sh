@@ -1,9 +1,9 @@
 #!/bin/bash
-# Quick PMC passes for the NTT kernels of one variant: bash tools/pmc_quick.sh <variant> <tag>
+# Quick PMC passes for the NTT kernels: bash tools/pmc_quick.sh <tag>
 set -o pipefail
-v=${1:-0}; tag=${2:-q}
+tag=${1:-q}
 out=gpurun_out/pmc_$tag; mkdir -p $out
-export MI_NTT_VARIANT=$v PYTHONUNBUFFERED=1
+export PYTHONUNBUFFERED=1
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAIT_ANY" \
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
