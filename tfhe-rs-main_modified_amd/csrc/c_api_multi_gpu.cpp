@@ -227,7 +227,7 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys,
       return fail(MI_ERR_INVALID_ARG, "keys differ in shape");
   }
   const size_t in_w = keys[0]->n_lwe + 1, out_w = (size_t)keys[0]->k * keys[0]->plan->n + 1;
-  std::vector<uint64_t*> ins(G, nullptr), outs(G, nullptr);
+  std::vector<uint64_t*> ins(G, nullptr), outs(G, nullptr), scratch(G, nullptr);
   int st = MI_OK;
   for (size_t i = 0; i < G && st == MI_OK; ++i) {
     size_t off = 0, n = 0;
@@ -241,7 +241,7 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys,
     uint64_t* buf = nullptr;
     if (hipMallocAsync((void**)&buf, n * (in_w + out_w) * sizeof(uint64_t), m->streams[i]) != hipSuccess)
       st = fail(MI_ERR_OOM, "shard scratch allocation failed");
-    ins[i] = buf;
+    scratch[i] = ins[i] = buf;
     outs[i] = buf ? buf + n * in_w : nullptr;
   }
   if (st == MI_OK) st = mi_multi_gpu_scatter(m, lwe_in, (void* const*)ins.data(), batch, in_w * 8, stream);
@@ -254,9 +254,9 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys,
   }
   if (st == MI_OK) st = mi_multi_gpu_gather(m, lwe_out, (const void* const*)outs.data(), batch, out_w * 8, stream);
   for (size_t i = 1; i < G; ++i)
-    if (ins[i]) {
+    if (scratch[i]) {
       DeviceGuard g(m->devices[i]);
-      (void)hipFreeAsync(ins[i], m->streams[i]);
+      (void)hipFreeAsync(scratch[i], m->streams[i]);
     }
   return st;
 }
