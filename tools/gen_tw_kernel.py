@@ -306,42 +306,31 @@ def gs_core(sg, sl, a, b):
 
 
 def gs(sg, sl, a, b, S, ac=False, bc=False):
-    """GS butterfly; ac / bc: whether a / b are known canonical (skips the canonicalisation).
-    Returns whether the new b is canonical."""
+    """GS butterfly (a, b) -> (a + b, (a - b) w), w = 2^S; ac / bc: whether a / b are known canonical.
+
+    The subtraction needs a canonical subtrahend and the sign of w decides which operand that is:
+    (a - b) w = (b - a) |w| when w < 0, so the subtrahend is b for w > 0 and a for w < 0.  That operand is
+    canonicalised in place when it is not known canonical (a + b only needs one canonical operand, the
+    same one), so the new b is always the canonical, positive tmul magnitude: no negation is ever
+    emitted.  Returns True (new b canonical)."""
     alo, ahi, ap = a
     blo, bhi, bp = b
     v, P, c = sl.v, sl.P, sl.c
     e = S % 96
     neg = (S >= 96) != (e >= 64)
-    if bc or not ac:
-        if not bc:  # canonicalise b into v2:v3, then a' = a + cb, b <- a - cb
-            sg.add(f"v_mad_u64_u32 {P[3]}, {c[1]}, -1, 1, {bp}", [bp], [P[3], c[1]])
-            sg.add(f"v_cndmask_b32_e64 {v[2]}, {blo}, {v[6]}, {c[1]}", [blo, v[6], c[1]], [v[2]])
-            sg.add(f"v_cndmask_b32_e64 {v[3]}, {bhi}, {v[7]}, {c[1]}", [bhi, v[7], c[1]], [v[3]])
-            tlo, thi = v[2], v[3]
-        else:
-            tlo, thi = blo, bhi
-        if neg and ac:
-            # (a - b) w = (b - a) |w|: subtract the canonical a instead, no negation afterwards
-            add_part1(sg, sl, alo, ahi, tlo, thi)
-            sub_seq(sg, sl, blo, bhi, tlo, thi, alo, ahi) if bc else sub_seq(sg, sl, blo, bhi, v[2], v[3], alo, ahi)
-            add_part2(sg, sl, ap)
-            neg = False
-        else:
-            add_part1(sg, sl, alo, ahi, tlo, thi)
-            sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
-            add_part2(sg, sl, ap)
+    sub_a = neg  # subtrahend: a when w < 0 (d = b - a), b otherwise (d = a - b)
+    if sub_a and not ac:
+        canon(sg, sl, a)
+    if not sub_a and not bc:
+        canon(sg, sl, b)
+    if sub_a:
+        add_part1(sg, sl, blo, bhi, alo, ahi)          # s = b + a (a canonical)
+        sub_seq(sg, sl, blo, bhi, blo, bhi, alo, ahi)  # d = b - a
     else:
-        # only a canonical: a' = b + a, b <- b - a, sign flips
-        add_part1(sg, sl, blo, bhi, alo, ahi)
-        sub_seq(sg, sl, blo, bhi, blo, bhi, alo, ahi)
-        add_part2(sg, sl, ap)
-        neg = not neg
-    tmul(sg, S, blo, bhi, bp, sl, blo, bhi)
-    if neg:
-        sg.add(f"v_sub_co_u32_e64 {blo}, {sl.c[2]}, 1, {blo}", [blo], [blo, sl.c[2]])
-        sg.add(f"v_subb_co_u32_e64 {bhi}, {JUNK}, -1, {bhi}, {sl.c[2]}", [bhi, sl.c[2]], [bhi, JUNK])
-        return False
+        add_part1(sg, sl, alo, ahi, blo, bhi)          # s = a + b (b canonical)
+        sub_seq(sg, sl, blo, bhi, alo, ahi, blo, bhi)  # d = a - b
+    add_part2(sg, sl, ap)
+    tmul(sg, S, blo, bhi, bp, sl, blo, bhi)  # |w| d, canonical; the sign is absorbed by the orientation
     return True
 
 
@@ -622,10 +611,86 @@ def slot_view(m, c23):
     return sl
 
 
-def pair_stage(B, dmap, fwd, ad=NTT_ADDR):
-    """Cyclic stage q = 5 on lane pairs: regroup W1 -> W1' (DPP), butterfly with the per-lane twiddle
-    w_g, g = k + 16 (lane & 1), from the 32-entry table; forward: CT then canonical outputs (layout
-    stays W1' for T2); inverse: GS then regroup back to W1."""
+def shift_class(e):
+    """tmul code path of an exponent e = S % 96: 0 (e <= 32), 1 (32 < e < 64), 2 (64 <= e < 96)."""
+    return 0 if e <= 32 else (1 if e < 64 else 2)
+
+
+def lane_tmul_applies(Se, So):
+    """Whether tmul_lane covers the lane pair (even lanes x 2^Se, odd lanes x 2^So): one code path and
+    one sign for both lanes, and a per-lane shift amount that is never out of range (r >= 1 in class 1)."""
+    ee, eo = Se % 96, So % 96
+    neg = lambda S, e: (S >= 96) != (e >= 64)
+    if shift_class(ee) != shift_class(eo) or neg(Se, ee) != neg(So, eo):
+        return False
+    if shift_class(ee) == 0:
+        return max(ee, eo) < 32  # v_bfe width r must stay below 32
+    return shift_class(ee) != 1 or min(ee, eo) > 32
+
+
+def tmul_lane(sg, S_even, S_odd, x, sl, tlo, thi, par3, amt):
+    """tmul with a lane-dependent exponent (even lanes S_even, odd lanes S_odd = S_even +- 3): the
+    compile-time code path of the common class with VGPR shift amounts built from par3 = 3 (lane & 1).
+    Same VALU count as tmul plus two full-rate adds; returns the common sign flag."""
+    xlo, xhi, xp = x
+    v, P, c = sl.v, sl.P, sl.c
+    e0, e1 = S_even % 96, S_odd % 96
+    assert lane_tmul_applies(S_even, S_odd) and abs(e1 - e0) == 3, (S_even, S_odd)
+    neg = (S_even >= 96) != (e0 >= 64)
+    A0, A1 = amt
+    op_up = "v_add_u32" if e1 > e0 else "v_sub_u32"      # amount grows with the exponent
+    op_dn = "v_sub_u32" if e1 > e0 else "v_add_u32"
+    cls = shift_class(e0)
+    if cls == 0:
+        # r = e, h = top r bits of x_hi (v_bfe: width 0 gives 0, so r = 0 needs no special case)
+        sg.add(f"{op_up} {A0}, {e0}, {par3}", [par3], [A0])
+        sg.add(f"{op_dn} {A1}, {32 - e0}, {par3}", [par3], [A1])
+        sg.add(f"v_lshlrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
+        sg.add(f"v_bfe_u32 {v[4]}, {xhi}, {A1}, {A0}", [xhi, A1, A0], [v[4]])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[4]}, -1, {P[0]}", [v[4], P[0]], [P[1], c[0]])
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {P[1]}", [P[1]], [P[0], c[1]])
+        sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
+        sg.add(f"v_cndmask_b32_e64 {tlo}, {v[2]}, {v[0]}, {c[1]}", [v[2], v[0], c[1]], [tlo])
+        sg.add(f"v_cndmask_b32_e64 {thi}, {v[3]}, {v[1]}, {c[1]}", [v[3], v[1], c[1]], [thi])
+    elif cls == 1:
+        # r = e - 32 >= 1: y = x 2^r folded once, then y 2^32 = y_lo 2^32 + y_hi eps
+        sg.add(f"{op_up} {A0}, {e0 - 32}, {par3}", [par3], [A0])
+        sg.add(f"{op_dn} {A1}, {64 - e0}, {par3}", [par3], [A1])
+        sg.add(f"v_lshlrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
+        sg.add(f"v_lshrrev_b32 {v[4]}, {A1}, {xhi}", [A1, xhi], [v[4]])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[4]}, -1, {P[0]}", [v[4], P[0]], [P[1], c[0]])
+        sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[0]}", [c[0]], [v[4]])
+        sg.add(f"v_mad_u64_u32 {P[0]}, {JUNK}, {v[4]}, 1, {P[1]}", [v[4], P[1]], [P[0], JUNK])
+        sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
+        sg.add(f"v_mov_b32 {v[7]}, {v[0]}", [v[0]], [v[7]])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[1]}, -1, {P[3]}", [v[1], P[3]], [P[1], c[0]])
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {P[1]}", [P[1]], [P[0], c[1]])
+        sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
+        sg.add(f"v_cndmask_b32_e64 {tlo}, {v[2]}, {v[0]}, {c[1]}", [v[2], v[0], c[1]], [tlo])
+        sg.add(f"v_cndmask_b32_e64 {thi}, {v[3]}, {v[1]}, {c[1]}", [v[3], v[1], c[1]], [thi])
+    else:
+        # K = 96 - e in [3, 32]: x 2^-K = (x >> K) + u - u 2^32, u = low K bits of x moved to the top of a word
+        sg.add(f"{op_dn} {A0}, {96 - e0}, {par3}", [par3], [A0])
+        sg.add(f"{op_up} {A1}, {e0 - 64}, {par3}", [par3], [A1])
+        sg.add(f"v_lshrrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
+        sg.add(f"v_lshlrev_b32 {v[4]}, {A1}, {xlo}", [A1, xlo], [v[4]])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {JUNK}, {v[4]}, 1, {P[0]}", [v[4], P[0]], [P[1], JUNK])
+        sg.add(f"v_sub_co_u32_e64 {v[3]}, {c[0]}, {v[3]}, {v[4]}", [v[3], v[4]], [v[3], c[0]])
+        sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -15, {c[0]}", [c[0]], [v[5]])
+        tp = pair_of(tlo, thi)
+        sg.add(f"v_mad_i64_i32 {tp}, {JUNK}, {v[5]}, s{S_X15}, {P[1]}", [v[5], P[1]], [tp, tlo, thi, JUNK])
+    return neg
+
+
+def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None):
+    """Cyclic stage q = 5 on lane pairs: regroup W1 -> W1' (DPP), then butterfly k of lane 2i + par uses
+    the twiddle w_g = 2^E[g], g = k + 16 par (E = the exponent row of the stage).  Where both lanes'
+    exponents share one code path the multiply is a shift-twiddle tmul with per-lane shift amounts
+    (tmul_lane); elsewhere a general multiply by the table value (entry g of the 32-entry table).
+    Forward: CT then canonical outputs (layout stays W1' for T2); inverse: GS then regroup back to W1."""
+    if tabs is None:
+        tabs = load_tables()
+    E = tabs["CYC_FWD" if fwd else "CYC_INV"][5]
     regs = []
     for b in free_blocks_except(dmap):
         regs += list(range(b, b + 8))
@@ -634,33 +699,52 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR):
     tmps = [regs[16:20], regs[20:24]]
     msl = [MulSlot(regs[24], SG0), MulSlot(regs[36], SG0 + 6)]
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
+    par3 = f"v{regs[48]}" if len(regs) > 48 else None
+    assert par3, "need a register for the lane-parity shift offset"
+    B.raw(f"v_cndmask_b32_e64 {par3}, 0, 3, s[{S_PAR}:{S_PAR + 1}]")
     for half in range(2):
         ks = list(range(8 * half, 8 * half + 8))
-        B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in enumerate(ks)], ad.lw_wait or ad.tw_wait, "s_nop 1")
+        gm = [(i, k) for i, k in enumerate(ks) if not lane_tmul_applies(E[k], E[k + 16])]
+        if gm:
+            B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in gm], ad.lw_wait or ad.tw_wait, "s_nop 1")
         sg = Seg()
         for i, k in enumerate(ks):
             tmp = [f"v{r}" for r in tmps[i % 2]]
             m = msl[i % 2]
             sl = slot_view(m, c23[i % 2])
+            lane = lane_tmul_applies(E[k], E[k + 16])
             wlo, whi = f"v{wb[2 * i]}", f"v{wb[2 * i] + 1}"
             regroup(sg, dmap, k, tmp, True)
             a, b = X(dmap, k), X(dmap, k + 16)
             if fwd:
-                # t = b * w into the slot's Z1 pair, then CT with t viewed as v2:v3
-                gmul(sg, m, b, wlo, whi, m.v[8], m.v[9])
-                ct_sl = Slot.__new__(Slot)
-                ct_sl.v = [m.v[0], m.v[1], m.v[8], m.v[9], m.v[4], m.v[5], m.v[6], m.v[7]]
-                ct_sl.P = [m.P[0], None, None, m.P[3]]
-                ct_sl.c = sl.c
-                ct_core(sg, ct_sl, a, b, False)
-                canon(sg, ct_sl, a)
-                canon(sg, ct_sl, b)
+                if lane:
+                    neg = tmul_lane(sg, E[k], E[k + 16], b, sl, sl.v[2], sl.v[3], par3, (wlo, whi))
+                    ct_core(sg, sl, a, b, neg)
+                else:
+                    # t = b * w into the slot's Z1 pair, then CT with t viewed as v2:v3
+                    gmul(sg, m, b, wlo, whi, m.v[8], m.v[9])
+                    ct_sl = Slot.__new__(Slot)
+                    ct_sl.v = [m.v[0], m.v[1], m.v[8], m.v[9], m.v[4], m.v[5], m.v[6], m.v[7]]
+                    ct_sl.P = [m.P[0], None, None, m.P[3]]
+                    ct_sl.c = sl.c
+                    ct_core(sg, ct_sl, a, b, False)
+                canon(sg, sl, a)
+                canon(sg, sl, b)
             else:
-                # inputs are canonical (loaded data): a' = a + b, b <- a - b, no canonicalisation
+                # inputs are canonical (loaded data), so either may be the subtrahend: a' = a + b and
+                # d = a - b, or d = b - a when the shift twiddle is negative (the product stays positive)
+                e0 = E[k] % 96
+                swap = lane and ((E[k] >= 96) != (e0 >= 64))
                 add_part1(sg, sl, a[0], a[1], b[0], b[1])
-                sub_seq(sg, sl, b[0], b[1], a[0], a[1], b[0], b[1])
+                if swap:
+                    sub_seq(sg, sl, b[0], b[1], b[0], b[1], a[0], a[1])
+                else:
+                    sub_seq(sg, sl, b[0], b[1], a[0], a[1], b[0], b[1])
                 add_part2(sg, sl, a[2])
-                gmul(sg, m, b, wlo, whi, b[0], b[1])
+                if lane:
+                    tmul_lane(sg, E[k], E[k + 16], b, sl, b[0], b[1], par3, (wlo, whi))
+                else:
+                    gmul(sg, m, b, wlo, whi, b[0], b[1])
                 regroup(sg, dmap, k, tmp, False)
         for j, op in enumerate(sg.ops):
             op.idx = j
@@ -752,8 +836,8 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR):
         B.stage("gs", 16 >> s, tabs["G1_INV"][s], dmap, fb, cf)
     sg = Seg()
     sls = B.slots(fb)
-    for r in range(32):
-        canon(sg, sls[r % len(sls)], X(dmap, r))
+    for k, r in enumerate([r for r in range(32) if not cf[r]]):
+        canon(sg, sls[k % len(sls)], X(dmap, r))
     for j, op in enumerate(sg.ops):
         op.idx = j
     B.out(sg.schedule())
