@@ -179,11 +179,14 @@ class Slot:
 
 
 class MulSlot:
-    """12 scratch VGPRs for a general multiply + 2 SGPR carry pairs."""
+    """12 scratch VGPRs (6 aligned pairs: vbase.. contiguous, or an explicit register list) for a general
+    multiply + 2 SGPR carry pairs."""
 
-    def __init__(self, vbase, sbase):
-        self.v = [f"v{vbase + i}" for i in range(12)]
-        self.P = [pv(vbase + 2 * i) for i in range(6)]
+    def __init__(self, vbase, sbase, regs=None):
+        regs = regs if regs is not None else list(range(vbase, vbase + 12))
+        assert len(regs) == 12 and all(regs[2 * i] % 2 == 0 and regs[2 * i + 1] == regs[2 * i] + 1 for i in range(6))
+        self.v = [f"v{r}" for r in regs]
+        self.P = [pv(regs[2 * i]) for i in range(6)]
         self.c = [f"s[{sbase + 2 * i}:{sbase + 2 * i + 1}]" for i in range(2)]
 
 
@@ -682,7 +685,13 @@ def tmul_lane(sg, S_even, S_odd, x, sl, tlo, thi, par3, amt):
     return neg
 
 
-def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None):
+def pair_stage_gmul_ks(tabs, fwd):
+    """Butterflies of the lane-pair stage that need a table twiddle (no common shift path)."""
+    E = tabs["CYC_FWD" if fwd else "CYC_INV"][5]
+    return [k for k in range(16) if not lane_tmul_applies(E[k], E[k + 16])]
+
+
+def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
     """Cyclic stage q = 5 on lane pairs: regroup W1 -> W1' (DPP), then butterfly k of lane 2i + par uses
     the twiddle w_g = 2^E[g], g = k + 16 par (E = the exponent row of the stage).  Where both lanes'
     exponents share one code path the multiply is a shift-twiddle tmul with per-lane shift amounts
@@ -692,19 +701,22 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None):
         tabs = load_tables()
     E = tabs["CYC_FWD" if fwd else "CYC_INV"][5]
     regs = []
-    for b in free_blocks_except(dmap):
+    for b in free_blocks_except(dmap, busy):
         regs += list(range(b, b + 8))
-    assert len(regs) >= 48, len(regs)
+    assert len(regs) >= (48 if busy else 49), len(regs)
     wb = regs[0:16]
     tmps = [regs[16:20], regs[20:24]]
     msl = [MulSlot(regs[24], SG0), MulSlot(regs[36], SG0 + 6)]
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
-    par3 = f"v{regs[48]}" if len(regs) > 48 else None
-    assert par3, "need a register for the lane-parity shift offset"
+    # the lane-parity shift offset: the top register of the reserved block (its twiddles use the bottom)
+    par3 = f"v{busy[-1]}" if busy else f"v{regs[48]}"
+    assert not pre or all(r + 1 < busy[-1] for r in pre.values())
     B.raw(f"v_cndmask_b32_e64 {par3}, 0, 3, s[{S_PAR}:{S_PAR + 1}]")
+    if pre:
+        B.raw(ad.lw_wait or ad.tw_wait)  # the preloaded twiddles (issued stages ago: normally no stall)
     for half in range(2):
         ks = list(range(8 * half, 8 * half + 8))
-        gm = [(i, k) for i, k in enumerate(ks) if not lane_tmul_applies(E[k], E[k + 16])]
+        gm = [(i, k) for i, k in enumerate(ks) if not lane_tmul_applies(E[k], E[k + 16]) and not (pre and k in pre)]
         if gm:
             B.raw(*[ad.lw_load(wb[2 * i], k) for i, k in gm], ad.lw_wait or ad.tw_wait, "s_nop 1")
         sg = Seg()
@@ -714,6 +726,8 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None):
             sl = slot_view(m, c23[i % 2])
             lane = lane_tmul_applies(E[k], E[k + 16])
             wlo, whi = f"v{wb[2 * i]}", f"v{wb[2 * i] + 1}"
+            if pre and k in pre:  # twiddle loaded earlier, latency hidden behind the previous stages
+                wlo, whi = f"v{pre[k]}", f"v{pre[k] + 1}"
             regroup(sg, dmap, k, tmp, True)
             a, b = X(dmap, k), X(dmap, k + 16)
             if fwd:
@@ -755,13 +769,14 @@ def store_raw(dmap):
     return store_rows(dmap, S_GB) + ["s_waitcnt vmcnt(0)"]
 
 
-def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None):
+def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None, first_loaded=False):
     """x[r] *= table row r (general multiplies) for the 32 registers, in 4 batches of 8 rows; the next
     batch's 8 table rows are loaded into the other buffer before this batch multiplies, so the table
     latency (L2 or LDS) hides behind the multiplies.  The slots' zero addend halves are set once."""
     B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
     buf = (lambda i, k: bufs[i] + 2 * k) if contiguous else (lambda i, k: regs[16 * i + 2 * k])
-    B.raw(*[ad.tw_load(0, k, buf(0, k)) for k in range(8)])
+    if not first_loaded:
+        B.raw(*[ad.tw_load(0, k, buf(0, k)) for k in range(8)])
     for bt in range(4):
         if bt + 1 < 4:
             B.raw(*[ad.tw_load(bt + 1, k, buf((bt + 1) % 2, k)) for k in range(8)], ad.tw_wait_n(8))
@@ -770,29 +785,42 @@ def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None):
         B.mulrows(dmap, list(range(8 * bt, 8 * bt + 8)), [buf(bt % 2, k) for k in range(8)], ms, zero_hi=False)
 
 
-def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None):
+def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False):
     """Forward transform of the W0 data in dmap (must be v64..v127); returns the output dmap (W0,
-    canonical).  With `stop`, returns early (debug bodies)."""
-    fb = free_blocks_except(dmap)
+    canonical).  With `stop`, returns early (debug bodies).  `prefetch` (the standalone kernel, whose
+    waves run in lockstep so a wait on a table load is not covered by other waves): the first twist
+    batch is loaded before the G1 stages into v8..v23 and the lane-pair table twiddles right after T1,
+    each load's latency hidden behind the stages in between (one or two fewer scratch slots there)."""
+    busy = tuple(range(8, 24)) if prefetch else ()
+    if prefetch:
+        B.raw(*[ad.tw_load(0, k, 8 + 2 * k) for k in range(8)])
+    fb = free_blocks_except(dmap, busy)
     for s in range(5):
         B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
     if stop == "g1":
         return dmap
     # twist: 4 batches of 8 rows; table rows double-buffered in v8..v23 / v48..v63 (batch bt + 1
     # loads while batch bt multiplies), 2 multiply slots in v24..v47
-    twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)])
+    twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)], first_loaded=prefetch)
     if stop == "twist":
         return dmap
     dmap = t1(B, dmap, 8, 64, ad)
     if stop == "t1":
         return dmap
-    fb = free_blocks_except(dmap)
+    pre, busy = None, ()
+    if prefetch:
+        gks = pair_stage_gmul_ks(tabs, True)
+        fb0 = free_blocks_except(dmap)
+        pre = {k: fb0[0] + 2 * i for i, k in enumerate(gks)}
+        busy = tuple(range(fb0[0], fb0[0] + 8))
+        B.raw(*[ad.lw_load(r, k) for k, r in pre.items()])
+    fb = free_blocks_except(dmap, busy)
     cf = [True] * 32  # twist outputs are canonical
     for q in range(5):
         B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf)
     if stop == "cyc":
         return dmap
-    pair_stage(B, dmap, True, ad)
+    pair_stage(B, dmap, True, ad, tabs, pre, busy)
     if stop == "last":
         return dmap
     return t_iw0(B, dmap, True, 96, 64, ad)
@@ -805,7 +833,7 @@ def gen_fwd(tabs, stop=None):
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    dmap = fwd_core(B, tabs, dmap, stop=stop)
+    dmap = fwd_core(B, tabs, dmap, stop=stop, prefetch=True)
     if stop:
         B.raw(*store_raw(dmap))
         return B
@@ -813,23 +841,41 @@ def gen_fwd(tabs, stop=None):
     return B
 
 
-def inv_core(B, tabs, dmap, ad=NTT_ADDR):
-    """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical)."""
+INV_PRE_LW = 40          # v40..v43: the inverse lane-pair table twiddles, loaded with the data
+INV_PRE_TW = 40          # v40..v55: the first untwist batch, loaded during the lane-pair stage
+
+
+def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False):
+    """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  `prefetch`
+    (standalone kernel, see fwd_core): the caller has loaded the lane-pair table twiddles into
+    v40..v43 with the data; the first untwist batch is loaded into v40..v55 after the lane-pair stage
+    and stays there through the cyclic stages and T4 (the one register range free in both layouts)."""
     dmap = t1(B, dmap, 8, 64, ad)
-    pair_stage(B, dmap, False, ad)
-    fb = free_blocks_except(dmap)
+    gks = pair_stage_gmul_ks(tabs, False)
+    pre = {k: INV_PRE_LW + 2 * i for i, k in enumerate(gks)} if prefetch else None
+    pair_stage(B, dmap, False, ad, tabs, pre, tuple(range(INV_PRE_LW, INV_PRE_LW + 8)) if prefetch else ())
+    busy = tuple(range(INV_PRE_TW, INV_PRE_TW + 16)) if prefetch else ()
+    if prefetch:
+        B.raw(*[ad.tw_load(0, k, INV_PRE_TW + 2 * k) for k in range(8)])
+    fb = free_blocks_except(dmap, busy)
     cf = [False] * 32
     for q in range(4, -1, -1):
         B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
     dmap = t_iw0(B, dmap, False, 96, 64, ad)
     # untwist: table rows and multiply slots in the registers the data does not occupy
-    free = free_blocks_except(dmap)
+    free = free_blocks_except(dmap, busy)
     regs = []
     for b in free:
         regs += list(range(b, b + 8))
-    assert len(regs) >= 56, len(regs)
-    twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(regs[32 + 12 * i], SG0 + 6 * i) for i in range(2)],
-               contiguous=False, regs=regs)
+    if prefetch:
+        assert len(regs) >= 40, len(regs)
+        tregs = list(range(INV_PRE_TW, INV_PRE_TW + 16)) + regs[0:16]
+        ms = [MulSlot(0, SG0, regs[16:28]), MulSlot(0, SG0 + 6, regs[28:40])]
+        twist_rows(B, dmap, ad, None, ms, contiguous=False, regs=tregs, first_loaded=True)
+    else:
+        assert len(regs) >= 56, len(regs)
+        twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(regs[32 + 12 * i], SG0 + 6 * i) for i in range(2)],
+                   contiguous=False, regs=regs)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
@@ -850,8 +896,10 @@ def gen_inv(tabs, stop=None):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
-    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    dmap = inv_core(B, tabs, dmap)
+    gks = pair_stage_gmul_ks(tabs, False)
+    B.raw(*load_rows(dmap, S_GB), *[NTT_ADDR.lw_load(INV_PRE_LW + 2 * i, k) for i, k in enumerate(gks)],
+          "s_waitcnt vmcnt(0)")
+    dmap = inv_core(B, tabs, dmap, prefetch=True)
     B.raw(*store_rows(dmap, S_GB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
 
