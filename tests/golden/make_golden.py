@@ -73,7 +73,27 @@ def make_one(name, p, n):
     )
 
 
+def make_large(n):
+    """A single-polynomial Solinas fixture beyond one workgroup (the engine's two-pass large-N path):
+    x, fwd(x), inv(x) only, self-checked by inv(fwd(x)) = N x and canonical outputs."""
+    p = O.SOLINAS_P
+    plan = O.Plan.try_new(n, p)
+    x = O.fill_uniform(SEED + n, p, n).reshape(1, n)
+    fx, ix = plan.fwd(x, threads=8), plan.inv(x, threads=8)
+    back = plan.inv(fx, threads=8)
+    assert all(int(b) == O.mul_mod(int(v), n, p) for b, v in zip(back[0], x[0]))
+    assert int(fx.max()) < p and int(ix.max()) < p
+    return dict(p=np.array([p], np.uint64), n=np.array([n], np.uint64), x=x, fwd_x=fx, inv_x=ix)
+
+
+LARGE_SIZES = [32768]
+
+
 def main():
+    for n in LARGE_SIZES:
+        path = os.path.join(HERE, f"large_solinas_n{n}.npz")
+        np.savez_compressed(path, **make_large(n))
+        print("wrote", os.path.relpath(path, ROOT))
     for name, p in golden_primes().items():
         for n in SIZES.get(name, SIZES["default"]):
             if O.Plan.try_new(n, p) is None:

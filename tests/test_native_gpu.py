@@ -27,7 +27,7 @@ def _primes32(oracle):
     return [1062862849, 1073479681, lo30, lo31, NO.PRIMES32[9]]
 
 
-@pytest.mark.parametrize("n", [32, 1024, 2048])
+@pytest.mark.parametrize("n", [32, 1024, 2048, 32768])
 def test_prime32_plan_parity(engine, oracle, n):
     import torch
     for p in _primes32(oracle):

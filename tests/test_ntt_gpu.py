@@ -33,8 +33,9 @@ def host(t):
     return t.cpu().numpy().view(np.uint64)
 
 
-@pytest.mark.parametrize("logn", list(range(4, 15)))
+@pytest.mark.parametrize("logn", list(range(4, 19)))
 def test_fwd_inv_all_sizes_solinas(engine, oracle, logn):
+    """N = 16 ... 2^18; N > 2^14 runs the two-pass large-N path (top stages + 2^14 blocks)."""
     n = 1 << logn
     batch = max(1, min(37, (1 << 17) // n))  # ragged (not a multiple of the polys-per-workgroup)
     plan, ora = engine.Plan.try_new(n, SOLINAS_P), oracle.Plan.try_new(n, SOLINAS_P)
@@ -51,12 +52,15 @@ def test_fwd_inv_all_sizes_solinas(engine, oracle, logn):
 
 
 @pytest.mark.parametrize("name", ["p64", "p63", "p62", "p50", "p30"])
-@pytest.mark.parametrize("logn", [4, 5, 10, 11, 12])
+@pytest.mark.parametrize("logn", [4, 5, 10, 11, 12, 15, 16])
 def test_fwd_inv_other_primes(engine, oracle, name, logn):
     p = _primes(oracle)[name]
     n = 1 << logn
     plan, ora = engine.Plan.try_new(n, p), oracle.Plan.try_new(n, p)
-    batch = 5
+    assert (plan is None) == (ora is None)  # no 2N-th root: None on both sides
+    if ora is None:
+        return
+    batch = 5 if logn < 15 else 2
     x = oracle.fill_uniform(17 + logn, p, batch * n).reshape(batch, n)
     t = dev(x)
     plan.fwd(t)
@@ -64,6 +68,26 @@ def test_fwd_inv_other_primes(engine, oracle, name, logn):
     t = dev(x)
     plan.inv(t)
     assert np.array_equal(host(t), ora.inv(x))
+
+
+@pytest.mark.parametrize("logn,batch", [(15, 3), (17, 2)])
+def test_large_n_strided_batch(engine, oracle, logn, batch):
+    """Large-N path on a padded-stride batch: bit-exact, gaps never written, inv(fwd(x)) = N x."""
+    import torch
+    n = 1 << logn
+    stride = n + 64
+    plan, ora = engine.Plan.try_new(n, SOLINAS_P), oracle.Plan.try_new(n, SOLINAS_P)
+    full = oracle.fill_uniform(0xB16 + logn, SOLINAS_P, batch * stride).reshape(batch, stride)
+    t = dev(full)
+    plan.fwd(t[:, :n])
+    out = host(t)
+    fx = ora.fwd(np.ascontiguousarray(full[:, :n]), threads=8)
+    assert np.array_equal(out[:, :n], fx) and np.array_equal(out[:, n:], full[:, n:])
+    plan.inv(t[:, :n])
+    back = host(t)[:, :n]
+    want = np.array([[oracle.mul_mod(int(v), n, SOLINAS_P) for v in row[:64]] for row in full[:, :n]], np.uint64)
+    assert np.array_equal(back[:, :64], want)
+    assert np.array_equal(back, ora.inv(fx, threads=8))
 
 
 def test_strided_batch_leaves_gaps_untouched(engine, oracle):

@@ -26,16 +26,22 @@ namespace mi {
 
 // IO = u64 (prime64 plans) or uint32_t (prime32 plans, prime32.rs:797-898: the same transform on
 // u32 buffers; arithmetic stays 64-bit Montgomery, exact for any odd prime)
-template <class G, bool FWD, class Mod, class IO>
+// SUB: large-N plans; the launch covers batch * 2^sub_log blocks of N = 2^G::LOGN, block b of
+// polynomial q at data + q * stride + b * N, with the block's twiddle multiplier 2^sub_log + b.
+template <class G, bool FWD, class Mod, class IO, bool SUB = false>
 __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__ data, uint32_t batch, uint64_t stride,
-                                                                const u64* __restrict__ tw, Mod mod) {
+                                                                const u64* __restrict__ tw, Mod mod,
+                                                                uint32_t sub_log = 0) {
   __shared__ u64 lds[G::PPW * G::PADDED];
   const int tid = threadIdx.x;
   const int pw = tid >> G::LOGT;     // polynomial within the workgroup
   const int t = tid & (G::T - 1);    // lane within the polynomial
-  const uint64_t poly = (uint64_t)blockIdx.x * G::PPW + pw;
+  const uint64_t unit = (uint64_t)blockIdx.x * G::PPW + pw;
+  const uint64_t poly = SUB ? unit >> sub_log : unit;
+  const uint32_t blk = SUB ? (uint32_t)(unit & ((1u << sub_log) - 1)) : 0;
+  const uint32_t twc = SUB ? (1u << sub_log) + blk : 1;
   const bool valid = poly < batch;
-  IO* __restrict__ src = data + poly * stride;
+  IO* __restrict__ src = data + poly * stride + (SUB ? (uint64_t)blk * G::N : 0);
   u64* sh = lds + pw * G::PADDED;
 
   u64 x[G::E];
@@ -55,13 +61,56 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__
       for (int r = 0; r < G::E; ++r) x[r] = sh[lds_addr(elem<G>(t, r, lo))];
       __syncthreads();
     }
-    window_butterflies<G, FWD>(x, t, w, tw, mod);
+    window_butterflies<G, FWD, Mod, SUB>(x, t, w, tw, mod, twc);
   }
   if (valid) {
     const int lo = win_lo<G, FWD>(G::NWIN - 1);
 #pragma unroll
     for (int r = 0; r < G::E; ++r) src[elem<G>(t, r, lo)] = (IO)x[r];
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Large-N plans (N > 2^14, beyond one workgroup's registers): the transform is split in two passes
+// through memory, the decomposition the reference's depth-first recursion also uses
+// (generic_solinas.rs:931-1032: top stages on the whole polynomial, then independent halves).
+//   forward = K top CT stages on strided columns (this kernel), then 2^K independent blocks of
+//             2^14 with the remaining stages (ntt_window_kernel<SUB>, twiddle multiplier 2^K + b);
+//   inverse = the blocks' GS stages first, then the K bottom GS stages on strided columns.
+// Thread j of polynomial q owns the 2^K elements j + i N / 2^K (i < 2^K): coalesced across j.
+template <int K, bool FWD, class Mod, class IO>
+__global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn,
+                                                      const u64* __restrict__ tw, Mod mod) {
+  constexpr int R = 1 << K;
+  const uint64_t cols = (uint64_t)1 << (logn - K);
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  IO* __restrict__ src = data + (uint64_t)blockIdx.y * stride + j;
+  u64 x[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) x[i] = (u64)src[i * cols];
+#pragma unroll
+  for (int st = 0; st < K; ++st) {
+    const int s = FWD ? st : K - 1 - st;  // stage s has m = 2^s groups, pair distance 2^(K-1-s) in i
+    const int m = 1 << s, d = 1 << (K - 1 - s);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i & d) continue;
+      const u64 wv = tw[m + (i >> (K - s))];
+      if (FWD) {
+        const u64 z = mod.mul(x[i + d], wv);
+        const u64 a = x[i];
+        x[i] = mod.add(a, z);
+        x[i + d] = mod.sub(a, z);
+      } else {
+        const u64 a = x[i], b = x[i + d];
+        x[i] = mod.add(a, b);
+        x[i + d] = mod.mul(mod.sub(a, b), wv);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -77,9 +126,55 @@ static hipError_t launch_window(IO* data, size_t batch, size_t stride, const u64
   return hipGetLastError();
 }
 
+constexpr int SUB_LOGN = 14;  // block size of the large-N second pass
+
+template <int K, bool FWD, class Mod, class IO>
+static hipError_t launch_top(IO* data, size_t batch, size_t stride, int logn, const u64* tw, const Mod& mod,
+                             hipStream_t s) {
+  const uint64_t cols = (uint64_t)1 << (logn - K);
+  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Mod, IO>), grid, dim3(256), 0, s, data, (uint64_t)stride, (uint32_t)logn,
+                     tw, mod);
+  return hipGetLastError();
+}
+
+template <bool FWD, class Mod, class IO>
+static hipError_t dispatch_large(int logn, IO* data, size_t batch, size_t stride, const u64* tw, const Mod& mod,
+                                 hipStream_t s) {
+  const int k = logn - SUB_LOGN;
+  if (k < 1 || k > 4) return hipErrorInvalidValue;
+  if (batch > 65535) {  // the top pass puts polynomials on grid.y
+    for (size_t b0 = 0; b0 < batch; b0 += 65535) {
+      const size_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+      const hipError_t e = dispatch_large<FWD>(logn, data + b0 * stride, nb, stride, tw, mod, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  auto top = [&]() -> hipError_t {
+    switch (k) {
+      case 1: return launch_top<1, FWD>(data, batch, stride, logn, tw, mod, s);
+      case 2: return launch_top<2, FWD>(data, batch, stride, logn, tw, mod, s);
+      case 3: return launch_top<3, FWD>(data, batch, stride, logn, tw, mod, s);
+      default: return launch_top<4, FWD>(data, batch, stride, logn, tw, mod, s);
+    }
+  };
+  auto blocks = [&]() -> hipError_t {
+    using G = Geo<SUB_LOGN, 4>;
+    const uint64_t units = (uint64_t)batch << k;
+    hipLaunchKernelGGL((ntt_window_kernel<G, FWD, Mod, IO, true>), dim3((unsigned)units), dim3(G::THREADS), 0, s, data,
+                       (uint32_t)batch, (uint64_t)stride, tw, mod, (uint32_t)k);
+    return hipGetLastError();
+  };
+  hipError_t e = FWD ? top() : blocks();
+  if (e == hipSuccess) e = FWD ? blocks() : top();
+  return e;
+}
+
 template <bool FWD, class Mod, class IO>
 static hipError_t dispatch(int logn, IO* data, size_t batch, size_t stride, const u64* tw,
                            const Mod& mod, hipStream_t s) {
+  if (logn > SUB_LOGN) return dispatch_large<FWD>(logn, data, batch, stride, tw, mod, s);
   switch (logn) {
     case 4: return launch_window<4, 3, FWD>(data, batch, stride, tw, mod, s);
     case 5: return launch_window<5, 3, FWD>(data, batch, stride, tw, mod, s);

@@ -49,9 +49,12 @@ __host__ __device__ __forceinline__ constexpr int win_lo(int w) {
   return (w < G::NFULL) ? G::LOGE * w : G::LOGN - G::LOGE;
 }
 
-template <class G, bool FWD, class Mod>
+// `twc` (SUB only): the transform is block b of 2^k blocks left by k top stages of a larger one
+// (large-N plans): its stage with m groups reads the big table at m * twc + g, twc = 2^k + b, because
+// the big stage has m 2^k groups and block b owns groups [b m, (b + 1) m).
+template <class G, bool FWD, class Mod, bool SUB = false>
 __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w, const u64* __restrict__ tw,
-                                                   const Mod& mod) {
+                                                   const Mod& mod, uint32_t twc = 1) {
   const int lo = win_lo<G, FWD>(w);
   int rb_first, rb_last;  // r-bits of this window that still need a stage
   if (w < G::NFULL) { rb_first = 0; rb_last = G::LOGE - 1; }
@@ -70,7 +73,7 @@ __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w,
     for (int r0 = 0; r0 < G::E; ++r0) {
       if (r0 & half) continue;
       const int r1 = r0 | half;
-      const u64 wv = tw[m + (tpart | (r0 >> (rb + 1)))];
+      const u64 wv = tw[(SUB ? m * twc : m) + (tpart | (r0 >> (rb + 1)))];
       if (FWD) {
         const u64 z1w = mod.mul(x[r1], wv);
         const u64 a = x[r0];
