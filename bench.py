@@ -209,6 +209,41 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
     return res
 
 
+def bench_pbs_solinas(args, eng, torch, dev, world, barrier):
+    """Solinas-modulus PBS (programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized, ntt64_pbs.rs:482-538)
+    at the PARAM_MESSAGE_2_CARRY_2 shape with q = p: the reference's own NTT PBS benchmark runs the shortint
+    parameter sets with this custom modulus (tfhe-benchmark/benches/core_crypto/pbs_bench.rs:646-905)."""
+    M = eng.ntt64_pbs
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    n_lwe, batch = PBS_N_LWE, args.pbs_batch
+    bsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 60, SOLINAS_P)
+    key = M.NttBootstrapKey(plan, bsk, PBS_BASE_LOG, PBS_LEVEL, M.SOLINAS)
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 61, SOLINAS_P)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 62, SOLINAS_P)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+    run = lambda: M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe, out, lut, key)
+    run()
+    torch.cuda.synchronize()
+    K = args.pbs_steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    del key
+    return {"metric": "PBS/sec, Solinas modulus (ntt64_pbs), PARAM_MESSAGE_2_CARRY_2 shape", "value": world * batch * K / el,
+            "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3,
+            "config": {"workload": "programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized, q = 2^64 - 2^32 + 1, "
+                                   "n=918 k=1 N=2048 base_log=23 level=1 (pbs_bench.rs:646-905 shape)",
+                       "batch_per_gpu": batch}}
+
+
 def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk):
     """Config 5: one global batch of PBS (default 65,536) held on the root, scattered over the ranks,
     bootstrapped, gathered back (strong scaling).  The transfers are grouped point-to-point sends from
@@ -560,6 +595,7 @@ def main():
     if not args.no_pbs:
         out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
+        out["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
         out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -96,3 +96,66 @@ def test_emulated_decomposition_corners(oracle, base_log):
     out = np.array([rnd.getrandbits(64) for _ in range(2 * N)], dtype=np.uint64)
     _, o = asm_emu.run_ext(HDR, glwe, out, ggsw, tf + ti + ti_norm, base_log, False)
     assert np.array_equal(o.reshape(-1), ctx.ext_product(out, ggsw, glwe, 1, base_log, 1, bnf=True))
+
+
+def _sol_ms(a):
+    """pbs_tw.hip's pre-switch of a Solinas mask element (ms_non_native mod 2N)."""
+    import oracle as O
+    return O.pbs_modulus_switch_non_native(int(a), N, P) % (2 * N)
+
+
+@pytest.mark.parametrize("seed,base_log", [(1, 23), (2, 10), (3, 31), (4, 1)])
+def test_emulated_solinas_pbs_matches_oracle(oracle, seed, base_log):
+    """Solinas-modulus blind rotation (ntt64_pbs.rs:213-286): the body on the pre-switched mask and the
+    wrapper's LUT pre-rotation / sample extraction vs the oracle PBS, bit for bit."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_emu
+    plan, tf, ti = _tables(oracle)
+    ctx = oracle.NttContext(N)
+    rnd = random.Random(100 + seed)
+    n_lwe = 4
+    bsk = np.array([rnd.randrange(P) for _ in range(n_lwe * 4 * N)], dtype=np.uint64)  # Normalize key
+    lut = np.array([rnd.randrange(P) for _ in range(2 * N)], dtype=np.uint64)
+    lut[:4] = [0, P - 1, 1, P // 2]
+    # mask: 0 (skipped), values that switch to 0 / 2N / the wrap, extremes, random
+    lwe = [0, P - 1, P // 2, 1] if seed == 1 else [rnd.randrange(P) for _ in range(n_lwe)]
+    lwe = np.array(lwe + [rnd.randrange(P)], dtype=np.uint64)
+    want = ctx.pbs(lwe, lut, bsk, 1, base_log, 1, bnf=False)
+    msb = oracle.pbs_modulus_switch_non_native(int(lwe[-1]), N, P)
+    acc0 = np.stack([oracle.poly_monomial_div(lut[c * N:(c + 1) * N], msb, P) for c in range(2)])
+    msed = np.array([_sol_ms(a) for a in lwe[:-1]] + [0], dtype=np.uint64)
+    acc = asm_emu.run_pbs(HDR, msed, lut, bsk, tf + ti, base_log, n_lwe, name="sol_l1", acc0=acc0)
+    got = oracle.sample_extract(acc.reshape(-1), N, 1, P)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("cmux", [False, True])
+@pytest.mark.parametrize("base_log", [23, 10, 31, 1])
+def test_emulated_solinas_ext_product_corners(oracle, cmux, base_log):
+    """Solinas external product / CMUX (ntt64_pbs.rs:553-702) with the non-native decomposition's
+    corners: the sign threshold p/2 + 1 and its neighbours, 0, 1, p - 1 and the rounding boundaries
+    k 2^(63-B) +- 1 of the magnitude, on both sides of the threshold."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import asm_emu
+    plan, tf, ti = _tables(oracle)
+    ctx = oracle.NttContext(N)
+    rnd = random.Random(base_log + 50 * cmux)
+    half = P // 2 + 1
+    q = 1 << (63 - base_log)
+    corners = [half, half - 1, half + 1, P // 2, 0, 1, 2, P - 1, P - 2, q, q - 1, q // 2, q // 2 + 1, 3 * q // 2,
+               (1 << 62), (1 << 63) - 1 - P // 2]
+    vals = []
+    for c in corners:
+        for d in (-1, 0, 1):
+            vals += [(c + d) % P, (P - c - d) % P]
+    glwe = np.array((vals * (2 * N // len(vals) + 1))[: 2 * N], dtype=np.uint64)
+    rnd.shuffle(glwe)
+    ggsw = np.array([rnd.randrange(P) for _ in range(4 * N)], dtype=np.uint64)
+    out = np.array([rnd.randrange(P) for _ in range(2 * N)], dtype=np.uint64)
+    g, o = asm_emu.run_ext(HDR, glwe, out, ggsw, tf + ti, base_log, cmux, sol=True)
+    if cmux:
+        want = ctx.cmux(out, glwe, ggsw, 1, base_log, 1, bnf=False)
+        assert np.array_equal(g.reshape(-1), np.array([(int(a) - int(b)) % P for a, b in zip(glwe, out)], np.uint64))
+    else:
+        want = ctx.ext_product(out, ggsw, glwe, 1, base_log, 1, bnf=False)
+    assert np.array_equal(o.reshape(-1), want)

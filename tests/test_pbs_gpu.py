@@ -227,3 +227,84 @@ def test_pbs_pre_switched(engine, plan, ctx, oracle, bnf):
           else M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)
     fn(dev(msed), out, dev(lut), key, M.MS_PRE_SWITCHED)
     assert np.array_equal(host(out), want)
+
+
+def _fast_bsk_solinas(oracle, g, lwe_sk, glwe_sk, base_log, noise_log2):
+    """H.bsk_gen for q = p with the GLWE mask products through the oracle's NTT (exact mod (X^N + 1, p)):
+    GGSW rows as ggsw_encryption.rs:20-45, level 1, k = 1.  Test infrastructure only."""
+    n_lwe, n = lwe_sk.size, glwe_sk.shape[1]
+    plan = oracle.Plan.try_new(n, P)
+    masks = g.integers(0, P, size=(n_lwe * 2, n), dtype=np.uint64)
+    s_hat = plan.fwd(glwe_sk[0].astype(np.uint64))
+    prod = plan.inv(plan.mul_assign_normalize(plan.fwd(masks, threads=16), np.broadcast_to(s_hat, masks.shape).copy()),
+                    threads=16)
+    bsk = np.zeros((n_lwe, 1, 2, 2, n), np.uint64)
+    factor0 = pow(2, 64 - base_log, P)
+    s_obj = glwe_sk[0].astype(object)
+    for i, b in enumerate(lwe_sk):
+        factor = (-int(b) * factor0) % P
+        for r in range(2):
+            body = prod[2 * i + r].astype(object)
+            if r == 0:
+                body = body + s_obj * factor
+            else:
+                body[0] = body[0] + (-factor) % P
+            e = H.noise_q(g, n, noise_log2, P).astype(object)
+            bsk[i, 0, r, 0] = masks[2 * i + r]
+            bsk[i, 0, r, 1] = np.array((body + e) % P, dtype=np.uint64)
+    return bsk
+
+
+def test_pbs_solinas_reference_params(engine, plan, ctx, oracle):
+    """The reference's own Solinas PBS test shape, TEST_PARAMS_3_BITS_SOLINAS_U64 (algorithms/test/mod.rs:106-128:
+    n = 742, N = 2048, B = 2^23, l = 1, 3-bit messages, q = p) with the property of
+    lwe_encrypt_pbs_ntt64_decrypt_custom_mod (lwe_programmable_bootstrapping.rs:708-865): decrypt(PBS(Enc(m)))
+    decodes to f(m) = m mod 8 for every m; plus the GPU output equals the oracle PBS bit for bit.  Real keys
+    (uniform noise at the reference's standard deviations: 2^46 LWE, 2^12 GLWE), the key converted Normalize on
+    the GPU; runs on the twisted Solinas engine (pbs_tw.hip)."""
+    n_lwe, base_log, level, msg_mod = 742, 23, 1, 8
+    delta = (P // 2) // msg_mod  # get_encoding_with_padding(custom) = q / 2
+    g = H.rng(742)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (K, N))
+    bsk = _fast_bsk_solinas(oracle, g, lwe_sk, glwe_sk, base_log, 12)
+    f = lambda x: x % msg_mod
+    lut = H.pbs_lut(N, K, msg_mod, delta, f, P)
+    msgs = list(range(msg_mod)) * 2
+    lwe = np.stack([H.lwe_encrypt(g, (m * delta) % P, lwe_sk, 46, P) for m in msgs])
+    M = engine.ntt64_pbs
+    gkey = dev(np.zeros_like(bsk))
+    M.convert_standard_lwe_bootstrap_key_to_ntt64(plan, dev(bsk), gkey, normalize=True, input_modulus_width=None)
+    nbsk = host(gkey)
+    key = M.NttBootstrapKey(plan, gkey, base_log, level, M.SOLINAS)
+    out = dev(np.zeros((len(msgs), K * N + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    out_sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    for i, m in enumerate(msgs):
+        pt = H.lwe_decrypt(got[i], out_sk, P)
+        assert H.decode(pt, delta, msg_mod, P) % msg_mod == f(m), (m, pt)
+    want = np.stack([ctx.pbs(lwe[i], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, bnf=False)
+                     for i in range(4)])
+    assert np.array_equal(got[:4], want)
+
+
+@pytest.mark.parametrize("batch", [1, 37])
+def test_pbs_solinas_config4_shape(engine, plan, ctx, batch):
+    """Solinas-modulus PBS at the PARAM_MESSAGE_2_CARRY_2 shape (n = 918, B = 2^23, l = 1) on a random key
+    (the reference's NTT PBS bench shape, pbs_bench.rs:646-905), vs the oracle; masks hit 0 (skipped)
+    and values that switch to 2N."""
+    g = H.rng(9180 + batch)
+    n_lwe, base_log, level = 918, 23, 1
+    bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)
+    lut = rand_q(g, (K + 1, N), P)
+    lwe = _pbs_inputs(g, batch, n_lwe, P)
+    lwe[:, 9::17] = np.uint64(P - 1)
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(plan, dev(bsk), base_log, level, M.SOLINAS)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    for b in range(min(batch, 3)):
+        want = ctx.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, bnf=False)
+        assert np.array_equal(got[b], want)

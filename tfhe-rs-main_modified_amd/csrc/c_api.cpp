@@ -357,10 +357,11 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
 
 extern "C" {
 
-// the twisted-transform bodies (pbs_tw.hip) cover BNF, level 1, base_log <= 31 on the Solinas N = 2048
-// plan; every other shape runs the generic kernels (pbs_kernels.hip)
+// the twisted-transform bodies (pbs_tw.hip) cover level 1, base_log <= 31 (BNF and Solinas) on the
+// Solinas N = 2048 plan; every other shape runs the generic kernels (pbs_kernels.hip)
 static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int base_log, int level) {
-  return variant == MI_NTT64_BNF && level == 1 && base_log <= 31 && plan->twisted;
+  (void)variant;
+  return level == 1 && base_log <= 31 && plan->twisted;
 }
 
 int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
@@ -387,8 +388,8 @@ int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, co
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
   if (twisted_ext_applies(plan, variant, base_log, level)) {
-    hipError_t e = mi::launch_ext_tw(false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_ntt, batch, base_log,
-                                     plan->d_twist_f, (hipStream_t)stream);
+    hipError_t e = mi::launch_ext_tw(false, variant == MI_NTT64_SOLINAS, out_glwe, const_cast<uint64_t*>(in_glwe),
+                                     ggsw_ntt, batch, base_log, plan->d_twist_f, (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
   }
   hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
@@ -406,7 +407,8 @@ int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1,
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
   if (twisted_ext_applies(plan, variant, base_log, level)) {
-    hipError_t e = mi::launch_ext_tw(true, ct0, ct1, ggsw_ntt, batch, base_log, plan->d_twist_f, (hipStream_t)stream);
+    hipError_t e = mi::launch_ext_tw(true, variant == MI_NTT64_SOLINAS, ct0, ct1, ggsw_ntt, batch, base_log,
+                                     plan->d_twist_f, (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
   }
   hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
@@ -484,6 +486,25 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   const mi_ntt64_plan* plan = key->plan;
   const hipStream_t s = (hipStream_t)stream;
   DeviceGuard g(plan->device);
+  if (key->variant == MI_NTT64_SOLINAS && twisted_ext_applies(plan, key->variant, key->base_log, key->level)) {
+    // Solinas on the twisted engine: the body reads switched values (the caller's, or switched here
+    // into stream-ordered scratch by ms_non_native)
+    const size_t count = batch * (key->n_lwe + 1);
+    u64* sw = nullptr;
+    if (ms_mode != MI_MS_PRE_SWITCHED) {
+      if (hipMallocAsync((void**)&sw, count * sizeof(u64), s) != hipSuccess)
+        return fail(MI_ERR_OOM, "scratch allocation failed");
+      hipError_t e = mi::launch_ms_non_native(sw, lwe_in, count, s);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(sw, s);
+        return hip_fail(e, "modulus switch launch");
+      }
+    }
+    hipError_t e = mi::launch_pbs_tw_sol(lwe_out, sw ? sw : lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
+                                         plan->d_twist_f, s);
+    if (sw) (void)hipFreeAsync(sw, s);
+    return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
+  }
   u64* lifted = nullptr;  // PRE_SWITCHED: stream-ordered copy lifted back to the standard switch
   if (ms_mode == MI_MS_PRE_SWITCHED) {
     const size_t count = batch * (key->n_lwe + 1);

@@ -65,8 +65,12 @@ hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in
 // BNF, level 1, base_log <= 31, on the twisted transform; tab = plan twist tables [fwd | inverse]
 // BNF level-1 external product (cmux=false: out += GGSW . glwe) / CMUX (cmux=true: ct0 = out,
 // ct1 = glwe) on the twisted transform; the GGSW is the Raw NTT key (N^-1 via the third table)
-hipError_t launch_ext_tw(bool cmux, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch, int base_log,
-                         const uint64_t* tab, hipStream_t s);
+hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
+                         int base_log, const uint64_t* tab, hipStream_t s);
+// Solinas PBS on the twisted engine: switched = pre-switched mask + body values in [0, 2N)
+hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s);
+hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,
+                             size_t n_lwe, size_t batch, int base_log, const uint64_t* tab, hipStream_t s);
 hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const uint64_t* bsk, size_t n_lwe,
                          size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s);
 

@@ -1,6 +1,7 @@
-// pbs_tw.hip — programmable bootstrap, BNF flavour, decomposition level 1, on the twisted N = 2048
-// Goldilocks transform (reference: tfhe/src/core_crypto/algorithms/lwe_programmable_bootstrapping/
-// ntt64_bnf_pbs.rs:208-726, programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized).
+// pbs_tw.hip — programmable bootstrap, BNF and Solinas flavours, decomposition level 1, on the twisted
+// N = 2048 Goldilocks transform (reference: tfhe/src/core_crypto/algorithms/lwe_programmable_bootstrapping/
+// ntt64_bnf_pbs.rs:208-726, programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized; ntt64_pbs.rs:
+// 213-702, programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized).
 //
 // MI355X design: one 128-lane workgroup (2 waves) per LWE ciphertext.  Each wave keeps one GLWE
 // polynomial of the accumulator in VGPRs (v128..v191) for the whole blind rotation and runs the
@@ -115,8 +116,84 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   }
 }
 
-// external product / CMUX batch (config 3): one workgroup per GLWE pair, wave w on polynomial w
-template <bool CMUX>
+// ---- Solinas-modulus PBS (ntt64_pbs.rs:213-286, 482-538) on the same engine ---------------------------
+static constexpr u64 P = GL_P;
+__device__ __forceinline__ u64 neg_custom(u64 a) { return a == 0 ? 0 : P - a; }
+
+// ntt64_pbs.rs:540-549 pbs_modulus_switch_non_native (divide_round(a 2N, p), misc.rs:6-18), reduced mod
+// 2N: X^(2N) = 1, so a value that rounds to 2N rotates like 0 (and 0 skips the step, whose CMUX
+// difference would be 0 anyway)
+__device__ __forceinline__ u64 ms_non_native(u64 input) {
+  const unsigned __int128 num = ((unsigned __int128)input) << (LOG_MOD);
+  const u64 nh = (u64)(num >> 64), nl = (u64)num;
+  unsigned __int128 r = (unsigned __int128)nh * GL_EPS + nl;  // num = nh p + r
+  u64 q = nh;
+  while (r >= P) { r -= P; ++q; }
+  return (q + (r >= (P >> 1) ? 1 : 0)) & (2 * N - 1);
+}
+
+__global__ __launch_bounds__(256) void ms_non_native_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
+                                                            uint64_t count) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (uint64_t)gridDim.x * 256)
+    dst[i] = ms_non_native(src[i]);
+}
+
+// switched: batch x (n+1) switched values in [0, 2N) (mask, then body); lut: 2 x N mod p;
+// bsk: n x 2 x 2 x N Normalize NTT key.  The LUT is rotated by -ms(b) into LDS first
+// (polynomial_wrapping_monic_monomial_div_assign_custom_mod, ntt64_pbs.rs:237-249); the body runs the
+// loop; sample extraction at nth = 0 negates modulo p (glwe_sample_extraction.rs:89-160).
+__global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ switched,
+                                                         const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                         uint32_t n_lwe, uint32_t batch, int base_log,
+                                                         const u64* __restrict__ tab) {
+  __shared__ u64 buf[2 * N];
+  __shared__ u64 lwtab[64];
+  const int t = threadIdx.x;
+  const uint32_t lane = t & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;
+  const u64* msw = switched + (size_t)b * (n_lwe + 1);
+  load_lane_pair_tables(lwtab, tab, t);
+  {
+    const u64 body = msw[n_lwe] & (2 * N - 1);
+    const int full = (int)(body / N) & 1, rem = (int)(body % N);
+    const u64* l = lut + (size_t)w * N;
+    for (int r = 0; r < 32; ++r) {
+      const int m = 64 * r + (int)lane;  // new[m] = old[(m + rem) % N], negated for m >= N - rem
+      u64 v = l[(m + rem) & (N - 1)];
+      if (full ^ (m >= N - rem)) v = neg_custom(v);
+      buf[w * N + m] = v;
+    }
+  }
+  __syncthreads();
+  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
+  const u64* gown = bsk + (size_t)3 * w * N;
+  const u64* gpar = bsk + (size_t)(2 - w) * N;
+  const uint32_t gown_lo = (uint32_t)(uintptr_t)gown, gown_hi = (uint32_t)((uintptr_t)gown >> 32);
+  const uint32_t gpar_lo = (uint32_t)(uintptr_t)gpar, gpar_hi = (uint32_t)((uintptr_t)gpar >> 32);
+  const uint32_t lwe_lo = (uint32_t)(uintptr_t)msw, lwe_hi = (uint32_t)((uintptr_t)msw >> 32);
+  const uint32_t tab_lo = (uint32_t)(uintptr_t)tab, tab_hi = (uint32_t)((uintptr_t)tab >> 32);
+  MI_PBS_BODY_SOL_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
+                     [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [lwe_lo] "s"(lwe_lo), [lwe_hi] "s"(lwe_hi),
+                     [n] "s"(n_lwe), [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log),
+                     [LW] "s"((uint32_t)(uintptr_t)lwtab));
+  const u64* acc = buf + w * N;
+  u64* out = lwe_out + (size_t)b * (N + 1);
+  if (w == 0) {
+#pragma unroll 4
+    for (int r = 0; r < 32; ++r) {
+      const int j = 64 * r + (int)lane;
+      out[j] = (j == 0) ? acc[0] : neg_custom(acc[N - j]);
+    }
+  } else if (lane == 0) {
+    out[N] = acc[0];
+  }
+}
+
+// external product / CMUX batch (config 3): one workgroup per GLWE pair, wave w on polynomial w;
+// SOL: GLWEs modulo p with a Normalize GGSW (ntt64_pbs.rs:553-702), else BNF (native GLWEs, Raw GGSW)
+template <bool CMUX, bool SOL = false>
 __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                      const u64* __restrict__ ggsw, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab) {
@@ -137,7 +214,17 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
   const uint32_t gown_lo = (uint32_t)(uintptr_t)gown, gown_hi = (uint32_t)((uintptr_t)gown >> 32);
   const uint32_t gpar_lo = (uint32_t)(uintptr_t)gpar, gpar_hi = (uint32_t)((uintptr_t)gpar >> 32);
   const uint32_t tab_lo = (uint32_t)(uintptr_t)tab, tab_hi = (uint32_t)((uintptr_t)tab >> 32);
-  if constexpr (CMUX)
+  if constexpr (SOL && CMUX)
+    MI_PBS_BODY_CMUX_SOL_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
+                            [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
+                            [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
+                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
+  else if constexpr (SOL)
+    MI_PBS_BODY_EXT_SOL_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
+                           [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
+                           [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
+                           [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
+  else if constexpr (CMUX)
     MI_PBS_BODY_CMUX_BNF_L1([lane] "v"(lane), [S] "s"(S), [SP] "s"(SP), [glwe_lo] "s"(g_lo), [glwe_hi] "s"(g_hi),
                             [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
                             [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
@@ -151,16 +238,36 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
 
 }  // namespace pbstw
 
-hipError_t launch_ext_tw(bool cmux, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch, int base_log,
-                         const uint64_t* tab, hipStream_t s) {
+hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
+                         int base_log, const uint64_t* tab, hipStream_t s) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
-  if (cmux)
-    hipLaunchKernelGGL(pbstw::ext_tw_kernel<true>, dim3((unsigned)batch), dim3(128), 0, s, out, glwe, ggsw,
-                       (uint32_t)batch, base_log, tab);
+  const dim3 g((unsigned)batch), blk(128);
+  if (sol && cmux)
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+  else if (sol)
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+  else if (cmux)
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
   else
-    hipLaunchKernelGGL(pbstw::ext_tw_kernel<false>, dim3((unsigned)batch), dim3(128), 0, s, out, glwe, ggsw,
-                       (uint32_t)batch, base_log, tab);
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  uint64_t blocks = (count + 255) / 256;
+  if (blocks > 65535) blocks = 65535;
+  hipLaunchKernelGGL(pbstw::ms_non_native_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, (uint64_t)count);
+  return hipGetLastError();
+}
+
+hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,
+                             size_t n_lwe, size_t batch, int base_log, const uint64_t* tab, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pbstw::pbs_tw_sol_kernel, dim3((unsigned)batch), dim3(128), 0, s, out, switched, lut, bsk,
+                     (uint32_t)n_lwe, (uint32_t)batch, base_log, tab);
   return hipGetLastError();
 }
 

@@ -79,6 +79,9 @@ class Wave:
         b = self.vpair(tok)
         if b is not None:
             return self.v[b] | (self.v[b + 1] << np.uint64(32))
+        sb = self.spair(tok)
+        if sb is not None:
+            return np.full(LANES, self.s[sb] | (self.s[sb + 1] << np.uint64(32)), dtype=np.uint64)
         return np.full(LANES, np.uint64(int(tok, 0) & 0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
 
     def wv(self, r, val):
@@ -183,6 +186,13 @@ class Wave:
 
     def op_v_sub_u32(self, a):
         self.wv(self.vreg(a[0]), (self.src32(a[1]) - self.src32(a[2])) & M32)
+
+    def op_v_cmp_ge_u64_e64(self, a):
+        self.set_mask(a[0], self.src64(a[1]) >= self.src64(a[2]))
+
+    def op_v_bfi_b32(self, a):
+        m = self.src32(a[1])
+        self.wv(self.vreg(a[0]), (m & self.src32(a[2])) | (~m & M32 & self.src32(a[3])))
 
     def op_v_cmp_eq_u32_e64(self, a):
         self.set_mask(a[0], self.src32(a[1]) == self.src32(a[2]))
@@ -402,15 +412,19 @@ def _lds_with_lane_pair_tables(tab, N):
     return lds
 
 
-def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
+def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1", acc0=None):
     """Emulate the 2-wave workgroup of the blind-rotation body (tools/gen_pbs_kernel.py) on one LWE
     ciphertext.  bsk: n x 2 x 2 x N NTT-domain key (N^-1 folded in), tab: the plan's twist tables
-    [fwd | lane-pair | inverse | lane-pair].  Returns the accumulator (2 x N) the body leaves in LDS."""
+    [fwd | lane-pair | inverse | lane-pair].  Returns the accumulator (2 x N) the body leaves in LDS.
+    Solinas bodies (name "sol_l1"): lwe holds the pre-switched mask, acc0 (2 x N) the rotated LUT the
+    wrapper leaves in LDS."""
     N = 2048
     LB, UB, KB, TB = 0x100000000, 0x200000000, 0x300000000, 0x400000000
     mem = {LB: np.array(lwe, dtype=np.uint64), UB: np.array(lut, dtype=np.uint64).reshape(-1),
            KB: np.array(bsk, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
     lds = _lds_with_lane_pair_tables(tab, N)
+    if acc0 is not None:
+        lds[:2 * N] = np.array(acc0, dtype=np.uint64).reshape(-1)
     lines = body_lines(hdr, name, "MI_PBS_BODY_")
     waves = []
     for w in range(2):
@@ -435,7 +449,7 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1"):
     return lds[:2 * N].reshape(2, N).copy()
 
 
-def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
+def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False, sol=False):
     """Emulate the 2-wave external-product / CMUX body on one GLWE pair (glwe, out: 2 x N, updated
     in place and returned); ggsw: 2 x 2 x N Raw NTT key; tab: [fwd | inverse | inverse * N^-1]."""
     N = 2048
@@ -444,7 +458,8 @@ def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False):
     o = np.array(out, dtype=np.uint64).reshape(-1).copy()
     mem = {GB: g, OB: o, KB: np.array(ggsw, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
     lds = _lds_with_lane_pair_tables(tab, N)
-    lines = body_lines(hdr, "cmux_bnf_l1" if cmux else "ext_bnf_l1", "MI_PBS_BODY_")
+    kind = "sol" if sol else "bnf"
+    lines = body_lines(hdr, f"cmux_{kind}_l1" if cmux else f"ext_{kind}_l1", "MI_PBS_BODY_")
     waves = []
     for w in range(2):
         lo = lambda a: str(a & 0xFFFFFFFF)

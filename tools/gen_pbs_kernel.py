@@ -45,7 +45,9 @@ GBUF, PBUF = 208, 240
 S_SH, S_BM1, S_HALF, S_K1, S_FULL = 26, 28, 29, 30, 31   # s27: T.S_X15
 S_TWF, S_TWI, S_GOWN, S_GPAR, S_LWE = 78, 80, 82, 84, 86
 S_CNT, S_AMS, S_A, S_R8, S_HLO = 88, 89, 90, 92, 93
+S_PHALF = 94   # s[94:95] (Solinas bodies): p / 2 + 1, the sign threshold of the non-native decomposition
 SGPR_CLOBBER = list(range(20, 32)) + list(range(36, 94))
+SGPR_CLOBBER_SOL = SGPR_CLOBBER + [94, 95]
 STEP_BYTES = 4 * 2048 * 8   # one level-1 GGSW (2 x 2 polynomials)
 
 
@@ -160,8 +162,34 @@ def decompose(sg, sl, xl, xh):
     sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
 
 
-def rotate_decompose(B):
-    """dmap v64..v127 <- decompose(+-acc[(e - a) mod N] - acc[e])."""
+def decompose_sol(sg, sl, xl, xh):
+    """Level-1 signed decomposition of x in [0, p] modulo the Solinas prime, in place, mapped into
+    [0, p): TensorSignedDecompositionLendingIterNonNative (iter.rs:623-745) with one level.  The sign is
+    s = x >= p / 2 + 1 (div_ceil), the magnitude |x| = s ? p - x : x < 2^63, the rounded state
+    (closest_abs_nonnative, decomposer.rs:521-548) ((|x| >> (63 - B)) + 1) >> 1 <= 2^(B-1), so the one
+    level's digit is that state itself (decompose_one_level never carries here); the signed digit
+    d = s ? -state : state becomes d mod p as in `decompose` (x = p decomposes like 0)."""
+    v, c = sl.v, sl.c
+    nl, nh, t = v[1], v[2], v[3]
+    sg.add(f"v_cmp_ge_u64_e64 {c[2]}, {T.pv(int(xl[1:]))}, s[{S_PHALF}:{S_PHALF + 1}]", [xl, xh], [c[2]])
+    sg.add(f"v_sub_co_u32_e64 {nl}, {c[0]}, 1, {xl}", [xl], [nl, c[0]])
+    sg.add(f"v_subb_co_u32_e64 {nh}, {JUNK}, -1, {xh}, {c[0]}", [xh, c[0]], [nh, JUNK])
+    sg.add(f"v_cndmask_b32_e64 {nh}, {xh}, {nh}, {c[2]}", [xh, nh, c[2]], [nh])       # |x| high word
+    sg.add(f"v_lshrrev_b32 {t}, s{S_SH}, {nh}", [nh], [t])                          # top B + 1 bits
+    sg.add(f"v_add_u32 {t}, 1, {t}", [t], [t])
+    sg.add(f"v_lshrrev_b32 {t}, 1, {t}", [t], [t])                                  # state = digit
+    sg.add(f"v_sub_u32 {nl}, 0, {t}", [t], [nl])
+    sg.add(f"v_cndmask_b32_e64 {xl}, {t}, {nl}, {c[2]}", [t, nl, c[2]], [xl])
+    sg.add(f"v_ashrrev_i32 {xh}, 31, {xl}", [xl], [xh])
+    m = v[4]
+    sg.add(f"v_and_b32 {m}, -15, {xh}", [xh], [m])
+    xp = pv(int(xl[1:]))
+    sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
+
+
+def rotate_decompose(B, sol=False):
+    """dmap v64..v127 <- decompose(+-acc[(e - a) mod N] - acc[e]); Solinas bodies negate and subtract
+    modulo p (polynomial_wrapping_monic_monomial_mul_assign_custom_mod, then the CMUX difference)."""
     B.raw(f"s_and_b32 s{S_R8}, s{S_AMS}, 0x7ff", f"s_lshl_b32 s{S_R8}, s{S_R8}, 3",
           f"s_lshr_b32 s{S_FULL}, s{S_AMS}, 11", f"s_sub_u32 s{S_FULL}, 0, s{S_FULL}",
           f"v_subrev_u32 v{V_U8}, s{S_R8}, v{VOFF}")
@@ -187,6 +215,18 @@ def rotate_decompose(B):
             sg.add(f"v_add_u32 {m}, {512 * r}, v{V_U8}", [f"v{V_U8}"], [m])
             sg.add(f"v_ashrrev_i32 {m}, 31, {m}", [m], [m])
             sg.add(f"v_xor_b32 {m}, s{S_FULL}, {m}", [m], [m])
+            if sol:
+                # m = -1: p - x (p for x = 0, which later decomposes like 0); then - acc mod p
+                nl, nh = v[6], v[7]
+                sg.add(f"v_sub_co_u32_e64 {nl}, {c[0]}, 1, {xl}", [xl], [nl, c[0]])
+                sg.add(f"v_subb_co_u32_e64 {nh}, {JUNK}, -1, {xh}, {c[0]}", [xh, c[0]], [nh, JUNK])
+                sg.add(f"v_bfi_b32 {xl}, {m}, {nl}, {xl}", [m, nl, xl], [xl])
+                sg.add(f"v_bfi_b32 {xh}, {m}, {nh}, {xh}", [m, nh, xh], [xh])
+                sg.add(f"v_sub_co_u32_e64 {xl}, {c[0]}, {xl}, {al}", [xl, al], [xl, c[0]])
+                sg.add(f"v_subb_co_u32_e64 {xh}, {c[1]}, {xh}, {ah}, {c[0]}", [xh, ah, c[0]], [xh, c[1]])
+                minus_eps(sg, v[5], c[1], pv(int(xl[1:])))
+                decompose_sol(sg, sl, xl, xh)
+                continue
             sg.add(f"v_xor_b32 {xl}, {m}, {xl}", [m, xl], [xl])
             sg.add(f"v_xor_b32 {xh}, {m}, {xh}", [m, xh], [xh])
             sg.add(f"v_sub_co_u32_e64 {xl}, {c[0]}, {xl}, {m}", [xl, m], [xl, c[0]])
@@ -294,12 +334,41 @@ def modswitch_acc(B, dmap):
     sched(B, sg)
 
 
-def gen_pbs(tabs):
+def add_acc_sol(B, dmap):
+    """acc <- acc + y mod p, canonical (both canonical): ntt64.rs:244-266 add_backward, custom modulus."""
+    sg = Seg()
+    sls = B.slots(free_blocks_except(dmap))
+    for r in range(32):
+        sl = sls[r % len(sls)]
+        v, P, c = sl.v, sl.P, sl.c
+        vl, vh, _ = X(dmap, r)
+        al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+        sg.add(f"v_add_co_u32_e64 {v[0]}, {c[0]}, {al}, {vl}", [al, vl], [v[0], c[0]])
+        sg.add(f"v_addc_co_u32_e64 {v[1]}, {c[0]}, {ah}, {vh}, {c[0]}", [ah, vh, c[0]], [v[1], c[0]])
+        sg.add(f"v_mad_u64_u32 {P[1]}, {c[1]}, -1, 1, {P[0]}", [P[0]], [P[1], c[1]])
+        sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
+        sg.add(f"v_cndmask_b32_e64 {al}, {v[0]}, {v[2]}, {c[1]}", [v[0], v[2], c[1]], [al])
+        sg.add(f"v_cndmask_b32_e64 {ah}, {v[1]}, {v[3]}, {c[1]}", [v[1], v[3], c[1]], [ah])
+    sched(B, sg)
+
+
+def gen_pbs(tabs, sol=False):
+    """BNF (sol=False): native ciphertexts, ms computed here from the raw mask, acc from the LUT rows.
+    Solinas (sol=True, ntt64_pbs.rs:213-286): the mask arrives pre-switched (lwe = the switched values,
+    0 skipped), acc starts from the wave's LDS buffer (the wrapper rotated the LUT by -ms(b) there)."""
     B = Body(tabs)
     prologue(B)
-    B.raw(f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]", f"s_mov_b32 s{S_CNT}, %[n]",
-          f"s_mov_b32 s{S_A}, %[lut_lo]", f"s_mov_b32 s{S_A + 1}, %[lut_hi]")
-    B.raw(*load_rows(ACC, S_A), "s_waitcnt vmcnt(0)")    # acc <- LUT polynomial of this wave
+    B.raw(f"s_mov_b32 s{S_LWE}, %[lwe_lo]", f"s_mov_b32 s{S_LWE + 1}, %[lwe_hi]", f"s_mov_b32 s{S_CNT}, %[n]")
+    if sol:
+        B.raw(f"s_mov_b32 s{S_PHALF}, 0x80000001", f"s_mov_b32 s{S_PHALF + 1}, 0x7fffffff")
+        B.raw(*[f"ds_read_b64 {pv(ACC + 2 * r)}, v{V_T4R} offset:{512 * r}" for r in range(32)],
+              "s_waitcnt lgkmcnt(0)")
+    else:
+        B.raw(f"s_mov_b32 s{S_A}, %[lut_lo]", f"s_mov_b32 s{S_A + 1}, %[lut_hi]")
+        B.raw(*load_rows(ACC, S_A), "s_waitcnt vmcnt(0)")    # acc <- LUT polynomial of this wave
+    ms = ([f"s_and_b32 s{S_AMS}, s{S_A}, 0xfff"] if sol else     # pre-switched, in [0, 2N)
+          [f"s_add_u32 s{S_AMS}, s{S_A + 1}, 0x80000",            # ms(a) = (a + 2^51) >> 52 (log_mod 12)
+           f"s_lshr_b32 s{S_AMS}, s{S_AMS}, 20"])
     B.raw("Lpbs_top_%=:",
           f"s_cmp_eq_u32 s{S_CNT}, 0",
           "s_cbranch_scc1 Lpbs_end_%=",
@@ -307,16 +376,18 @@ def gen_pbs(tabs):
           f"s_add_u32 s{S_LWE}, s{S_LWE}, 8", f"s_addc_u32 s{S_LWE + 1}, s{S_LWE + 1}, 0",
           f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
           "s_waitcnt lgkmcnt(0)",
-          f"s_add_u32 s{S_AMS}, s{S_A + 1}, 0x80000",      # ms(a) = (a + 2^51) >> 52 (log_mod 12)
-          f"s_lshr_b32 s{S_AMS}, s{S_AMS}, 20",
+          *ms,
           f"s_cmp_eq_u32 s{S_AMS}, 0",
           "s_cbranch_scc1 Lpbs_skip_%=")
     B.raw(*gload(0), *gload(1))
-    rotate_decompose(B)
+    rotate_decompose(B, sol)
     dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
     mac(B, dmap)
     dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
-    modswitch_acc(B, dmap)
+    if sol:
+        add_acc_sol(B, dmap)
+    else:
+        modswitch_acc(B, dmap)
     B.raw("Lpbs_skip_%=:",
           f"s_add_u32 s{S_GOWN}, s{S_GOWN}, {STEP_BYTES}", f"s_addc_u32 s{S_GOWN + 1}, s{S_GOWN + 1}, 0",
           f"s_add_u32 s{S_GPAR}, s{S_GPAR}, {STEP_BYTES}", f"s_addc_u32 s{S_GPAR + 1}, s{S_GPAR + 1}, 0",
@@ -327,14 +398,18 @@ def gen_pbs(tabs):
     return B
 
 
-def gen_ext(tabs, cmux):
+def gen_ext(tabs, cmux, sol=False):
     """One external product (cmux=False: out += GGSW . glwe) or CMUX (glwe -= out, then
-    out += GGSW . glwe), BNF, level 1; wave w handles polynomial w of one GLWE pair."""
+    out += GGSW . glwe), level 1; wave w handles polynomial w of one GLWE pair.  BNF (native GLWEs, Raw
+    GGSW) or Solinas (sol: GLWEs mod p, Normalize GGSW, ntt64_pbs.rs:553-702)."""
     B = Body(tabs)
     prologue(B)
     S_GL, S_OUT = S_LWE, S_A
-    # the GGSW is the reference's Raw NTT key: N^-1 comes from the third table (untwist * N^-1)
-    B.raw(f"s_add_u32 s{S_TWI}, %[tab_lo], {2 * 2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0")
+    if sol:
+        B.raw(f"s_mov_b32 s{S_PHALF}, 0x80000001", f"s_mov_b32 s{S_PHALF + 1}, 0x7fffffff")
+    else:
+        # the GGSW is the reference's Raw NTT key: N^-1 comes from the third table (untwist * N^-1)
+        B.raw(f"s_add_u32 s{S_TWI}, %[tab_lo], {2 * 2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0")
     B.raw(f"s_mov_b32 s{S_GL}, %[glwe_lo]", f"s_mov_b32 s{S_GL + 1}, %[glwe_hi]",
           f"s_mov_b32 s{S_OUT}, %[out_lo]", f"s_mov_b32 s{S_OUT + 1}, %[out_hi]")
     B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
@@ -343,7 +418,12 @@ def gen_ext(tabs, cmux):
     for r in range(32):
         sl = sls[r % len(sls)]
         xl, xh = f"v{64 + 2 * r}", f"v{65 + 2 * r}"
-        if cmux:  # ct1 -= ct0 (ntt64_bnf_pbs.rs:683-705, wrapping)
+        if cmux and sol:  # ct1 -= ct0 mod p (ntt64_pbs.rs:669-680)
+            al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+            sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[0]}, {xl}, {al}", [xl, al], [xl, sl.c[0]])
+            sg.add(f"v_subb_co_u32_e64 {xh}, {sl.c[1]}, {xh}, {ah}, {sl.c[0]}", [xh, ah, sl.c[0]], [xh, sl.c[1]])
+            minus_eps(sg, sl.v[5], sl.c[1], pv(64 + 2 * r))
+        elif cmux:  # ct1 -= ct0 (ntt64_bnf_pbs.rs:683-705, wrapping)
             al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
             sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[1]}, {xl}, {al}", [xl, al], [xl, sl.c[1]])
             sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {sl.c[1]}", [xh, ah, sl.c[1]], [xh, JUNK])
@@ -352,18 +432,21 @@ def gen_ext(tabs, cmux):
         B.raw(*store_rows(64, S_GL))
     sg = Seg()
     for r in range(32):
-        decompose(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}")
+        (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}")
     sched(B, sg)
     dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
     mac(B, dmap)
     dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
-    modswitch_acc(B, dmap)
+    if sol:
+        add_acc_sol(B, dmap)
+    else:
+        modswitch_acc(B, dmap)
     B.raw(*store_rows(ACC, S_OUT), "s_waitcnt vmcnt(0)")
     return B
 
 
-def emit(name, body):
-    clob = [f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
+def emit(name, body, sgprs=SGPR_CLOBBER):
+    clob = [f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in sgprs] + ['"scc"', '"memory"']
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
             f"#define MI_PBS_BODY_{name.upper()}(...) asm volatile(\\\n" +
             "\\\n".join(f'      "{l}\\n"' for l in body.lines) +
@@ -373,14 +456,21 @@ def emit(name, body):
 def main():
     tabs = T.load_tables()
     b = gen_pbs(tabs)
-    print("// GENERATED by tools/gen_pbs_kernel.py — do not edit.  BNF level-1 blind-rotation loop, external")
-    print("// product and CMUX as asm bodies per wave (pbs_tw.hip).  Own v8..v255, s20..s31 + s36..s93, exec (restored).")
+    print("// GENERATED by tools/gen_pbs_kernel.py — do not edit.  Level-1 blind-rotation loops, external products")
+    print("// and CMUXes (BNF and Solinas) as asm bodies per wave (pbs_tw.hip).  Own v8..v255, s20..s31 + s36..s93")
+    print("// (+ s94..s95 in the Solinas bodies), exec (restored).")
     print("#pragma once")
     print(emit("bnf_l1", b))
     e, c = gen_ext(tabs, False), gen_ext(tabs, True)
     print(emit("ext_bnf_l1", e))
     print(emit("cmux_bnf_l1", c))
-    print(f"// pbs step {b.nvalu} VALU, ext {e.nvalu}, cmux {c.nvalu}", file=sys.stderr)
+    bs = gen_pbs(tabs, sol=True)
+    es, cs = gen_ext(tabs, False, sol=True), gen_ext(tabs, True, sol=True)
+    print(emit("sol_l1", bs, SGPR_CLOBBER_SOL))
+    print(emit("ext_sol_l1", es, SGPR_CLOBBER_SOL))
+    print(emit("cmux_sol_l1", cs, SGPR_CLOBBER_SOL))
+    print(f"// pbs step {b.nvalu} VALU, ext {e.nvalu}, cmux {c.nvalu}; Solinas pbs step {bs.nvalu}, ext {es.nvalu}, "
+          f"cmux {cs.nvalu}", file=sys.stderr)
 
 
 if __name__ == "__main__":
