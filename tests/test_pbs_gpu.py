@@ -181,14 +181,17 @@ def test_pbs_functional_real_keys(engine, plan, ctx, bnf):
 def test_pbs_errors(engine, plan):
     import torch
     M = engine.ntt64_pbs
-    small = engine.Plan.try_new(1024, P)
-    bsk = torch.zeros((4, 1, 2, 2, 1024), dtype=torch.int64, device="cuda")
+    small = engine.Plan.try_new(512, P)
+    bsk = torch.zeros((4, 1, 2, 2, 512), dtype=torch.int64, device="cuda")
     with pytest.raises(engine.MiError) as e:
         M.NttBootstrapKey(small, bsk, 23, 1, M.BNF)
-    assert e.value.status == 6  # MI_ERR_UNSUPPORTED (N != 2048)
+    assert e.value.status == 6  # MI_ERR_UNSUPPORTED (N outside {1024, 2048, 4096})
     with pytest.raises(engine.MiError) as e:
-        M.NttBootstrapKey(plan, torch.zeros((2, 4, 2, 2, N), dtype=torch.int64, device="cuda"), 10, 4, M.BNF)
-    assert e.value.status == 6  # level > 3
+        M.NttBootstrapKey(plan, torch.zeros((2, 1, 4, 4, N), dtype=torch.int64, device="cuda"), 10, 1, M.BNF)
+    assert e.value.status == 6  # k = 3
+    with pytest.raises(engine.MiError) as e:
+        M.NttBootstrapKey(plan, torch.zeros((2, 4, 2, 2, N), dtype=torch.int64, device="cuda"), 16, 4, M.BNF)
+    assert e.value.status == 1  # base_log * level = 64: SignedDecomposer::new's assertion
     bsk = torch.zeros((4, 1, 2, 2, N), dtype=torch.int64, device="cuda")
     with pytest.raises(ValueError):
         M.NttBootstrapKey(plan, bsk, 23, 2, M.BNF)  # shape / level mismatch
@@ -308,3 +311,93 @@ def test_pbs_solinas_config4_shape(engine, plan, ctx, batch):
     for b in range(min(batch, 3)):
         want = ctx.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, bnf=False)
         assert np.array_equal(got[b], want)
+
+
+SHAPES = [(1024, 1), (1024, 2), (2048, 2), (4096, 1), (4096, 2)]
+
+
+@pytest.mark.parametrize("n,k", SHAPES)
+@pytest.mark.parametrize("bnf", [True, False])
+def test_generic_shapes_ext_product_cmux(engine, oracle, n, k, bnf):
+    """External product and CMUX for N in {1024, 4096} and GLWE dimension k = 2 (the reference's
+    shape-generic ntt64_bnf_pbs.rs:541-681 / ntt64_pbs.rs:553-663), levels 1 and 2, vs the oracle."""
+    q = 0 if bnf else P
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    for base_log, level in ((23, 1), (12, 2)):
+        g = H.rng(n + 10 * k + base_log + bnf)
+        batch = 3
+        ggsw = rand_q(g, (level, k + 1, k + 1, n), P)
+        glwe = rand_q(g, (batch, k + 1, n), q)
+        out0 = rand_q(g, (batch, k + 1, n), q)
+        want = np.stack([c.ext_product(out0[b].reshape(-1), ggsw.reshape(-1), glwe[b].reshape(-1), k, base_log,
+                                       level, bnf=bnf).reshape(k + 1, n) for b in range(batch)])
+        out = dev(out0)
+        fn = M.add_external_product_ntt64_bnf_assign if bnf else M.add_external_product_ntt64_assign
+        fn(pl, out, dev(ggsw), dev(glwe), base_log, level)
+        assert np.array_equal(host(out), want), (base_log, level)
+        t0, t1 = dev(out0), dev(glwe)
+        fn = M.cmux_ntt64_bnf_assign if bnf else M.cmux_ntt64_assign
+        fn(pl, t0, t1, dev(ggsw), base_log, level)
+        want0 = np.stack([c.cmux(out0[b].reshape(-1), glwe[b].reshape(-1), ggsw.reshape(-1), k, base_log, level,
+                                 bnf=bnf).reshape(k + 1, n) for b in range(batch)])
+        assert np.array_equal(host(t0), want0)
+
+
+@pytest.mark.parametrize("n,k", SHAPES)
+@pytest.mark.parametrize("bnf", [True, False])
+def test_generic_shapes_pbs(engine, oracle, n, k, bnf):
+    """PBS for N in {1024, 4096}, k = 2, levels 1 / 3 on random keys vs the oracle (incl. the key
+    conversion of the same shape on the GPU)."""
+    q = 0 if bnf else P
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    for base_log, level in ((23, 1), (7, 3)):
+        g = H.rng(7 * n + k + level + bnf)
+        n_lwe, batch = 12, 3
+        bsk = rand_q(g, (n_lwe, level, k + 1, k + 1, n), P)
+        lut = rand_q(g, (k + 1, n), q)
+        lwe = _pbs_inputs(g, batch, n_lwe, q)
+        want = np.stack([c.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), k, base_log, level, bnf=bnf)
+                         for b in range(batch)])
+        key = M.NttBootstrapKey(pl, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
+        out = dev(np.zeros((batch, k * n + 1), np.uint64))
+        fn = (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf
+              else M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)
+        fn(dev(lwe), out, dev(lut), key)
+        assert np.array_equal(host(out), want), (base_log, level)
+    # key conversion of this shape
+    polys = 2 * (k + 1) ** 2
+    src = rand_q(g, (polys, n), 0 if bnf else P)
+    want = c.bsk_to_ntt(src.reshape(-1), 64 if bnf else 0, not bnf).reshape(polys, n)
+    d = dev(np.zeros_like(src))
+    M.convert_standard_lwe_bootstrap_key_to_ntt64(pl, dev(src), d, not bnf, 64 if bnf else None)
+    assert np.array_equal(host(d), want)
+
+
+def test_pbs_functional_k2_real_keys(engine, oracle):
+    """A real-key BNF PBS at GLWE dimension 2, N = 1024: GPU == oracle bit for bit and decrypts to f(m)."""
+    n, k, n_lwe, base_log, level, msg_mod = 1024, 2, 48, 23, 1, 4
+    delta = (1 << 63) // msg_mod
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    g = H.rng(2024)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (k, n))
+    bsk = H.bsk_gen(g, lwe_sk, glwe_sk, base_log, level, 17, 0)
+    nbsk = c.bsk_to_ntt(bsk.reshape(-1), 64, normalize=False).reshape(bsk.shape)
+    f = lambda x: (x + 1) % msg_mod
+    lut = H.pbs_lut(n, k, msg_mod, delta, f, 0)
+    msgs = list(range(msg_mod))
+    lwe = np.stack([H.lwe_encrypt(g, m * delta, lwe_sk, 30, 0) for m in msgs])
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(pl, dev(nbsk), base_log, level, M.BNF)
+    out = dev(np.zeros((len(msgs), k * n + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    out_sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    for i, m in enumerate(msgs):
+        assert np.array_equal(got[i], c.pbs(lwe[i], lut.reshape(-1), nbsk.reshape(-1), k, base_log, level))
+        assert H.decode(H.lwe_decrypt(got[i], out_sk, 0), delta, msg_mod, 0) % msg_mod == f(m)

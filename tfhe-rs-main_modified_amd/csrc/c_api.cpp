@@ -349,9 +349,8 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   if (variant != MI_NTT64_SOLINAS && variant != MI_NTT64_BNF) return fail(MI_ERR_INVALID_ARG, "unknown variant");
   if (level < 1 || base_log < 1 || base_log * level > 63)
     return fail(MI_ERR_INVALID_ARG, "decomposition must satisfy level >= 1, base_log >= 1, base_log*level < 64");
-  if (!plan->goldilocks || plan->n != 2048 || k != 1)
-    return fail(MI_ERR_UNSUPPORTED, "external product / PBS run for the Solinas plan at N = 2048, k = 1");
-  if (level > 3) return fail(MI_ERR_UNSUPPORTED, "decomposition level > 3");
+  if (!plan->goldilocks || plan->logn < 10 || plan->logn > 12 || k < 1 || k > 2)
+    return fail(MI_ERR_UNSUPPORTED, "external product / PBS run for the Solinas plan at N in {1024, 2048, 4096}, k in {1, 2}");
   return MI_OK;
 }
 
@@ -359,9 +358,9 @@ extern "C" {
 
 // the twisted-transform bodies (pbs_tw.hip) cover level 1, base_log <= 31 (BNF and Solinas) on the
 // Solinas N = 2048 plan; every other shape runs the generic kernels (pbs_kernels.hip)
-static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int base_log, int level) {
+static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level) {
   (void)variant;
-  return level == 1 && base_log <= 31 && plan->twisted;
+  return k == 1 && level == 1 && base_log <= 31 && plan->twisted;
 }
 
 int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
@@ -370,10 +369,11 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
   if (n_polys == 0) return MI_OK;
   if (!bsk_std || !bsk_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (in_modulus_width > 64) return fail(MI_ERR_INVALID_ARG, "in_modulus_width > 64");
-  if (!plan->goldilocks || plan->n != 2048) return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N = 2048");
+  if (!plan->goldilocks || plan->logn < 10 || plan->logn > 12)
+    return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {1024, 2048, 4096}");
   if (n_polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "too many polynomials");
   DeviceGuard g(plan->device);
-  hipError_t e = mi::launch_bsk_to_ntt(bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0, plan->n_inv,
+  hipError_t e = mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0, plan->n_inv,
                                        plan->d_twid, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
 }
@@ -387,12 +387,12 @@ int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, co
   if (!out_glwe || !in_glwe || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
-  if (twisted_ext_applies(plan, variant, base_log, level)) {
+  if (twisted_ext_applies(plan, variant, k, base_log, level)) {
     hipError_t e = mi::launch_ext_tw(false, variant == MI_NTT64_SOLINAS, out_glwe, const_cast<uint64_t*>(in_glwe),
                                      ggsw_ntt, batch, base_log, plan->d_twist_f, (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
   }
-  hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
+  hipError_t e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
                                         ggsw_ntt, batch, base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv,
                                         (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
@@ -406,12 +406,12 @@ int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1,
   if (!ct0 || !ct1 || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
-  if (twisted_ext_applies(plan, variant, base_log, level)) {
+  if (twisted_ext_applies(plan, variant, k, base_log, level)) {
     hipError_t e = mi::launch_ext_tw(true, variant == MI_NTT64_SOLINAS, ct0, ct1, ggsw_ntt, batch, base_log,
                                      plan->d_twist_f, (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
   }
-  hipError_t e = mi::launch_ext_product(variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
+  hipError_t e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
                                         plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
 }
@@ -486,7 +486,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   const mi_ntt64_plan* plan = key->plan;
   const hipStream_t s = (hipStream_t)stream;
   DeviceGuard g(plan->device);
-  if (key->variant == MI_NTT64_SOLINAS && twisted_ext_applies(plan, key->variant, key->base_log, key->level)) {
+  if (key->variant == MI_NTT64_SOLINAS && twisted_ext_applies(plan, key->variant, key->k, key->base_log, key->level)) {
     // Solinas on the twisted engine: the body reads switched values (the caller's, or switched here
     // into stream-ordered scratch by ms_non_native)
     const size_t count = batch * (key->n_lwe + 1);
@@ -510,7 +510,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
     const size_t count = batch * (key->n_lwe + 1);
     if (hipMallocAsync((void**)&lifted, count * sizeof(u64), s) != hipSuccess)
       return fail(MI_ERR_OOM, "scratch allocation failed");
-    hipError_t e = mi::launch_lift_switched(lifted, lwe_in, count, key->variant == MI_NTT64_BNF, s);
+    hipError_t e = mi::launch_lift_switched(lifted, lwe_in, count, key->variant == MI_NTT64_BNF, plan->logn, s);
     if (e != hipSuccess) {
       (void)hipFreeAsync(lifted, s);
       return hip_fail(e, "lift launch");
@@ -519,11 +519,11 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
     ms_mode = MI_MS_STANDARD;
   }
   hipError_t e;
-  if (twisted_ext_applies(plan, key->variant, key->base_log, key->level))
+  if (twisted_ext_applies(plan, key->variant, key->k, key->base_log, key->level))
     e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
                           ms_mode == MI_MS_CENTERED, s);
   else
-    e = mi::launch_pbs(key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
+    e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
                        key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);
   if (lifted) (void)hipFreeAsync(lifted, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");

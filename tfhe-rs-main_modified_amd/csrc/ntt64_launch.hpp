@@ -50,16 +50,17 @@ hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint6
 
 namespace mi {
 
-// pbs_kernels.hip — Goldilocks, N = 2048, k = 1 only (callers validate the shape).
-hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, hipStream_t s);
-hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
-                             uint64_t n_inv, const uint64_t* tw, hipStream_t s);
+// pbs_kernels.hip — Goldilocks, N = 2^logn for logn in {10, 11, 12}, GLWE dimension k in {1, 2}, any level
+// count (callers validate the shape; other shapes return hipErrorInvalidValue).
+hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s);
+hipError_t launch_bsk_to_ntt(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
+                             int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s);
 hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s);
 // cmux: glwe -= out first (written back), then out += GGSW (.) glwe
-hipError_t launch_ext_product(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
-                              size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
-                              hipStream_t s);
-hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
+                              const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
+                              const uint64_t* itw, uint64_t n_inv, hipStream_t s);
+hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s);
 // BNF, level 1, base_log <= 31, on the twisted transform; tab = plan twist tables [fwd | inverse]

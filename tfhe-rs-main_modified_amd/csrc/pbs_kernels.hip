@@ -4,14 +4,17 @@
 //   BNF     : native 2^64 ciphertexts, back-and-forth modulus switch to the Goldilocks prime
 //             (algorithms/lwe_programmable_bootstrapping/ntt64_bnf_pbs.rs:208-726)
 //   SOLINAS : ciphertexts modulo the prime (algorithms/lwe_programmable_bootstrapping/ntt64_pbs.rs:213-702)
+// for every shape the twisted engine (pbs_tw.hip: N = 2048, k = 1, level 1) does not cover: polynomial
+// sizes N = 2^LOGN (1024, 2048, 4096), GLWE dimension k = K (1, 2), any decomposition level count
+// (a runtime loop), as the reference's shape-generic code (ntt64_bnf_pbs.rs:541-681, ntt64_pbs.rs:553-663).
 //
-// MI355X design: one workgroup (256 lanes) owns one ciphertext for the WHOLE blind rotation.  The
-// GLWE accumulator (k+1 = 2 polynomials of N = 2048) lives in VGPRs across all n CMUX steps, so the
-// only per-step global traffic is the step's NTT GGSW (64 KiB, shared by every workgroup of the
-// launch, hence L2/MALL-resident: all workgroups walk the key in the same order).  Each step
-// rotates through LDS, decomposes in registers, runs 2 forward + 2 inverse NTTs with the register
-// window engine of ntt64_regs.hpp, multiply-accumulates against the GGSW in the NTT domain and
-// switches the result back — the reference's ~10 host-side passes per CMUX fused into one loop body.
+// MI355X design: one workgroup (T = N / 8 lanes) owns one ciphertext for the WHOLE blind rotation.  The
+// GLWE accumulator (k+1 polynomials) lives in VGPRs across all n CMUX steps, so the only per-step global
+// traffic is the step's NTT GGSW (shared by every workgroup of the launch, hence L2/MALL-resident: all
+// workgroups walk the key in the same order).  Each step rotates through LDS, decomposes in registers,
+// runs (k+1) forward + (k+1) inverse NTTs per level with the register-window engine of ntt64_regs.hpp,
+// multiply-accumulates against the GGSW in the NTT domain and switches the result back — the
+// reference's host-side passes per CMUX fused into one loop body.
 //
 // Bit-exactness: every step restates the reference arithmetic exactly; the only reordering is the
 // BNF N^{-1} normalisation, which is folded into a private copy of the key (exact: Goldilocks
@@ -26,13 +29,19 @@
 namespace mi {
 namespace pbs {
 
-using G = Geo<11, 3>;  // N = 2048, 8 coefficients per lane, 256 lanes
-static constexpr int N = G::N;
-static constexpr int T = G::T;
-static constexpr int E = G::E;
 static constexpr u64 P = GL_P;
-static constexpr int LO_COL = G::LOGN - G::LOGE;          // column layout e = r * T + t
-static constexpr int LO_NTT = win_lo<G, true>(G::NWIN - 1);  // forward exit / inverse entry layout
+static constexpr int LOGE = 3;  // 8 coefficients per lane
+
+template <int LOGN>
+struct Shape {
+  using G = Geo<LOGN, LOGE>;
+  static constexpr int N = G::N;
+  static constexpr int T = G::T;  // lanes per polynomial = workgroup size
+  static constexpr int E = G::E;
+  static constexpr int LO_COL = G::LOGN - G::LOGE;                  // column layout e = r * T + t
+  static constexpr int LO_NTT = win_lo<G, true>(G::NWIN - 1);       // forward exit / inverse entry layout
+  static constexpr unsigned LOG_MOD = LOGN + 1;  // PolynomialSize::to_blind_rotation_input_modulus_log
+};
 
 // ---- scalar helpers (each restates one reference function) ----------------------------------
 
@@ -85,9 +94,9 @@ __device__ __forceinline__ u64 modulus_switch(u64 input, unsigned log_modulus) {
 }
 
 // ntt64_pbs.rs:540-549 + algorithms/misc.rs:6-18 divide_round
-__device__ __forceinline__ u64 ms_non_native(u64 input) {
-  const unsigned __int128 num = ((unsigned __int128)input) << (G::LOGN + 1);
-  // num / p with the 2^64 = p + EPS split (num < 2^76)
+__device__ __forceinline__ u64 ms_non_native(u64 input, unsigned log_mod) {
+  const unsigned __int128 num = ((unsigned __int128)input) << log_mod;
+  // num / p with the 2^64 = p + EPS split (num < 2^(64 + log_mod))
   const u64 nh = (u64)(num >> 64), nl = (u64)num;
   unsigned __int128 r = (unsigned __int128)nh * GL_EPS + nl;  // num = nh*p + r
   u64 q = nh;
@@ -103,73 +112,87 @@ template <bool BNF>
 __device__ __forceinline__ u64 neg_q(u64 a) { return BNF ? (u64)0 - a : neg_custom(a); }
 
 // ---- one external product on registers ------------------------------------------------------
-// in: ct1[2][E] (column layout, the GLWE to decompose); out: y[2][E] (column layout, the GLWE
-// contribution out += GGSW (.) ct1 in the ciphertext domain).  `ggsw` = LEVELS x 2 x 2 x N (NTT
-// domain, highest level first); BNF keys are expected pre-normalised unless `normalize`.
-template <bool BNF, int LEVELS>
-__device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[2][E], u64 (&y)[2][E], const u64* __restrict__ ggsw,
-                                                 int base_log, int t, u64* sh, const u64* __restrict__ tw,
-                                                 const u64* __restrict__ itw, bool normalize, u64 n_inv) {
+// in: ct1[K+1][E] (column layout, the GLWE to decompose); out: y[K+1][E] (column layout, the GLWE
+// contribution out += GGSW (.) ct1 in the ciphertext domain).  `ggsw` = level x (K+1) x (K+1) x N (NTT
+// domain, highest level first; row r = the decomposition of GLWE polynomial r); BNF keys are expected
+// pre-normalised unless `normalize`.  The decomposition levels are a runtime loop.
+template <int LOGN, int K, bool BNF>
+__device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<LOGN>::E],
+                                                 u64 (&y)[K + 1][Shape<LOGN>::E], const u64* __restrict__ ggsw,
+                                                 int base_log, int level, int t, u64* sh,
+                                                 const u64* __restrict__ tw, const u64* __restrict__ itw,
+                                                 bool normalize, u64 n_inv) {
+  using S = Shape<LOGN>;
+  using G = typename S::G;
+  constexpr int E = S::E, N = S::N;
   const Goldilocks gl;
-  u64 state[2][E];
-  unsigned char sign[2][E];
-  (void)sign;
+  u64 state[K + 1][E];
+  bool sign[K + 1][E];
   if (BNF) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
-      for (int r = 0; r < E; ++r) state[c][r] = decomp_init_native(ct1[c][r], base_log, LEVELS);
+      for (int r = 0; r < E; ++r) {
+        state[c][r] = decomp_init_native(ct1[c][r], base_log, level);
+        sign[c][r] = false;
+      }
   } else {
     // iter.rs:623-670 TensorSignedDecompositionLendingIterNonNative::new (q = p: ceil_log2 = 64)
-    const unsigned shift = 64u - (unsigned)(base_log * LEVELS);
+    const unsigned shift = 64u - (unsigned)(base_log * level);
     const u64 half = P / 2 + 1;  // div_ceil(2)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) {
         const u64 x = ct1[c][r];
         const bool s = x >= half;
-        state[c][r] = closest_abs_nonnative(s ? P - x : x, base_log, LEVELS) >> shift;
+        state[c][r] = closest_abs_nonnative(s ? P - x : x, base_log, level) >> shift;
         sign[c][r] = s;
       }
   }
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c <= K; ++c)
 #pragma unroll
     for (int r = 0; r < E; ++r) y[c][r] = 0;
 
+#pragma unroll 1
+  for (int li = 0; li < level; ++li) {
+    u64 x[K + 1][E];
 #pragma unroll
-  for (int li = 0; li < LEVELS; ++li) {
-    u64 x[2][E];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) {
         u64 term = decompose_one_level(base_log, state[c][r]);
         if (!BNF && sign[c][r]) term = (u64)0 - term;  // iter.rs:722-731
         x[c][r] = ((int64_t)term < 0) ? term + P : term;  // ntt64.rs:231-238 / iter.rs:724-730
       }
-    ntt_regs<G, true, 2>(x, t, sh, tw, gl);
-    const u64* mat = ggsw + (size_t)li * 4 * N;
+    ntt_regs<G, true, K + 1>(x, t, sh, tw, gl);
+    // the iterator yields DecompositionLevel(level_count) first (the least significant digit), the
+    // GGSW stores that level first too (ggsw_encryption.rs:318-375): GGSW block li pairs with term li
+    const u64* mat = ggsw + (size_t)li * (K + 1) * (K + 1) * N;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      const int pos = elem<G>(t, r, LO_NTT);
-      const u64 g00 = mat[0 * N + pos], g01 = mat[1 * N + pos], g10 = mat[2 * N + pos], g11 = mat[3 * N + pos];
-      // update_with_fmadd (ntt64_pbs.rs:683-702 / ntt64_bnf_pbs.rs:707-726): row r' times column c
-      y[0][r] = gl.add(y[0][r], gl.add(gl.mul(x[0][r], g00), gl.mul(x[1][r], g10)));
-      y[1][r] = gl.add(y[1][r], gl.add(gl.mul(x[0][r], g01), gl.mul(x[1][r], g11)));
+      const int pos = elem<G>(t, r, S::LO_NTT);
+      // update_with_fmadd (ntt64_pbs.rs:683-702 / ntt64_bnf_pbs.rs:707-726): row rr times column c
+#pragma unroll
+      for (int c = 0; c <= K; ++c) {
+        u64 acc = y[c][r];
+#pragma unroll
+        for (int rr = 0; rr <= K; ++rr) acc = gl.add(acc, gl.mul(x[rr][r], mat[(rr * (K + 1) + c) * N + pos]));
+        y[c][r] = acc;
+      }
     }
   }
   if (BNF && normalize) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) y[c][r] = gl.mul(y[c][r], n_inv);
   }
-  ntt_regs<G, false, 2>(y, t, sh, itw, gl);
+  ntt_regs<G, false, K + 1>(y, t, sh, itw, gl);
   if (BNF) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) y[c][r] = modswitch_prime_to_native(y[c][r]);
   }
@@ -178,23 +201,27 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[2][E], u64 (&y
 // ---- external product / CMUX batch (config 3) ----------------------------------------------------
 // EXT : out[b] += GGSW (.) glwe[b]                          (add_external_product_ntt64[_bnf]_assign)
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
-template <bool BNF, int LEVELS, bool CMUX>
-__global__ __launch_bounds__(256) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
-                                                          const u64* __restrict__ ggsw, uint32_t batch, int base_log,
-                                                          const u64* __restrict__ tw, const u64* __restrict__ itw,
-                                                          u64 n_inv) {
-  __shared__ u64 sh[2 * G::PADDED];
+template <int LOGN, int K, bool BNF, bool CMUX>
+__global__ __launch_bounds__(Shape<LOGN>::T) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                                     const u64* __restrict__ ggsw, uint32_t batch,
+                                                                     int base_log, int level,
+                                                                     const u64* __restrict__ tw,
+                                                                     const u64* __restrict__ itw, u64 n_inv) {
+  using S = Shape<LOGN>;
+  using G = typename S::G;
+  constexpr int E = S::E, N = S::N;
+  __shared__ u64 sh[(K + 1) * G::PADDED];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;  // uniform per workgroup
-  u64* in = glwe + (size_t)b * 2 * N;
-  u64* o = out + (size_t)b * 2 * N;
-  u64 ct[2][E], y[2][E], acc[2][E];
+  u64* in = glwe + (size_t)b * (K + 1) * N;
+  u64* o = out + (size_t)b * (K + 1) * N;
+  u64 ct[K + 1][E], y[K + 1][E], acc[K + 1][E];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c <= K; ++c)
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      const int e = c * N + elem<G>(t, r, LO_COL);
+      const int e = c * N + elem<G>(t, r, S::LO_COL);
       ct[c][r] = in[e];
       acc[c][r] = o[e];
       if (CMUX) {  // ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705: ct1 -= ct0
@@ -202,20 +229,20 @@ __global__ __launch_bounds__(256) void ext_product_kernel(u64* __restrict__ out,
         in[e] = ct[c][r];
       }
     }
-  ext_product_regs<BNF, LEVELS>(ct, y, ggsw, base_log, t, sh, tw, itw, true, n_inv);
+  ext_product_regs<LOGN, K, BNF>(ct, y, ggsw, base_log, level, t, sh, tw, itw, true, n_inv);
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c <= K; ++c)
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      const int e = c * N + elem<G>(t, r, LO_COL);
+      const int e = c * N + elem<G>(t, r, S::LO_COL);
       o[e] = BNF ? acc[c][r] + y[c][r] : add_custom(acc[c][r], y[c][r]);  // ntt64.rs:110-137 / 244-266
     }
 }
 
 // algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the
 // workgroup (uses sh[0 .. 2T) and leaves it free again).
-__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int t,
-                                        u64* sh) {
+template <int T>
+__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int t, u64* sh) {
   u64 sum_half = 0;
   int64_t sum_hed = 0;
   for (uint32_t i = t; i < n_lwe; i += T) {
@@ -244,44 +271,47 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
 }
 
 // ---- programmable bootstrap batch (configs 4/5) -----------------------------------------------
-// lwe_in: batch x (n+1); lut: 2 x N shared; bsk: n x LEVELS x 2 x 2 x N (BNF: pre-normalised copy);
-// lwe_out: batch x (N+1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
-template <bool BNF, int LEVELS>
-__global__ __launch_bounds__(256) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
-                                                  const u64* __restrict__ lut, const u64* __restrict__ bsk,
-                                                  uint32_t n_lwe, uint32_t batch, int base_log,
-                                                  const u64* __restrict__ tw, const u64* __restrict__ itw,
-                                                  int centered) {
-  __shared__ u64 sh[2 * G::PADDED];
+// lwe_in: batch x (n+1); lut: (K+1) x N shared; bsk: n x level x (K+1) x (K+1) x N (BNF: pre-normalised
+// copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
+template <int LOGN, int K, bool BNF>
+__global__ __launch_bounds__(Shape<LOGN>::T) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+                                                             const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                             uint32_t n_lwe, uint32_t batch, int base_log, int level,
+                                                             const u64* __restrict__ tw, const u64* __restrict__ itw,
+                                                             int centered) {
+  using S = Shape<LOGN>;
+  using G = typename S::G;
+  constexpr int E = S::E, N = S::N, T = S::T;
+  __shared__ u64 sh[(K + 1) * G::PADDED];
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
-  const size_t ggsw_len = (size_t)LEVELS * 4 * N;
-  const unsigned log_mod = G::LOGN + 1;  // PolynomialSize::to_blind_rotation_input_modulus_log
+  const size_t ggsw_len = (size_t)level * (K + 1) * (K + 1) * N;
+  const unsigned log_mod = S::LOG_MOD;
 
   u64 body_corr = 0;
-  if (BNF && centered) body_corr = centered_body_correction(lwe, n_lwe, log_mod, t, sh);
+  if (BNF && centered) body_corr = centered_body_correction<T>(lwe, n_lwe, log_mod, t, sh);
 
-  u64 acc[2][E];
+  u64 acc[K + 1][E];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c <= K; ++c)
 #pragma unroll
-    for (int r = 0; r < E; ++r) acc[c][r] = lut[c * N + elem<G>(t, r, LO_COL)];
+    for (int r = 0; r < E; ++r) acc[c][r] = lut[c * N + elem<G>(t, r, S::LO_COL)];
 
   if (!BNF) {  // ntt64_pbs.rs:237-249: rotate the LUT by -ms(b) first (custom modulus)
-    const u64 body = ms_non_native(lwe[n_lwe]);
+    const u64 body = ms_non_native(lwe[n_lwe], log_mod);
     const int full = (int)(body / N) & 1, rem = (int)(body % N);
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
-      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, S::LO_COL)] = acc[c][r];
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) {
-        const int m = elem<G>(t, r, LO_COL);  // div_assign: new[m] = old[(m + rem) % N], neg for m >= N - rem
+        const int m = elem<G>(t, r, S::LO_COL);  // div_assign: new[m] = old[(m + rem) % N], neg for m >= N - rem
         u64 v = sh[c * N + ((m + rem) & (N - 1))];
         if (full ^ (m >= N - rem)) v = neg_custom(v);
         acc[c][r] = v;
@@ -297,38 +327,38 @@ __global__ __launch_bounds__(256) void pbs_kernel(u64* __restrict__ lwe_out, con
       if (a == 0) continue;  // ntt64_bnf_pbs.rs:241
     } else {
       if (a_raw == 0) continue;  // ntt64_pbs.rs:257
-      a = ms_non_native(a_raw);
+      a = ms_non_native(a_raw, log_mod);
     }
     const int full = (int)(a / N) & 1, rem = (int)(a % N);
     // ct1 = acc * X^a (polynomial_wrapping_monic_monomial_mul_assign[_custom_mod]) ; ct1 -= acc
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
-      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+      for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, S::LO_COL)] = acc[c][r];
     __syncthreads();
-    u64 ct1[2][E], y[2][E];
+    u64 ct1[K + 1][E], y[K + 1][E];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) {
-        const int e = elem<G>(t, r, LO_COL);  // mul_assign: new[e] = old[(e - rem) % N], neg for e < rem
+        const int e = elem<G>(t, r, S::LO_COL);  // mul_assign: new[e] = old[(e - rem) % N], neg for e < rem
         u64 v = sh[c * N + ((e - rem) & (N - 1))];
         if (full ^ (e < rem)) v = neg_q<BNF>(v);
         ct1[c][r] = BNF ? v - acc[c][r] : sub_custom(v, acc[c][r]);  // cmux: ct1 - ct0
       }
     __syncthreads();
-    ext_product_regs<BNF, LEVELS>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, t, sh, tw, itw, false, 0);
+    ext_product_regs<LOGN, K, BNF>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, level, t, sh, tw, itw, false, 0);
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) acc[c][r] = BNF ? acc[c][r] + y[c][r] : add_custom(acc[c][r], y[c][r]);
   }
 
   // BNF: final rotation by -ms(b) (ntt64_bnf_pbs.rs:262-270); then sample extract (nth = 0)
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+  for (int c = 0; c <= K; ++c)
 #pragma unroll
-    for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, LO_COL)] = acc[c][r];
+    for (int r = 0; r < E; ++r) sh[c * N + elem<G>(t, r, S::LO_COL)] = acc[c][r];
   __syncthreads();
   int full = 0, rem = 0;
   if (BNF) {
@@ -336,29 +366,35 @@ __global__ __launch_bounds__(256) void pbs_kernel(u64* __restrict__ lwe_out, con
     full = (int)(body / N) & 1;
     rem = (int)(body % N);
   }
-  // rotated[c][m] = sign * acc[c][(m + rem) % N]
-  u64* out = lwe_out + (size_t)b * (N + 1);
+  // rotated[c][m] = sign * acc[c][(m + rem) % N]; glwe_sample_extraction.rs:89-160: mask polynomial c
+  // gives out[c N + 0] = A_c[0], out[c N + j] = -A_c[N - j]; the body coefficient 0 gives out[K N]
+  u64* out = lwe_out + (size_t)b * (K * N + 1);
 #pragma unroll
-  for (int r = 0; r < E; ++r) {
-    const int j = elem<G>(t, r, LO_COL);
-    // glwe_sample_extraction.rs:89-160: out[0] = A[0], out[j] = -A[N - j]
-    const int m = (j == 0) ? 0 : N - j;
-    u64 v = sh[(m + rem) & (N - 1)];
-    if (full ^ (m >= N - rem)) v = neg_q<BNF>(v);
-    out[j] = (j == 0) ? v : neg_q<BNF>(v);
-  }
+  for (int c = 0; c < K; ++c)
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int j = elem<G>(t, r, S::LO_COL);
+      const int m = (j == 0) ? 0 : N - j;
+      u64 v = sh[c * N + ((m + rem) & (N - 1))];
+      if (full ^ (m >= N - rem)) v = neg_q<BNF>(v);
+      out[c * N + j] = (j == 0) ? v : neg_q<BNF>(v);
+    }
   if (t == 0) {
-    u64 v = sh[N + (rem & (N - 1))];
+    u64 v = sh[K * N + (rem & (N - 1))];
     if (full ^ (0 >= N - rem)) v = neg_q<BNF>(v);
-    out[N] = v;
+    out[K * N] = v;
   }
 }
 
 // ---- key conversion (lwe_bootstrap_key_conversion.rs:294-365) + normalisation ---------------------
 // bsk_ntt[pi] = fwd(modswitch_{2^w -> p}(bsk_std[pi])) [* N^-1]; also used to prepare the BNF copy.
-__global__ __launch_bounds__(256) void bsk_to_ntt_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
-                                                         uint64_t n_polys, unsigned in_width, int normalize,
-                                                         u64 n_inv, const u64* __restrict__ tw) {
+template <int LOGN>
+__global__ __launch_bounds__(Shape<LOGN>::T) void bsk_to_ntt_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
+                                                                    uint64_t n_polys, unsigned in_width, int normalize,
+                                                                    u64 n_inv, const u64* __restrict__ tw) {
+  using S = Shape<LOGN>;
+  using G = typename S::G;
+  constexpr int E = S::E, N = S::N;
   __shared__ u64 sh[G::PADDED];
   const Goldilocks gl;
   const int t = threadIdx.x;
@@ -367,7 +403,7 @@ __global__ __launch_bounds__(256) void bsk_to_ntt_kernel(u64* __restrict__ dst, 
   u64 x[1][E];
 #pragma unroll
   for (int r = 0; r < E; ++r) {
-    u64 v = src[pi * N + elem<G>(t, r, LO_COL)];
+    u64 v = src[pi * N + elem<G>(t, r, S::LO_COL)];
     if (in_width) {  // ntt64.rs:166-178
       const unsigned __int128 w = ((unsigned __int128)(v >> (64u - in_width))) * P + ((unsigned __int128)1 << (in_width - 1));
       v = (u64)(w >> in_width);
@@ -379,7 +415,7 @@ __global__ __launch_bounds__(256) void bsk_to_ntt_kernel(u64* __restrict__ dst, 
   for (int r = 0; r < E; ++r) {
     u64 v = x[0][r];
     if (normalize) v = gl.mul(v, n_inv);
-    dst[pi * N + elem<G>(t, r, LO_NTT)] = v;
+    dst[pi * N + elem<G>(t, r, S::LO_NTT)] = v;
   }
 }
 
@@ -391,33 +427,48 @@ __global__ __launch_bounds__(256) void scale_kernel(u64* __restrict__ dst, const
 }
 
 // PRE_SWITCHED inputs: lift each switched value v in [0, 2N) to a representative whose standard
-// switch is v again — BNF: v << 52 ((v 2^52 + 2^51) >> 52 = v); Solinas: round(v p / 2N), whose
-// ms_non_native is v (the rounding error is < 2N / p) and which is 0 iff v is 0 (same skip).
+// switch is v again — BNF: v << (64 - log 2N) ((v 2^s + 2^(s-1)) >> s = v); Solinas: round(v p / 2N),
+// whose ms_non_native is v (the rounding error is < 2N / p) and which is 0 iff v is 0 (same skip).
 __global__ __launch_bounds__(256) void lift_switched_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
-                                                            uint64_t count, int bnf) {
+                                                            uint64_t count, int bnf, unsigned log2n) {
+  const u64 n2 = 1ull << log2n;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
-    const u64 v = src[i] & (2 * N - 1);
-    dst[i] = bnf ? v << (64 - (G::LOGN + 1)) : (u64)(((unsigned __int128)v * P + N) >> (G::LOGN + 1));
+    const u64 v = src[i] & (n2 - 1);
+    dst[i] = bnf ? v << (64 - log2n) : (u64)(((unsigned __int128)v * P + (n2 >> 1)) >> log2n);
   }
 }
 
 }  // namespace pbs
 
-hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, hipStream_t s) {
+// ---- dispatch ------------------------------------------------------------------------------------
+// Shapes compiled: N = 2^LOGN for LOGN in {10, 11, 12}, K in {1, 2}; callers validate (c_api.cpp).
+
+hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s) {
   if (count == 0) return hipSuccess;
   uint64_t blocks = (count + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pbs::lift_switched_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, (uint64_t)count,
-                     bnf ? 1 : 0);
+                     bnf ? 1 : 0, (unsigned)(logn + 1));
   return hipGetLastError();
 }
 
-hipError_t launch_bsk_to_ntt(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
+template <int LOGN>
+static hipError_t bsk_launch(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
                              uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
-  if (n_polys == 0) return hipSuccess;
-  hipLaunchKernelGGL(pbs::bsk_to_ntt_kernel, dim3((unsigned)n_polys), dim3(256), 0, s, dst, src, (uint64_t)n_polys,
-                     in_width, normalize, n_inv, tw);
+  hipLaunchKernelGGL((pbs::bsk_to_ntt_kernel<LOGN>), dim3((unsigned)n_polys), dim3(pbs::Shape<LOGN>::T), 0, s, dst, src,
+                     (uint64_t)n_polys, in_width, normalize, n_inv, tw);
   return hipGetLastError();
+}
+
+hipError_t launch_bsk_to_ntt(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
+                             int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
+  if (n_polys == 0) return hipSuccess;
+  switch (logn) {
+    case 10: return bsk_launch<10>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
+    case 11: return bsk_launch<11>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
+    case 12: return bsk_launch<12>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s) {
@@ -428,50 +479,63 @@ hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64
   return hipGetLastError();
 }
 
-template <bool BNF, bool CMUX>
-static hipError_t ext_dispatch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
-                               int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
-  const dim3 grid((unsigned)batch), block(256);
-  switch (level) {
-    case 1: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 1, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
-    case 2: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 2, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
-    case 3: hipLaunchKernelGGL((pbs::ext_product_kernel<BNF, 3, CMUX>), grid, block, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tw, itw, n_inv); break;
-    default: return hipErrorInvalidValue;
-  }
+template <int LOGN, int K, bool BNF, bool CMUX>
+static hipError_t ext_launch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
+                             int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
+  hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX>), dim3((unsigned)batch), dim3(pbs::Shape<LOGN>::T), 0,
+                     s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw, n_inv);
   return hipGetLastError();
 }
 
-hipError_t launch_ext_product(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
-                              size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
-                              hipStream_t s) {
+template <int LOGN, int K>
+static hipError_t ext_shape(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
+                            size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
+                            hipStream_t s) {
+  if (bnf)
+    return cmux ? ext_launch<LOGN, K, true, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
+                : ext_launch<LOGN, K, true, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+  return cmux ? ext_launch<LOGN, K, false, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
+              : ext_launch<LOGN, K, false, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+}
+
+hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
+                              const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
+                              const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
   if (batch == 0) return hipSuccess;
-  if (cmux)
-    return bnf ? ext_dispatch<true, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
-               : ext_dispatch<false, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
-  return bnf ? ext_dispatch<true, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
-             : ext_dispatch<false, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+#define MI_EXT_SHAPE(L, KK)                                                                      \
+  if (logn == L && k == KK)                                                                      \
+    return ext_shape<L, KK>(bnf, cmux, level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+  MI_EXT_SHAPE(10, 1) MI_EXT_SHAPE(10, 2) MI_EXT_SHAPE(11, 1) MI_EXT_SHAPE(11, 2) MI_EXT_SHAPE(12, 1)
+  MI_EXT_SHAPE(12, 2)
+#undef MI_EXT_SHAPE
+  return hipErrorInvalidValue;
 }
 
-template <bool BNF>
-static hipError_t pbs_dispatch(int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
-                               const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
-                               const uint64_t* itw, int centered, hipStream_t s) {
-  const dim3 grid((unsigned)batch), block(256);
-  switch (level) {
-    case 1: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 1>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
-    case 2: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 2>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
-    case 3: hipLaunchKernelGGL((pbs::pbs_kernel<BNF, 3>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, (uint32_t)batch, base_log, tw, itw, centered); break;
-    default: return hipErrorInvalidValue;
-  }
+template <int LOGN, int K>
+static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+                            const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
+                            const uint64_t* itw, int centered, hipStream_t s) {
+  const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN>::T);
+  if (bnf)
+    hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, true>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe,
+                       (uint32_t)batch, base_log, level, tw, itw, centered);
+  else
+    hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, false>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe,
+                       (uint32_t)batch, base_log, level, tw, itw, centered);
   return hipGetLastError();
 }
 
-hipError_t launch_pbs(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s) {
   if (batch == 0) return hipSuccess;
-  return bnf ? pbs_dispatch<true>(level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s)
-             : pbs_dispatch<false>(level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s);
+#define MI_PBS_SHAPE(L, KK)                                                                                     \
+  if (logn == L && k == KK)                                                                                     \
+    return pbs_shape<L, KK>(bnf, level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s);
+  MI_PBS_SHAPE(10, 1) MI_PBS_SHAPE(10, 2) MI_PBS_SHAPE(11, 1) MI_PBS_SHAPE(11, 2) MI_PBS_SHAPE(12, 1)
+  MI_PBS_SHAPE(12, 2)
+#undef MI_PBS_SHAPE
+  return hipErrorInvalidValue;
 }
 
 }  // namespace mi

@@ -75,7 +75,9 @@ def convert_standard_lwe_bootstrap_key_to_ntt64(plan, input_bsk, output_bsk, nor
 
 def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux):
     n = plan.ntt_size()
-    k = 1
+    if out.dim() < 2:
+        raise ValueError(f"assertion failed: out shape {tuple(out.shape)} != (..., k + 1, {n})")
+    k = int(out.shape[-2]) - 1  # the GLWE dimension follows the operands (GlweSize = k + 1)
     b = _glwe_batch(out, k, n, "out")
     if glwe.shape != out.shape:
         raise ValueError(f"assertion failed: glwe shape {tuple(glwe.shape)} != out shape {tuple(out.shape)}")
@@ -107,16 +109,16 @@ def cmux_ntt64_bnf_assign(plan, ct0, ct1, ggsw, base_log: int, level: int) -> No
 class NttBootstrapKey:
     """An NTT-domain bootstrap key bound to a plan (``mi_pbs_ntt64_key``).
 
-    ``bsk`` is the device tensor (n_lwe, level, k+1, k+1, N) produced by
+    ``bsk`` is the device tensor (n_lwe, level, k+1, k+1, N) (k = the GLWE dimension) produced by
     ``convert_standard_lwe_bootstrap_key_to_ntt64``: Raw for ``BNF`` (a private copy with N^-1
     folded in is made once, on the tensor's current stream), Normalize for ``SOLINAS`` (referenced;
     keep the tensor alive)."""
 
     def __init__(self, plan, bsk, base_log: int, level: int, variant: int = BNF):
         n = plan.ntt_size()
-        k = 1
+        k = int(bsk.shape[2]) - 1 if bsk.dim() == 5 else 1
         if bsk.dim() != 5 or tuple(bsk.shape[1:]) != (level, k + 1, k + 1, n):
-            raise ValueError(f"assertion failed: bsk shape {tuple(bsk.shape)} != (n_lwe, {level}, 2, 2, {n})")
+            raise ValueError(f"assertion failed: bsk shape {tuple(bsk.shape)} != (n_lwe, {level}, k + 1, k + 1, {n})")
         self._bind(plan, bsk, int(bsk.shape[0]), k, base_log, level, variant)
         h = ctypes.c_void_p()
         check(lib().mi_pbs_ntt64_key_create(plan.handle, _dev(bsk, "bsk"), self.input_lwe_dimension, k, base_log,
