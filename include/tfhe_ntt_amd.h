@@ -91,8 +91,10 @@ int mi_fill_uniform(uint64_t *buf, size_t count, uint64_t seed, uint64_t p, int 
 
 /* ---- External product / CMUX / PBS (core_crypto consumers of the plan) -------------------
  * Reference paths below are relative to /root/reference/tfhe/src/core_crypto.  These run for the
- * Solinas plan (p = 2^64 - 2^32 + 1) at N = 2048, GLWE dimension k = 1, 1 <= level <= 3; other
- * shapes return MI_ERR_UNSUPPORTED.  Layouts are the reference's entity layouts, contiguous:
+ * Solinas plan (p = 2^64 - 2^32 + 1) at N in {1024, 2048, 4096}, GLWE dimension k in {1, 2}, any
+ * decomposition with base_log * level < 64; other plans / shapes return MI_ERR_UNSUPPORTED (the
+ * N = 2048, k = 1 shapes run on the hand-scheduled engine, the rest on the generic kernels).
+ * Layouts are the reference's entity layouts, contiguous:
  *   GLWE       : (k+1) polynomials of N u64 (mask then body)
  *   GGSW (NTT) : level-major, highest level first; per level (k+1) rows x (k+1) columns of N u64,
  *                each polynomial in the plan's forward (bit-reversed) NTT order
