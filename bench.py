@@ -335,6 +335,69 @@ def bench_ext_product(args, eng, torch, dev, world, barrier):
             "algorithmic_bytes_per_unit": 32768 + 65536}
 
 
+def bench_bsk_conversion(args, eng, torch, dev, world, barrier):
+    """convert_standard_lwe_bootstrap_key_to_ntt64 (lwe_bootstrap_key_conversion.rs:294-365) of one whole
+    PARAM_MESSAGE_2_CARRY_2 key per step: 918 GGSWs x (k+1)^2 x level = 3,672 polynomials, native 2^64
+    input modswitched to p, forward NTT, Raw (BNF) output; standard and NTT keys resident in HBM."""
+    M = eng.ntt64_pbs
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    shape = (PBS_N_LWE, PBS_LEVEL, 2, 2, N)
+    std = torch.empty(shape, dtype=torch.int64, device=dev)
+    eng.fill_uniform(std, SEED + 70, 0)
+    ntt = torch.empty_like(std)
+    run = lambda: M.convert_standard_lwe_bootstrap_key_to_ntt64(plan, std, ntt, normalize=False)
+    run()
+    torch.cuda.synchronize()
+    K = max(20, args.steps // 20)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(K):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / K
+    polys = std.numel() // N
+    alg = polys * N * 16  # read the standard key, write the NTT key
+    return {"metric": "bootstrap keys converted to the NTT domain per second", "value": world * K / el,
+            "unit": "keys/s", "ms_per_step": el / K * 1e3, "kernel_ms": ms, "steps": K,
+            "polys_per_key": polys, "ntt_per_s": world * K * polys / el,
+            "config": {"workload": "convert_standard_lwe_bootstrap_key_to_ntt64, native 2^64 -> p, Raw, "
+                                   "n=918 k=1 N=2048 level=1 (PARAM_MESSAGE_2_CARRY_2)", "batch_per_gpu": 1},
+            "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": alg}}
+
+
+def cpu_baseline_bsk(seconds: float):
+    """Oracle restatement of the sequential conversion (one thread, as the reference's non-par function),
+    with the AVX-512 transform restatement where the host has it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    ctx = O.NttContext(N)
+    polys = PBS_N_LWE * PBS_LEVEL * 4
+    O.pbs_set_fast_ntt(True)
+    try:
+        std = O.fill_uniform(SEED + 70, 0, polys * N)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ctx.bsk_to_ntt(std, 64, False)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        O.pbs_set_fast_ntt(False)
+    return {"value": reps / el, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} whole keys ({polys} polys) in {el:.1f}s, restatement of "
+                      f"convert_standard_lwe_bootstrap_key_to_ntt64 "
+                      f"({'AVX-512' if O.have_avx512() else 'scalar'} transforms), 1 thread"}
+
+
 KS_IN, KS_BASE_LOG, KS_LEVEL = 2048, 4, 4  # PARAM_MESSAGE_2_CARRY_2 keyswitch (ks_pbs.rs:38-39): k*N -> n
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: i8 MFMA = 2x the dense bf16 rate (~2.5 PF)
 
@@ -598,11 +661,13 @@ def main():
         out["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
         out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
+        out["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_pbs:
             out["pbs"]["cpu_baseline"] = cpu_baseline_pbs(min(args.cpu_seconds, 10.0))
             out["keyswitch"]["cpu_baseline"] = cpu_baseline_ks(min(args.cpu_seconds, 5.0))
+            out["bsk_conversion"]["cpu_baseline"] = cpu_baseline_bsk(min(args.cpu_seconds, 3.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -46,7 +46,7 @@ def main():
                 merged[k][c] = sum(v) / len(v)
     summary = {}
     for k, cs in merged.items():
-        if not any(t in k for t in ("ntt_window_kernel", "ntt_gl", "ntt_tw", "pbs_kernel", "pbs_tw_kernel", "ext_tw_kernel", "ext_product",
+        if not any(t in k for t in ("ntt_window_kernel", "ntt_gl", "ntt_tw", "pbs_kernel", "pbs_tw_kernel", "pbs_tw_sol_kernel", "ext_tw_kernel", "bsk_to_ntt", "ext_product",
                                     "ks_gemm_kernel", "ks_digits_kernel")):
             continue
         if "ntt" in k and grids.get(k, 0) < 8192 * 64:  # only the full-batch launches
