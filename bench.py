@@ -438,7 +438,7 @@ def bench_keyswitch(args, eng, torch, dev, world, barrier):
                        "batch_per_gpu": batch},
             "roofline": {"bound": "mfma", "achieved": ops / (ms * 1e-3) / 1e12, "peak": I8_PEAK_TOPS,
                          "unit": "TOP/s", "frac": ops / (ms * 1e-3) / 1e12 / I8_PEAK_TOPS,
-                         "note": "digit pass + i8 MFMA GEMM (8 byte planes) per step"}}
+                         "note": "digit pass + i8 MFMA GEMM per step; counts all 8 recoded byte-plane MACs per u64 MAC, so this is matrix-core utilisation: the useful u64 work is 1/8 of it"}}
 
 
 def bench_ks_pbs(args, eng, torch, dev, world, barrier):

@@ -292,6 +292,58 @@ def test_pbs_solinas_reference_params(engine, plan, ctx, oracle):
     assert np.array_equal(got[:4], want)
 
 
+def _fast_bsk_native(g, lwe_sk, glwe_sk, base_log, noise_log2):
+    """H.bsk_gen for native 2^64 ciphertexts, k = 1, level 1, with every GGSW row's mask product computed in
+    one vectorised pass (ggsw_encryption.rs:20-45 summands).  Test infrastructure only."""
+    n_lwe, n = lwe_sk.size, glwe_sk.shape[1]
+    masks = H.uniform_u64(g, (n_lwe * 2, n))
+    prod = H.negacyclic_mul_binary(masks, glwe_sk[0]).reshape(n_lwe, 2, n)
+    factor = ((-(lwe_sk.astype(object)) * (1 << (64 - base_log))) % 2**64).astype(np.uint64)  # -b * 2^(64-B)
+    pt = np.zeros((n_lwe, 2, n), np.uint64)
+    with np.errstate(over="ignore"):
+        pt[:, 0] = factor[:, None] * glwe_sk[0][None, :]
+        pt[:, 1, 0] = np.uint64(0) - factor
+        body = prod + pt + H.noise_q(g, (n_lwe, 2, n), noise_log2)
+    bsk = np.zeros((n_lwe, 1, 2, 2, n), np.uint64)
+    bsk[:, 0, :, 0] = masks.reshape(n_lwe, 2, n)
+    bsk[:, 0, :, 1] = body
+    return bsk
+
+
+def test_pbs_config4_full_batch_real_keys(engine, plan, ctx):
+    """Config 4 at its full size: 4096 BNF PBS at the PARAM_MESSAGE_2_CARRY_2 shape (n = 918, N = 2048,
+    B = 2^23, l = 1, 2+2-bit messages with padding, TUniform noise bounds 2^45 LWE / 2^17 GLWE as ks_pbs.rs:29-47)
+    under real keys, key converted on the GPU.  Size-independent property over the whole batch: every output
+    decrypts to f(m) (lwe_programmable_bootstrapping.rs:1002-1163); bit-exact vs the oracle on 64 ciphertexts
+    spread over the batch (first, last and every 64th)."""
+    n_lwe, base_log, level, msg_mod, batch = 918, 23, 1, 16, 4096
+    delta = (1 << 63) // msg_mod
+    g = H.rng(4096918)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (K, N))
+    bsk = _fast_bsk_native(g, lwe_sk, glwe_sk, base_log, 17)
+    f = lambda x: (5 * x + 3) % msg_mod
+    lut = H.pbs_lut(N, K, msg_mod, delta, f)
+    msgs = np.arange(batch) % msg_mod
+    lwe = H.lwe_encrypt_batch(g, (msgs.astype(np.uint64) * np.uint64(delta)), lwe_sk, 45)
+    M = engine.ntt64_pbs
+    gkey = dev(np.zeros_like(bsk))
+    M.convert_standard_lwe_bootstrap_key_to_ntt64(plan, dev(bsk), gkey, normalize=False, input_modulus_width=64)
+    nbsk = host(gkey)
+    assert np.array_equal(nbsk[:3].reshape(-1), ctx.bsk_to_ntt(bsk[:3].reshape(-1), 64, normalize=False))
+    key = M.NttBootstrapKey(plan, gkey, base_log, level, M.BNF)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    pts = H.lwe_decrypt_batch(got, H.glwe_sk_as_lwe_sk(glwe_sk))
+    with np.errstate(over="ignore"):
+        dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
+    assert np.array_equal(dec, np.array([f(int(m)) for m in msgs], np.uint64))
+    idx = np.unique(np.concatenate([np.arange(0, batch, 64), [batch - 1]]))
+    want = ctx.pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, threads=16)
+    assert np.array_equal(got[idx], want)
+
+
 @pytest.mark.parametrize("batch", [1, 37])
 def test_pbs_solinas_config4_shape(engine, plan, ctx, batch):
     """Solinas-modulus PBS at the PARAM_MESSAGE_2_CARRY_2 shape (n = 918, B = 2^23, l = 1) on a random key
