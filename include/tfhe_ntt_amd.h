@@ -228,6 +228,54 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu *m, const mi_pbs_ntt64_key *const *keys,
                            const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
                            void *stream);
 
+/* ---- f64-FFT PBS (the default shortint PBS path) ----------------------------
+ * Reference paths relative to /root/reference/tfhe/src/core_crypto.  The negacyclic f64 FFT of
+ * fft_impl/fft64/math/fft/mod.rs (Twisties :58-76, forward_as_torus / forward_as_integer / backward_as_torus
+ * :406-511): N real u64 coefficients -> N/2 complex values x[n] + i x[n + N/2], twisted by exp(i pi n / N),
+ * transformed with an N/2-point DFT (exp(-2 pi i / (N/2)) kernel).  Fourier buffers hold interleaved
+ * (re, im) doubles, N/2 complex per polynomial, in this engine's order: position p holds frequency
+ * freq[p] (mi_fft64_fourier_order).  The reference's tfhe-fft "unordered" order is implementation defined,
+ * so Fourier keys are converted by this engine for this engine.  Results are f64 computations: parity with
+ * the reference is decryption-exact and within the FFT error bound, not bit-exact.  This build: N = 2048,
+ * GLWE dimension k in {1, 2}, any decomposition with base_log * level < 64. */
+typedef struct mi_fft64_plan mi_fft64_plan;
+/* Fft::new (fft_impl/fft64/math/fft/mod.rs:170-223): MI_ERR_INVALID_ARG if n is not a power of two,
+ * MI_ERR_UNSUPPORTED for sizes this build does not compile.  _cached: one plan per (n, device), kept until
+ * process exit as the reference's PLANS map (destroy is a no-op on it). */
+int mi_fft64_plan_create(size_t n, int device, mi_fft64_plan **out_plan);
+int mi_fft64_plan_cached(size_t n, int device, const mi_fft64_plan **out_plan);
+int mi_fft64_plan_destroy(mi_fft64_plan *plan);
+int mi_fft64_plan_info(const mi_fft64_plan *plan, size_t *n, int *device);
+/* freq[p] for p < n/2: the DFT frequency stored at Fourier position p (host call) */
+int mi_fft64_fourier_order(const mi_fft64_plan *plan, uint32_t *freq);
+/* FftView::forward_as_torus / backward_as_torus (add != 0: add_backward_as_torus), per polynomial over a
+ * batch of contiguous polynomials (device pointers, async): fourier = batch x n/2 x 2 doubles. */
+int mi_fft64_forward_torus_batch(const mi_fft64_plan *plan, double *fourier, const uint64_t *standard, size_t batch,
+                                 void *stream);
+int mi_fft64_backward_torus_batch(const mi_fft64_plan *plan, uint64_t *standard, const double *fourier, size_t batch,
+                                  int add, void *stream);
+/* convert_standard_lwe_bootstrap_key_to_fourier (algorithms/lwe_bootstrap_key_conversion.rs:20-43): every
+ * polynomial of the standard key (n_polys = n_lwe (k+1)^2 level) through forward_as_torus. */
+int mi_bsk_to_fourier64(const mi_fft64_plan *plan, const uint64_t *bsk_std, double *bsk_fourier, size_t n_polys,
+                        void *stream);
+/* add_external_product_assign / cmux_assign (algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330,
+ * 510-560; fft_impl/fft64/crypto/ggsw.rs:483-603): native 2^64 GLWEs, one shared Fourier GGSW (level x (k+1)
+ * x (k+1) x n/2 complex, highest level first).  CMUX leaves ct1 holding ct1 - ct0, as the reference. */
+int mi_fft64_ext_product_batch(const mi_fft64_plan *plan, uint64_t *out_glwe, const uint64_t *in_glwe,
+                               const double *ggsw_fourier, int k, int base_log, int level, size_t batch, void *stream);
+int mi_fft64_cmux_batch(const mi_fft64_plan *plan, uint64_t *ct0, uint64_t *ct1, const double *ggsw_fourier, int k,
+                        int base_log, int level, size_t batch, void *stream);
+/* A Fourier bootstrap key (FourierLweBootstrapKey, referenced: the caller keeps `fbsk` alive) and the batched
+ * programmable_bootstrap_lwe_ciphertext (fft64_pbs.rs:924-1060; blind rotation fft_impl/fft64/crypto/
+ * bootstrap.rs:294-381, 481-521).  ms_mode as mi_pbs_ntt64_batch. */
+typedef struct mi_fft64_pbs_key mi_fft64_pbs_key;
+int mi_fft64_pbs_key_create(const mi_fft64_plan *plan, const double *fbsk, size_t n_lwe, int k, int base_log,
+                            int level, mi_fft64_pbs_key **out_key);
+int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key *key);
+int mi_fft64_pbs_key_info(const mi_fft64_pbs_key *key, size_t *n_lwe, int *k, int *base_log, int *level);
+int mi_fft64_pbs_batch(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
+                       size_t batch, int ms_mode, void *stream);
+
 /* ---- prime32::Plan (tfhe-ntt/src/prime32.rs:632-1025) ----------------------------------------
  * The same negacyclic transform and pointwise ops on u32 buffers for a prime p < 2^32.  try_new
  * (prime32.rs:662-671) returns None for N < 32, N not a power of two, p not prime, no 2N-th root:

@@ -292,24 +292,6 @@ def test_pbs_solinas_reference_params(engine, plan, ctx, oracle):
     assert np.array_equal(got[:4], want)
 
 
-def _fast_bsk_native(g, lwe_sk, glwe_sk, base_log, noise_log2):
-    """H.bsk_gen for native 2^64 ciphertexts, k = 1, level 1, with every GGSW row's mask product computed in
-    one vectorised pass (ggsw_encryption.rs:20-45 summands).  Test infrastructure only."""
-    n_lwe, n = lwe_sk.size, glwe_sk.shape[1]
-    masks = H.uniform_u64(g, (n_lwe * 2, n))
-    prod = H.negacyclic_mul_binary(masks, glwe_sk[0]).reshape(n_lwe, 2, n)
-    factor = ((-(lwe_sk.astype(object)) * (1 << (64 - base_log))) % 2**64).astype(np.uint64)  # -b * 2^(64-B)
-    pt = np.zeros((n_lwe, 2, n), np.uint64)
-    with np.errstate(over="ignore"):
-        pt[:, 0] = factor[:, None] * glwe_sk[0][None, :]
-        pt[:, 1, 0] = np.uint64(0) - factor
-        body = prod + pt + H.noise_q(g, (n_lwe, 2, n), noise_log2)
-    bsk = np.zeros((n_lwe, 1, 2, 2, n), np.uint64)
-    bsk[:, 0, :, 0] = masks.reshape(n_lwe, 2, n)
-    bsk[:, 0, :, 1] = body
-    return bsk
-
-
 def test_pbs_config4_full_batch_real_keys(engine, plan, ctx):
     """Config 4 at its full size: 4096 BNF PBS at the PARAM_MESSAGE_2_CARRY_2 shape (n = 918, N = 2048,
     B = 2^23, l = 1, 2+2-bit messages with padding, TUniform noise bounds 2^45 LWE / 2^17 GLWE as ks_pbs.rs:29-47)
@@ -321,7 +303,7 @@ def test_pbs_config4_full_batch_real_keys(engine, plan, ctx):
     g = H.rng(4096918)
     lwe_sk = H.binary_key(g, n_lwe)
     glwe_sk = H.binary_key(g, (K, N))
-    bsk = _fast_bsk_native(g, lwe_sk, glwe_sk, base_log, 17)
+    bsk = H.bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, 17)
     f = lambda x: (5 * x + 3) % msg_mod
     lut = H.pbs_lut(N, K, msg_mod, delta, f)
     msgs = np.arange(batch) % msg_mod

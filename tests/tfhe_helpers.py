@@ -185,3 +185,21 @@ def ksk_gen(g, in_sk, out_sk, base_log, level, noise_log2):
 def lwe_decrypt_batch(cts, lwe_sk):
     with np.errstate(over="ignore"):
         return cts[..., -1] - (cts[..., :-1] * lwe_sk).sum(axis=-1, dtype=np.uint64)
+
+
+def bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, noise_log2):
+    """bsk_gen for native 2^64 ciphertexts, k = 1, level 1, with every GGSW row's mask product computed in
+    one vectorised pass (ggsw_encryption.rs:20-45 summands).  Test infrastructure only."""
+    n_lwe, n = lwe_sk.size, glwe_sk.shape[1]
+    masks = uniform_u64(g, (n_lwe * 2, n))
+    prod = negacyclic_mul_binary(masks, glwe_sk[0]).reshape(n_lwe, 2, n)
+    factor = ((-(lwe_sk.astype(object)) * (1 << (64 - base_log))) % 2**64).astype(np.uint64)  # -b * 2^(64-B)
+    pt = np.zeros((n_lwe, 2, n), np.uint64)
+    with np.errstate(over="ignore"):
+        pt[:, 0] = factor[:, None] * glwe_sk[0][None, :]
+        pt[:, 1, 0] = np.uint64(0) - factor
+        body = prod + pt + noise_q(g, (n_lwe, 2, n), noise_log2)
+    bsk = np.zeros((n_lwe, 1, 2, 2, n), np.uint64)
+    bsk[:, 0, :, 0] = masks.reshape(n_lwe, 2, n)
+    bsk[:, 0, :, 1] = body
+    return bsk

@@ -1,0 +1,258 @@
+// c_api_fft.cpp — C ABI of the f64-FFT PBS path (mi_fft64_*), the default shortint PBS of tfhe core_crypto
+// (SURVEY.md §8f rank 4).  Reference paths relative to /root/reference/tfhe/src/core_crypto:
+//   Fft::new + Twisties       fft_impl/fft64/math/fft/mod.rs:58-76, 104-224 (one plan per polynomial size)
+//   forward/backward_as_torus fft_impl/fft64/math/fft/mod.rs:406-511
+//   key conversion            algorithms/lwe_bootstrap_key_conversion.rs:20-150
+//   external product / CMUX   algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330, 510-560
+//   PBS                       algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:924-1060
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "c_api_internal.hpp"
+#include "fft64_launch.hpp"
+
+using namespace mi::capi;
+
+struct mi_fft64_plan {
+  size_t n = 0;
+  int device = 0;
+  bool cached = false;
+  double* d_tables = nullptr;  // t1 (2048) | t2 (128) | cm (32) | cmi (32) doubles
+  mi::FftTables tables{};
+};
+
+struct mi_fft64_pbs_key {
+  const mi_fft64_plan* plan = nullptr;
+  const double* fbsk = nullptr;  // caller-owned Fourier key
+  size_t n_lwe = 0;
+  int k = 1, base_log = 0, level = 0;
+};
+
+namespace {
+
+constexpr size_t FFT_N = 2048, FFT_M = 1024;
+constexpr size_t OFF_T2 = 2 * 1024, OFF_CM = OFF_T2 + 2 * 64, OFF_CMI = OFF_CM + 2 * 16, TABLE_DOUBLES = OFF_CMI + 2 * 16;
+
+// exp(i pi e / 2048) for an integer exponent (reduced exactly mod 4096 first), in long double
+void unit_root(long e, double* re, double* im) {
+  e %= 4096;
+  if (e < 0) e += 4096;
+  const long double a = 3.14159265358979323846264338327950288L * (long double)e / 2048.0L;
+  *re = (double)cosl(a);
+  *im = (double)sinl(a);
+}
+
+std::vector<double> host_tables() {
+  std::vector<double> h(TABLE_DOUBLES);
+  // t1[k1][j] = w^j omega^(j k1) = exp(i pi (j - 4 j k1) / 2048)
+  for (int k1 = 0; k1 < 16; ++k1)
+    for (int j = 0; j < 64; ++j) unit_root((long)j - 4L * j * k1, &h[2 * (k1 * 64 + j)], &h[2 * (k1 * 64 + j) + 1]);
+  // t2[j1][k2] = nu^(j1 k2) = exp(-2 pi i j1 k2 / 64) = exp(i pi (-64 j1 k2) / 2048)
+  for (int j1 = 0; j1 < 4; ++j1)
+    for (int k2 = 0; k2 < 16; ++k2)
+      unit_root(-64L * j1 * k2, &h[OFF_T2 + 2 * (j1 * 16 + k2)], &h[OFF_T2 + 2 * (j1 * 16 + k2) + 1]);
+  for (int m = 0; m < 16; ++m) {
+    unit_root(64L * m, &h[OFF_CM + 2 * m], &h[OFF_CM + 2 * m + 1]);  // exp(i pi m / 32)
+    double re, im;
+    unit_root(-64L * m, &re, &im);
+    h[OFF_CMI + 2 * m] = re / (double)FFT_M;  // exact: M is a power of two
+    h[OFF_CMI + 2 * m + 1] = im / (double)FFT_M;
+  }
+  return h;
+}
+
+int make_plan(size_t n, int device, mi_fft64_plan** out) {
+  if (n != FFT_N) return fail(MI_ERR_UNSUPPORTED, "this build runs the f64-FFT path for N = 2048");
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return fail(MI_ERR_INVALID_ARG, "device index out of range");
+  DeviceGuard g(device);
+  if (!g.ok) return fail(MI_ERR_HIP, "hipSetDevice failed");
+  auto* p = new (std::nothrow) mi_fft64_plan;
+  if (!p) return fail(MI_ERR_OOM, "host allocation failed");
+  p->n = n;
+  p->device = device;
+  const std::vector<double> h = host_tables();
+  hipError_t e = hipMalloc(&p->d_tables, h.size() * sizeof(double));
+  if (e != hipSuccess) {
+    delete p;
+    return fail(MI_ERR_OOM, "device allocation failed");
+  }
+  e = hipMemcpy(p->d_tables, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(p->d_tables);
+    delete p;
+    return hip_fail(e, "table upload");
+  }
+  p->tables = {p->d_tables, p->d_tables + OFF_T2, p->d_tables + OFF_CM, p->d_tables + OFF_CMI};
+  *out = p;
+  return MI_OK;
+}
+
+int check_shape(const mi_fft64_plan* plan, int k, int base_log, int level) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (level < 1 || base_log < 1 || base_log * level > 63)
+    return fail(MI_ERR_INVALID_ARG, "decomposition must satisfy level >= 1, base_log >= 1, base_log*level < 64");
+  if (k < 1 || k > 2) return fail(MI_ERR_UNSUPPORTED, "the f64-FFT external product / PBS run for k in {1, 2}");
+  return MI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mi_fft64_plan_create(size_t n, int device, mi_fft64_plan** out_plan) {
+  if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
+  *out_plan = nullptr;
+  if (n < 2 || (n & (n - 1))) return fail(MI_ERR_INVALID_ARG, "polynomial size must be a power of two");
+  return make_plan(n, device, out_plan);
+}
+
+int mi_fft64_plan_cached(size_t n, int device, const mi_fft64_plan** out_plan) {
+  if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
+  *out_plan = nullptr;
+  static std::mutex mu;
+  static std::map<std::pair<size_t, int>, mi_fft64_plan*> plans;  // lives until process exit (as PLANS)
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = plans.find({n, device});
+  if (it != plans.end()) {
+    *out_plan = it->second;
+    return MI_OK;
+  }
+  mi_fft64_plan* p = nullptr;
+  const int st = mi_fft64_plan_create(n, device, &p);
+  if (st != MI_OK) return st;
+  p->cached = true;
+  plans[{n, device}] = p;
+  *out_plan = p;
+  return MI_OK;
+}
+
+int mi_fft64_plan_destroy(mi_fft64_plan* plan) {
+  if (!plan || plan->cached) return MI_OK;
+  DeviceGuard g(plan->device);
+  (void)hipFree(plan->d_tables);
+  delete plan;
+  return MI_OK;
+}
+
+int mi_fft64_plan_info(const mi_fft64_plan* plan, size_t* n, int* device) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (n) *n = plan->n;
+  if (device) *device = plan->device;
+  return MI_OK;
+}
+
+int mi_fft64_fourier_order(const mi_fft64_plan* plan, uint32_t* freq) {
+  if (!plan || !freq) return fail(MI_ERR_INVALID_ARG, "NULL argument");
+  for (int r = 0; r < 16; ++r)
+    for (int l = 0; l < 64; ++l) freq[r * 64 + l] = mi::fft64_frequency(r, l);
+  return MI_OK;
+}
+
+int mi_fft64_forward_torus_batch(const mi_fft64_plan* plan, double* fourier, const uint64_t* standard, size_t batch,
+                                 void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (batch == 0) return MI_OK;
+  if (!fourier || !standard) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  const hipError_t e = mi::launch_fft64_fwd_torus(fourier, standard, batch, plan->tables, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 forward launch");
+}
+
+int mi_fft64_backward_torus_batch(const mi_fft64_plan* plan, uint64_t* standard, const double* fourier, size_t batch,
+                                  int add, void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (batch == 0) return MI_OK;
+  if (!fourier || !standard) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  const hipError_t e =
+      mi::launch_fft64_bwd_torus(standard, fourier, batch, add != 0, plan->tables, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 backward launch");
+}
+
+int mi_bsk_to_fourier64(const mi_fft64_plan* plan, const uint64_t* bsk_std, double* bsk_fourier, size_t n_polys,
+                        void* stream) {
+  return mi_fft64_forward_torus_batch(plan, bsk_fourier, bsk_std, n_polys, stream);
+}
+
+int mi_fft64_ext_product_batch(const mi_fft64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
+                               const double* ggsw_fourier, int k, int base_log, int level, size_t batch, void* stream) {
+  int st = check_shape(plan, k, base_log, level);
+  if (st != MI_OK) return st;
+  if (batch == 0) return MI_OK;
+  if (!out_glwe || !in_glwe || !ggsw_fourier) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  const hipError_t e = mi::launch_fft64_ext_product(k, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_fourier,
+                                                    batch, base_log, level, plan->tables, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 external product launch");
+}
+
+int mi_fft64_cmux_batch(const mi_fft64_plan* plan, uint64_t* ct0, uint64_t* ct1, const double* ggsw_fourier, int k,
+                        int base_log, int level, size_t batch, void* stream) {
+  int st = check_shape(plan, k, base_log, level);
+  if (st != MI_OK) return st;
+  if (batch == 0) return MI_OK;
+  if (!ct0 || !ct1 || !ggsw_fourier) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(plan->device);
+  const hipError_t e = mi::launch_fft64_ext_product(k, true, ct0, ct1, ggsw_fourier, batch, base_log, level,
+                                                    plan->tables, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 cmux launch");
+}
+
+int mi_fft64_pbs_key_create(const mi_fft64_plan* plan, const double* fbsk, size_t n_lwe, int k, int base_log,
+                            int level, mi_fft64_pbs_key** out_key) {
+  if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
+  *out_key = nullptr;
+  int st = check_shape(plan, k, base_log, level);
+  if (st != MI_OK) return st;
+  if (n_lwe == 0 || n_lwe > 0xFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "n_lwe out of range");
+  if (!fbsk) return fail(MI_ERR_INVALID_ARG, "bsk is NULL");
+  auto* key = new (std::nothrow) mi_fft64_pbs_key;
+  if (!key) return fail(MI_ERR_OOM, "host allocation failed");
+  key->plan = plan;
+  key->fbsk = fbsk;
+  key->n_lwe = n_lwe;
+  key->k = k;
+  key->base_log = base_log;
+  key->level = level;
+  *out_key = key;
+  return MI_OK;
+}
+
+int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key* key) {
+  delete key;
+  return MI_OK;
+}
+
+int mi_fft64_pbs_key_info(const mi_fft64_pbs_key* key, size_t* n_lwe, int* k, int* base_log, int* level) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (n_lwe) *n_lwe = key->n_lwe;
+  if (k) *k = key->k;
+  if (base_log) *base_log = key->base_log;
+  if (level) *level = key->level;
+  return MI_OK;
+}
+
+int mi_fft64_pbs_batch(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
+                       size_t batch, int ms_mode, void* stream) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (ms_mode < MI_MS_STANDARD || ms_mode > MI_MS_PRE_SWITCHED) return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
+  if (batch == 0) return MI_OK;
+  if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  DeviceGuard g(key->plan->device);
+  const hipError_t e = mi::launch_fft64_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
+                                            key->level, ms_mode, key->plan->tables, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 pbs launch");
+}
+
+}  // extern "C"

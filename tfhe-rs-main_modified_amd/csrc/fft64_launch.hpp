@@ -1,0 +1,37 @@
+// fft64_launch.hpp — host-side launchers of the f64-FFT PBS kernels (fft64_pbs.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mi {
+
+// Device twiddle tables of an N = 2048 plan (complex values as interleaved re, im doubles):
+//   t1  [16][64]  w^j omega^(j k1), w = exp(i pi / 2M), omega = exp(-2 pi i / M), M = 1024
+//   t2  [4][16]   nu^(j1 k2), nu = exp(-2 pi i / 64)
+//   cm  [16]      exp(i pi m / 32)
+//   cmi [16]      exp(-i pi m / 32) / M
+struct FftTables {
+  const double* t1;
+  const double* t2;
+  const double* cm;
+  const double* cmi;
+};
+
+hipError_t launch_fft64_fwd_torus(double* fourier, const uint64_t* std_, size_t batch, const FftTables& t,
+                                  hipStream_t s);
+hipError_t launch_fft64_bwd_torus(uint64_t* std_, const double* fourier, size_t batch, bool add, const FftTables& t,
+                                  hipStream_t s);
+hipError_t launch_fft64_ext_product(int k, bool cmux, uint64_t* out, uint64_t* glwe, const double* ggsw, size_t batch,
+                                    int base_log, int level, const FftTables& t, hipStream_t s);
+hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftTables& t,
+                            hipStream_t s);
+
+// position (register r, lane l) of the Fourier layout -> frequency index (see fft64_pbs.hip)
+inline uint32_t fft64_frequency(int r, int l) {
+  const int k1 = l >> 2, c = l & 3, g = r >> 2, k3 = r & 3;
+  return (uint32_t)(256 * k3 + 16 * (4 * c + g) + k1);
+}
+
+}  // namespace mi

@@ -1,0 +1,633 @@
+// fft64_pbs.hip — the f64-FFT programmable bootstrap of tfhe core_crypto (the default shortint PBS path)
+// on MI355X.  Reference paths relative to /root/reference/tfhe/src/core_crypto:
+//   negacyclic FFT          fft_impl/fft64/math/fft/mod.rs:30-76 (Twisties), 227-356 (conversions),
+//                           524-586 (forward_with_conv / backward_with_conv)
+//   external product        fft_impl/fft64/crypto/ggsw.rs:483-603 (+ update_with_fmadd :617-698)
+//   blind rotate / PBS      fft_impl/fft64/crypto/bootstrap.rs:294-381, 481-521
+//   key conversion          fft_impl/fft64/crypto/bootstrap.rs:199-225 (forward_as_torus per polynomial)
+//
+// The transform: a real negacyclic polynomial of N = 2048 u64 coefficients is folded into M = 1024 complex
+// values u[n] = x[n] + i x[n + M] (forward_with_conv's split), twisted by w^n = exp(i pi n / 2M)
+// (Twisties::new(M)), and transformed with an M-point complex DFT (exp(-2 pi i / M) kernel).  The reference
+// runs tfhe-fft's measured "unordered" plan, whose Fourier-domain order is implementation defined; here the
+// order is this engine's own (documented below, exported by mi_fft64_fourier_order), and keys converted by this
+// engine are read by this engine only.  Results are f64 computations, not bit-identical to the reference's
+// (parity is decryption + an error bound against a numpy restatement).
+//
+// MI355X mapping: one wave per polynomial, 16 complex values per lane in VGPRs (lane j holds u[j + 64 m],
+// m < 16), M = 16 x 64 split into three radix passes:
+//   pass 1  in-lane DFT16 over m, then twiddle T1[k1][j] = w^j omega^(j k1) (twist factor w^j folded in;
+//           the per-m part of the twist, exp(i pi m / 32), is applied before the DFT16)
+//   LDS transpose 1 (row stride 68 complex: conflict-free ds_write_b128 / ds_read_b128)
+//   pass 2  lane 4 k1 + j1 holds the 16 values j = j1 + 4 j2: DFT16 over j2, twiddle nu^(j1 k2) (nu = omega^16)
+//   LDS transpose 2 (slot 16 L + (k2 ^ (4 (L & 3) + ((L >> 2) & 3))): conflict-free both ways)
+//   pass 3  lane 4 k1 + c holds (g, j1) for k2 = 4 c + g: DFT4 over j1 -> k3
+// Fourier position (lane 4 k1 + c, register 4 g + k3) holds frequency 256 k3 + 16 (4 c + g) + k1.  The inverse
+// runs the passes backwards with conjugate twiddles.  All f64 arithmetic is FMA-contracted by hand where the
+// reference's pulp kernels use mul_add.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fft64_launch.hpp"
+
+namespace mi {
+namespace fft {
+
+using u64 = uint64_t;
+
+struct __align__(16) cplx {
+  double re, im;
+};
+
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+  return {__fma_rn(a.re, b.re, -a.im * b.im), __fma_rn(a.re, b.im, a.im * b.re)};
+}
+// a * conj(b)
+__device__ __forceinline__ cplx cmulc(cplx a, cplx b) {
+  return {__fma_rn(a.re, b.re, a.im * b.im), __fma_rn(a.im, b.re, -a.re * b.im)};
+}
+// acc + a * b
+__device__ __forceinline__ cplx cfma(cplx a, cplx b, cplx acc) {
+  return {__fma_rn(a.re, b.re, __fma_rn(-a.im, b.im, acc.re)), __fma_rn(a.re, b.im, __fma_rn(a.im, b.re, acc.im))};
+}
+__device__ __forceinline__ cplx mul_neg_i(cplx a) { return {a.im, -a.re}; }  // -i a
+__device__ __forceinline__ cplx mul_pos_i(cplx a) { return {-a.im, a.re}; }  // +i a
+
+constexpr double C8 = 0.92387953251128673848;   // cos(pi / 8)
+constexpr double S8 = 0.38268343236508978178;   // sin(pi / 8)
+constexpr double R2 = 0.70710678118654752440;   // sqrt(1/2)
+
+// DFT4 in place on a[o], a[o + s], a[o + 2s], a[o + 3s]; INV: exp(+2 pi i / 4) kernel
+template <bool INV>
+__device__ __forceinline__ void dft4(cplx* a, int o, int s) {
+  const cplx a0 = a[o], a1 = a[o + s], a2 = a[o + 2 * s], a3 = a[o + 3 * s];
+  const cplx s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = csub(a1, a3);
+  const cplx r = INV ? mul_pos_i(d13) : mul_neg_i(d13);
+  a[o] = cadd(s02, s13);
+  a[o + 2 * s] = csub(s02, s13);
+  a[o + s] = cadd(d02, r);
+  a[o + 3 * s] = csub(d02, r);
+}
+
+// x * W16^e (forward: exp(-2 pi i e / 16); INV: conjugate), e in 1..9
+template <bool INV>
+__device__ __forceinline__ cplx tw16(cplx x, int e) {
+  double c, s;  // W = c - i s (forward)
+  switch (e) {
+    case 1: c = C8, s = S8; break;
+    case 2: c = R2, s = R2; break;
+    case 3: c = S8, s = C8; break;
+    case 4: return INV ? mul_pos_i(x) : mul_neg_i(x);
+    case 6: c = -R2, s = R2; break;
+    case 9: c = -C8, s = -S8; break;  // exp(-2 pi i 9/16) = -cos(pi/8) + i sin(pi/8)
+    default: return x;
+  }
+  if (e == 2 || e == 6) {  // (c - i s) with |c| = |s| = R2: 2 adds + 2 muls
+    const double sgn_c = (e == 2) ? 1.0 : -1.0;
+    if (!INV) {  // (re + i im)(sgn R2 - i R2)
+      const double re = sgn_c * x.re + x.im, im = sgn_c * x.im - x.re;
+      return {re * R2, im * R2};
+    } else {  // (re + i im)(sgn R2 + i R2)
+      const double re = sgn_c * x.re - x.im, im = sgn_c * x.im + x.re;
+      return {re * R2, im * R2};
+    }
+  }
+  const cplx w = {c, INV ? s : -s};
+  return cmul(x, w);
+}
+
+// DFT16 of a[0..16) in place, natural order in and out: X[k1 + 4 k2] = sum_m a[m] W16^(m k)
+template <bool INV>
+__device__ __forceinline__ void dft16(cplx (&a)[16]) {
+#pragma unroll
+  for (int m1 = 0; m1 < 4; ++m1) dft4<INV>(a, m1, 4);  // over m2: a[m1 + 4 k1] = b[m1][k1]
+#pragma unroll
+  for (int m1 = 1; m1 < 4; ++m1)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1) a[m1 + 4 * k1] = tw16<INV>(a[m1 + 4 * k1], m1 * k1);
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) dft4<INV>(a, 4 * k1, 1);  // over m1: a[4 k1 + k2] = X[k1 + 4 k2]
+  cplx t[16];
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) t[k1 + 4 * k2] = a[4 * k1 + k2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = t[i];
+}
+
+constexpr int ROW1 = 68;               // transpose-1 row stride (complex)
+constexpr int BUF = 16 * ROW1;         // per-wave LDS buffer (complex): 17 KiB
+__device__ __forceinline__ int t2f(int L) { return 4 * (L & 3) + ((L >> 2) & 3); }
+
+// Forward: u[m] = folded value at n = lane + 64 m (untwisted); out: Fourier layout (see header).
+// `cm` = exp(i pi m / 32) (m < 16), `t1` = T1[k1 * 64 + j], `t2` = nu^(j1 k2) at [j1 * 16 + k2] (LDS).
+__device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
+                                        const cplx* __restrict__ cm, int lane) {
+#pragma unroll
+  for (int m = 1; m < 16; ++m) u[m] = cmul(u[m], cm[m]);
+  dft16<false>(u);
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) buf[k1 * ROW1 + lane] = cmul(u[k1], t1[k1 * 64 + lane]);
+  const int k1 = lane >> 2, j1 = lane & 3;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j2 = 0; j2 < 16; ++j2) u[j2] = buf[k1 * ROW1 + j1 + 4 * j2];
+  dft16<false>(u);
+#pragma unroll
+  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmul(u[k2], t2[j1 * 16 + k2]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int f = t2f(lane);
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) buf[lane * 16 + (k2 ^ f)] = u[k2];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int c = lane & 3;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int L = 4 * k1 + jj;
+      u[4 * g + jj] = buf[L * 16 + ((4 * c + g) ^ t2f(L))];
+    }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) dft4<false>(u, 4 * g, 1);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Inverse of fft_fwd including the 1/M normalisation and the untwist (`cmi` = exp(-i pi m / 32) / M).
+__device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
+                                        const cplx* __restrict__ cmi, int lane) {
+  const int k1 = lane >> 2, c = lane & 3;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) dft4<true>(u, 4 * g, 1);
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int L = 4 * k1 + jj;
+      buf[L * 16 + ((4 * c + g) ^ t2f(L))] = u[4 * g + jj];
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int f = t2f(lane), j1 = lane & 3;
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) u[k2] = buf[lane * 16 + (k2 ^ f)];
+#pragma unroll
+  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmulc(u[k2], t2[j1 * 16 + k2]);
+  dft16<true>(u);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int j2 = 0; j2 < 16; ++j2) buf[k1 * ROW1 + j1 + 4 * j2] = u[j2];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) u[kk] = cmulc(buf[kk * ROW1 + lane], t1[kk * 64 + lane]);
+  dft16<true>(u);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) u[m] = cmul(u[m], cmi[m]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- conversions (fft_impl/fft64/math/fft/mod.rs) -------------------------------------------------
+// u64 -> i64 -> f64 (into_signed().cast_into()); exact int64 -> double rounding as Rust's `as f64`
+__device__ __forceinline__ double s64_to_f64(u64 x) { return (double)(int64_t)x; }
+
+// Scalar::from_torus (commons/math/torus/mod.rs:72-78): fract = x - round(x); round(fract * 2^64) as i64 as u64.
+// round-half-even instead of half-away-from-zero: they differ only for fract exactly +-1/2 (and x an exact
+// half-integer), where the reference itself saturates 2^63 to i64::MAX.
+__device__ __forceinline__ u64 from_torus(double x) {
+  const double fr = x - __builtin_rint(x);
+  const double v = __builtin_rint(fr * 18446744073709551616.0);  // |v| <= 2^63, integral
+  const double hi = __builtin_floor(v * (1.0 / 4294967296.0));   // exact
+  const double lo = __fma_rn(-hi, 4294967296.0, v);             // in [0, 2^32), exact
+  const int32_t h = (hi >= 2147483648.0) ? 0x7fffffff : (int32_t)hi;
+  return ((u64)(uint32_t)h << 32) + (u64)(uint32_t)lo;
+}
+
+// ---- decomposition (commons/math/decomposition/decomposer.rs:156-185, iter.rs:131-151) ------------
+__device__ __forceinline__ u64 decomp_init_native(u64 input, int base_log, int level) {
+  const unsigned rep = base_log * level, non_rep = 64u - rep;
+  u64 res = input >> (non_rep - 1);
+  const u64 rounding_bit = res & 1u;
+  res += 1;
+  res >>= 1;
+  res &= (~0ull) >> (64u - rep);
+  const u64 need_balance = (((res - 1) | (rounding_bit << (rep - 1))) & res) >> (rep - 1);
+  return res - (need_balance << rep);
+}
+__device__ __forceinline__ u64 decompose_one_level(int base_log, u64& state) {
+  const u64 mask = (1ull << base_log) - 1;
+  const u64 res = state & mask;
+  state = (u64)((int64_t)state >> base_log);
+  const u64 carry = (((res - 1) | state) & res) >> (base_log - 1);
+  state += carry;
+  return res - (carry << base_log);
+}
+
+// fft_impl/common.rs:10-23
+__device__ __forceinline__ u64 modulus_switch(u64 input, unsigned log_modulus) {
+  return (input + (1ull << (64u - log_modulus - 1u))) >> (64u - log_modulus);
+}
+
+struct Tables {
+  const cplx* t1;   // [16][64] forward pass-1 twiddles (twist folded in)
+  const cplx* t2;   // [4][16]
+  const cplx* cm;   // [16] exp(i pi m / 32)
+  const cplx* cmi;  // [16] exp(-i pi m / 32) / M
+};
+
+constexpr int N = 2048, M = 1024, NPL = N / 64;  // 32 coefficients per lane
+
+// ---- forward_as_torus / backward_as_torus over a batch of polynomials (key conversion, tests) ------
+// one wave per polynomial; `fourier`: batch x 1024 complex in the Fourier layout (position reg * 64 + lane)
+__global__ __launch_bounds__(64) void fwd_torus_kernel(cplx* __restrict__ fourier, const u64* __restrict__ std_,
+                                                       uint64_t batch, Tables tb) {
+  __shared__ cplx buf[BUF];
+  __shared__ cplx t2[64];
+  const int lane = threadIdx.x;
+  t2[lane] = tb.t2[lane];
+  __syncthreads();
+  const uint64_t b = blockIdx.x;
+  if (b >= batch) return;
+  const u64* x = std_ + b * N;
+  constexpr double NORM = 1.0 / 18446744073709551616.0;  // 2^-64 (convert_forward_torus)
+  cplx u[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) u[m] = {s64_to_f64(x[lane + 64 * m]) * NORM, s64_to_f64(x[M + lane + 64 * m]) * NORM};
+  fft_fwd(u, buf, tb.t1, t2, tb.cm, lane);
+  cplx* out = fourier + b * M;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) out[r * 64 + lane] = u[r];
+}
+
+__global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, const cplx* __restrict__ fourier,
+                                                       uint64_t batch, int add, Tables tb) {
+  __shared__ cplx buf[BUF];
+  __shared__ cplx t2[64];
+  const int lane = threadIdx.x;
+  t2[lane] = tb.t2[lane];
+  __syncthreads();
+  const uint64_t b = blockIdx.x;
+  if (b >= batch) return;
+  const cplx* in = fourier + b * M;
+  cplx u[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) u[r] = in[r * 64 + lane];
+  fft_inv(u, buf, tb.t1, t2, tb.cmi, lane);
+  u64* x = std_ + b * N;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const u64 re = from_torus(u[m].re), im = from_torus(u[m].im);
+    x[lane + 64 * m] = add ? x[lane + 64 * m] + re : re;
+    x[M + lane + 64 * m] = add ? x[M + lane + 64 * m] + im : im;
+  }
+}
+
+// ---- external product on registers ----------------------------------------------------------------
+// Wave w (< K + 1) owns GLWE polynomial w.  in: ct1[NPL] = this wave's polynomial of the GLWE to decompose
+// (coefficient lane + 64 r); out: y[16] = the Fourier-domain contribution to polynomial w, then converted:
+// acc[r] += from_torus(...).  `ggsw`: level x (K+1) rows x (K+1) cols x M complex (Fourier layout), highest
+// level first, as the reference's FourierGgswCiphertext.  `bufs` = (K+1) per-wave buffers.
+template <int K, bool L1>
+__device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1)[NPL], const cplx* __restrict__ ggsw,
+                                                int base_log, int level, cplx* bufs, const cplx* t2, const Tables& tb,
+                                                int w, int lane) {
+  cplx* buf = bufs + w * BUF;
+  cplx y[16];
+  if (L1) {
+    cplx u[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      u64 s0 = decomp_init_native(ct1[m], base_log, 1), s1 = decomp_init_native(ct1[m + 16], base_log, 1);
+      const u64 d0 = decompose_one_level(base_log, s0), d1 = decompose_one_level(base_log, s1);
+      u[m] = {s64_to_f64(d0), s64_to_f64(d1)};  // convert_forward_integer: into_signed as f64
+    }
+    fft_fwd(u, buf, tb.t1, t2, tb.cm, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
+    __syncthreads();
+    // update_with_fmadd: y_w = sum_rr X_rr * G[rr][w]
+    const cplx* mat = ggsw;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      cplx a = cmul(u[r], mat[((size_t)w * (K + 1) + w) * M + r * 64 + lane]);
+#pragma unroll
+      for (int rr = 0; rr <= K; ++rr) {
+        if (rr == w) continue;
+        a = cfma(bufs[rr * BUF + r * 64 + lane], mat[((size_t)rr * (K + 1) + w) * M + r * 64 + lane], a);
+      }
+      y[r] = a;
+    }
+    __syncthreads();
+  } else {
+    u64 st[NPL];
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) st[r] = decomp_init_native(ct1[r], base_log, level);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y[r] = {0.0, 0.0};
+#pragma unroll 1
+    for (int li = 0; li < level; ++li) {
+      cplx u[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const u64 d0 = decompose_one_level(base_log, st[m]), d1 = decompose_one_level(base_log, st[m + 16]);
+        u[m] = {s64_to_f64(d0), s64_to_f64(d1)};
+      }
+      fft_fwd(u, buf, tb.t1, t2, tb.cm, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
+      __syncthreads();
+      // the decomposition iterator yields the least significant level first, which the GGSW stores first
+      const cplx* mat = ggsw + (size_t)li * (K + 1) * (K + 1) * M;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        cplx a = y[r];
+#pragma unroll
+        for (int rr = 0; rr <= K; ++rr)
+          a = cfma(bufs[rr * BUF + r * 64 + lane], mat[((size_t)rr * (K + 1) + w) * M + r * 64 + lane], a);
+        y[r] = a;
+      }
+      __syncthreads();
+    }
+  }
+  fft_inv(y, buf, tb.t1, t2, tb.cmi, lane);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {  // convert_add_backward_torus
+    acc[m] += from_torus(y[m].re);
+    acc[m + 16] += from_torus(y[m].im);
+  }
+}
+
+// EXT : out[b] += GGSW (.) glwe[b]                       (add_external_product_assign)
+// CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]    (cmux: ct1 -= ct0; ct0 += ext(ct1))
+template <int K, bool CMUX, bool L1>
+__device__ __forceinline__ void ext_product_body(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                 const cplx* __restrict__ ggsw, uint32_t batch, int base_log,
+                                                 int level, const Tables& tb, cplx* bufs, cplx* t2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x < 64) t2[lane] = tb.t2[lane];
+  __syncthreads();
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;  // uniform per workgroup
+  u64* in = glwe + ((size_t)b * (K + 1) + w) * N;
+  u64* o = out + ((size_t)b * (K + 1) + w) * N;
+  u64 ct[NPL], acc[NPL];
+#pragma unroll
+  for (int r = 0; r < NPL; ++r) {
+    ct[r] = in[lane + 64 * r];
+    acc[r] = o[lane + 64 * r];
+    if (CMUX) {
+      ct[r] -= acc[r];
+      in[lane + 64 * r] = ct[r];
+    }
+  }
+  ext_product_add<K, L1>(acc, ct, ggsw, base_log, level, bufs, t2, tb, w, lane);
+#pragma unroll
+  for (int r = 0; r < NPL; ++r) o[lane + 64 * r] = acc[r];
+}
+
+// The shortint shape (k = 1, one level) is held to 256 registers for 2 waves per SIMD; the coverage shapes
+// keep the compiler's choice (more registers, 1 wave per SIMD) instead of spilling.
+template <int K, bool CMUX, bool L1>
+__global__ __launch_bounds__(64 * (K + 1)) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                                   const cplx* __restrict__ ggsw, uint32_t batch,
+                                                                   int base_log, int level, Tables tb) {
+  __shared__ cplx bufs[(K + 1) * BUF];
+  __shared__ cplx t2[64];
+  ext_product_body<K, CMUX, L1>(out, glwe, ggsw, batch, base_log, level, tb, bufs, t2);
+}
+template <bool CMUX>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ext_product_kernel_k1l1(
+    u64* __restrict__ out, u64* __restrict__ glwe, const cplx* __restrict__ ggsw, uint32_t batch, int base_log,
+    int level, Tables tb) {
+  __shared__ cplx bufs[2 * BUF];
+  __shared__ cplx t2[64];
+  ext_product_body<1, CMUX, true>(out, glwe, ggsw, batch, base_log, level, tb, bufs, t2);
+}
+
+// algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the workgroup
+template <int T>
+__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int t,
+                                        u64* sh) {
+  u64 sum_half = 0;
+  int64_t sum_hed = 0;
+  for (uint32_t i = t; i < n_lwe; i += T) {
+    const u64 a = lwe[i];
+    const int64_t err = (int64_t)((modulus_switch(a, log_mod) << (64u - log_mod)) - a);
+    const int64_t half = err / 2;
+    sum_half += (u64)half;
+    sum_hed += 2 * half - err;
+  }
+  sh[t] = sum_half;
+  sh[T + t] = (u64)sum_hed;
+  __syncthreads();
+  for (int s = T / 2; s > 0; s >>= 1) {
+    if (t < s) {
+      sh[t] += sh[t + s];
+      sh[T + t] = (u64)((int64_t)sh[T + t] + (int64_t)sh[T + t + s]);
+    }
+    __syncthreads();
+  }
+  const u64 total_half = sh[0];
+  const int64_t total_hed = (int64_t)sh[T];
+  __syncthreads();
+  const u64 sum_halving = (u64)(total_hed / 2);
+  const u64 half_case = 1ull << (64u - log_mod - 1u);
+  return total_half - sum_halving - half_case;
+}
+
+// ---- programmable bootstrap (bootstrap.rs:481-521 + blind_rotate_assign :294-381) -------------------
+// lwe_in: batch x (n + 1); lut: (K+1) x N shared; fbsk: n x level x (K+1) x (K+1) x M complex;
+// lwe_out: batch x (K N + 1).  ms_mode: 0 standard, 1 centered, 2 pre-switched (values in [0, 2N)).
+template <int K, bool L1>
+__device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+                                         const u64* __restrict__ lut, const cplx* __restrict__ fbsk, uint32_t n_lwe,
+                                         uint32_t batch, int base_log, int level, int ms_mode, const Tables& tb,
+                                         cplx* bufs, cplx* t2) {
+  constexpr int T = 64 * (K + 1);
+  constexpr unsigned LOG_MOD = 12;  // PolynomialSize(2048)::to_blind_rotation_input_modulus_log
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t < 64) t2[lane] = tb.t2[lane];
+  __syncthreads();
+  const uint32_t b = blockIdx.x;
+  if (b >= batch) return;
+  const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
+  const size_t ggsw_len = (size_t)level * (K + 1) * (K + 1) * M;
+  u64* sh = reinterpret_cast<u64*>(bufs);        // all waves: reductions
+  u64* mine = reinterpret_cast<u64*>(bufs + w * BUF);  // this wave's rotation buffer (2048 u64 = 16 KiB)
+
+  u64 body_corr = 0;
+  if (ms_mode == 1) body_corr = centered_body_correction<T>(lwe, n_lwe, LOG_MOD, t, sh);
+  const u64 body = (ms_mode == 2) ? (lwe[n_lwe] & (2 * N - 1)) : modulus_switch(lwe[n_lwe] + body_corr, LOG_MOD);
+
+  // local accumulator = LUT / X^body (polynomial_wrapping_monic_monomial_div)
+  u64 acc[NPL];
+  {
+    const u64* lp = lut + (size_t)w * N;
+    const int full = (int)(body / N) & 1, rem = (int)(body % N);
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) {
+      const int m = lane + 64 * r;  // div: new[m] = old[(m + rem) % N], negated for m >= N - rem
+      u64 v = lp[(m + rem) & (N - 1)];
+      if (full ^ (m >= N - rem)) v = (u64)0 - v;
+      acc[r] = v;
+    }
+  }
+
+  for (uint32_t i = 0; i < n_lwe; ++i) {
+    const u64 a = (ms_mode == 2) ? (lwe[i] & (2 * N - 1)) : modulus_switch(lwe[i], LOG_MOD);
+    if (a == 0) continue;  // bootstrap.rs:336 (uniform per workgroup)
+    const int full = (int)(a / N) & 1, rem = (int)(a % N);
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) mine[lane + 64 * r] = acc[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u64 ct1[NPL];
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) {  // polynomial_wrapping_monic_monomial_mul_and_subtract
+      const int e = lane + 64 * r;
+      u64 v = mine[(e - rem) & (N - 1)];
+      if (full ^ (e < rem)) v = (u64)0 - v;
+      ct1[r] = v - acc[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ext_product_add<K, L1>(acc, ct1, fbsk + (size_t)i * ggsw_len, base_log, level, bufs, t2, tb, w, lane);
+  }
+
+  // extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160), nth = 0
+  u64* out = lwe_out + (size_t)b * (K * N + 1);
+  if (w < K) {
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) mine[lane + 64 * r] = acc[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) {
+      const int j = lane + 64 * r;
+      out[(size_t)w * N + j] = (j == 0) ? mine[0] : (u64)0 - mine[N - j];
+    }
+  } else if (lane == 0) {
+    out[(size_t)K * N] = acc[0];
+  }
+}
+
+template <int K, bool L1>
+__global__ __launch_bounds__(64 * (K + 1)) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+                                                           const u64* __restrict__ lut, const cplx* __restrict__ fbsk,
+                                                           uint32_t n_lwe, uint32_t batch, int base_log, int level,
+                                                           int ms_mode, Tables tb) {
+  __shared__ cplx bufs[(K + 1) * BUF];
+  __shared__ cplx t2[64];
+  pbs_body<K, L1>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, bufs, t2);
+}
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void pbs_kernel_k1l1(
+    u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in, const u64* __restrict__ lut,
+    const cplx* __restrict__ fbsk, uint32_t n_lwe, uint32_t batch, int base_log, int level, int ms_mode, Tables tb) {
+  __shared__ cplx bufs[2 * BUF];
+  __shared__ cplx t2[64];
+  pbs_body<1, true>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, bufs, t2);
+}
+
+}  // namespace fft
+
+// ---- launchers ----------------------------------------------------------------------------------
+static fft::Tables tables(const FftTables& t) {
+  return {reinterpret_cast<const fft::cplx*>(t.t1), reinterpret_cast<const fft::cplx*>(t.t2),
+          reinterpret_cast<const fft::cplx*>(t.cm), reinterpret_cast<const fft::cplx*>(t.cmi)};
+}
+
+hipError_t launch_fft64_fwd_torus(double* fourier, const uint64_t* std_, size_t batch, const FftTables& t,
+                                  hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft::fwd_torus_kernel, dim3((unsigned)batch), dim3(64), 0, s,
+                     reinterpret_cast<fft::cplx*>(fourier), std_, (uint64_t)batch, tables(t));
+  return hipGetLastError();
+}
+
+hipError_t launch_fft64_bwd_torus(uint64_t* std_, const double* fourier, size_t batch, bool add, const FftTables& t,
+                                  hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  hipLaunchKernelGGL(fft::bwd_torus_kernel, dim3((unsigned)batch), dim3(64), 0, s, std_,
+                     reinterpret_cast<const fft::cplx*>(fourier), (uint64_t)batch, add ? 1 : 0, tables(t));
+  return hipGetLastError();
+}
+
+template <int K, bool CMUX, bool L1>
+static hipError_t ext_one(uint64_t* out, uint64_t* glwe, const fft::cplx* g, size_t batch, int base_log, int level,
+                          const FftTables& t, hipStream_t s) {
+  if (K == 1 && L1)
+    hipLaunchKernelGGL((fft::ext_product_kernel_k1l1<CMUX>), dim3((unsigned)batch), dim3(128), 0, s, out, glwe, g,
+                       (uint32_t)batch, base_log, level, tables(t));
+  else
+    hipLaunchKernelGGL((fft::ext_product_kernel<K, CMUX, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out,
+                       glwe, g, (uint32_t)batch, base_log, level, tables(t));
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t ext_k(bool cmux, uint64_t* out, uint64_t* glwe, const double* ggsw, size_t batch, int base_log,
+                        int level, const FftTables& t, hipStream_t s) {
+  const auto* g = reinterpret_cast<const fft::cplx*>(ggsw);
+  if (level == 1)
+    return cmux ? ext_one<K, true, true>(out, glwe, g, batch, base_log, level, t, s)
+                : ext_one<K, false, true>(out, glwe, g, batch, base_log, level, t, s);
+  return cmux ? ext_one<K, true, false>(out, glwe, g, batch, base_log, level, t, s)
+              : ext_one<K, false, false>(out, glwe, g, batch, base_log, level, t, s);
+}
+
+hipError_t launch_fft64_ext_product(int k, bool cmux, uint64_t* out, uint64_t* glwe, const double* ggsw, size_t batch,
+                                    int base_log, int level, const FftTables& t, hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  if (k == 1) return ext_k<1>(cmux, out, glwe, ggsw, batch, base_log, level, t, s);
+  if (k == 2) return ext_k<2>(cmux, out, glwe, ggsw, batch, base_log, level, t, s);
+  return hipErrorInvalidValue;
+}
+
+template <int K, bool L1>
+static hipError_t pbs_one(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const fft::cplx* g, size_t n_lwe,
+                          size_t batch, int base_log, int level, int ms_mode, const FftTables& t, hipStream_t s) {
+  if (K == 1 && L1)
+    hipLaunchKernelGGL(fft::pbs_kernel_k1l1, dim3((unsigned)batch), dim3(128), 0, s, out, lwe_in, lut, g,
+                       (uint32_t)n_lwe, (uint32_t)batch, base_log, level, ms_mode, tables(t));
+  else
+    hipLaunchKernelGGL((fft::pbs_kernel<K, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out, lwe_in, lut, g,
+                       (uint32_t)n_lwe, (uint32_t)batch, base_log, level, ms_mode, tables(t));
+  return hipGetLastError();
+}
+
+hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftTables& t,
+                            hipStream_t s) {
+  if (batch == 0) return hipSuccess;
+  const auto* g = reinterpret_cast<const fft::cplx*>(fbsk);
+  const bool l1 = level == 1;
+  if (k == 1)
+    return l1 ? pbs_one<1, true>(out, lwe_in, lut, g, n_lwe, batch, base_log, level, ms_mode, t, s)
+              : pbs_one<1, false>(out, lwe_in, lut, g, n_lwe, batch, base_log, level, ms_mode, t, s);
+  if (k == 2)
+    return l1 ? pbs_one<2, true>(out, lwe_in, lut, g, n_lwe, batch, base_log, level, ms_mode, t, s)
+              : pbs_one<2, false>(out, lwe_in, lut, g, n_lwe, batch, base_log, level, ms_mode, t, s);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mi

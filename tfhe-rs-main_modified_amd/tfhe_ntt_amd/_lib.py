@@ -75,6 +75,21 @@ _SIGS = {
     "mi_multi_gpu_scatter": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "mi_multi_gpu_gather": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "mi_pbs_ntt64_multi_gpu": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_fft64_plan_create": (_int, [_sz, _int, ctypes.POINTER(_vp)]),
+    "mi_fft64_plan_cached": (_int, [_sz, _int, ctypes.POINTER(_vp)]),
+    "mi_fft64_plan_destroy": (_int, [_vp]),
+    "mi_fft64_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int)]),
+    "mi_fft64_fourier_order": (_int, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
+    "mi_fft64_forward_torus_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_fft64_backward_torus_batch": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_bsk_to_fourier64": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_fft64_ext_product_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _vp]),
+    "mi_fft64_cmux_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _vp]),
+    "mi_fft64_pbs_key_create": (_int, [_vp, _vp, _sz, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "mi_fft64_pbs_key_destroy": (_int, [_vp]),
+    "mi_fft64_pbs_key_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int),
+                                     ctypes.POINTER(_int)]),
+    "mi_fft64_pbs_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
     "mi_ntt32_plan_create": (_int, [_sz, ctypes.c_uint32, _int, ctypes.POINTER(_vp)]),
     "mi_ntt32_plan_destroy": (_int, [_vp]),
     "mi_ntt32_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(_int)]),
