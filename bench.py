@@ -244,6 +244,46 @@ def bench_pbs_solinas(args, eng, torch, dev, world, barrier):
                        "batch_per_gpu": batch}}
 
 
+def bench_pbs_fft(args, eng, torch, dev, world, barrier):
+    """The default shortint PBS, f64-FFT path (programmable_bootstrap_lwe_ciphertext, fft64_pbs.rs:924-1060)
+    at PARAM_MESSAGE_2_CARRY_2's shape: native 2^64 ciphertexts, Fourier key (60 MB of complex f64) resident."""
+    F = eng.fft64
+    fft = F.Fft(N, dev.index)
+    n_lwe, batch = PBS_N_LWE, args.pbs_batch
+    std = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(std, SEED + 80, 0)
+    fbsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N // 2, 2), dtype=torch.float64, device=dev)
+    F.convert_standard_lwe_bootstrap_key_to_fourier(std, fbsk, fft)
+    del std
+    key = F.FourierLweBootstrapKey(fbsk, PBS_BASE_LOG, PBS_LEVEL, fft)
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 81, 0)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 82, 0)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+    run = lambda: F.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, key)
+    run()
+    torch.cuda.synchronize()
+    K = args.pbs_steps
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(K):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    del key
+    return {"metric": "PBS/sec, f64-FFT path (default shortint PBS), PARAM_MESSAGE_2_CARRY_2 shape",
+            "value": world * batch * K / el, "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3,
+            "kernel_ms": e0.elapsed_time(e1) / K, "dtype": "f64",
+            "config": {"workload": "programmable_bootstrap_lwe_ciphertext (tfhe-fft path), n=918 k=1 N=2048 "
+                                   "base_log=23 level=1, standard modulus switch", "batch_per_gpu": batch}}
+
+
 def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk):
     """Config 5: one global batch of PBS (default 65,536) held on the root, scattered over the ranks,
     bootstrapped, gathered back (strong scaling).  The transfers are grouped point-to-point sends from
@@ -659,6 +699,7 @@ def main():
         out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
         out["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier)
+        out["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, world, barrier)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
         out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
         out["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier)

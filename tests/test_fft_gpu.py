@@ -2,9 +2,9 @@
 
 The reference's transform is a measured f64 FFT, so the bar is the f64 error bound, not bit equality
 (SURVEY.md §8f rank 4): transforms within ~1e-13 relative of the numpy restatement (oracle/fft_oracle.py)
-after mapping this engine's Fourier order; external products within 2^48 of the EXACT integer result;
-PBS outputs that decrypt to f(m) for every ciphertext of a full 4096 batch under real keys, and stay
-within the accumulated FFT noise of the restatement.
+after mapping this engine's Fourier order; external products within the f64 bound of the EXACT integer
+result; PBS outputs that decrypt to f(m) for every ciphertext of a full 4096 batch under real keys, with the
+phase noise of the restatement.
 """
 import numpy as np
 import pytest
@@ -139,7 +139,8 @@ def test_external_product_vs_exact(engine, fft, k, base_log, level):
         with np.errstate(over="ignore"):
             want = out0[b] + _exact_ext_product(glwe[b], ggsw, base_log, level)
         err = F.signed_diff(got[b], want).max()
-        assert err < 2.0 ** 48, (b, np.log2(err))
+        # f64 error: digits up to 2^(B-1) times torus values, summed over N terms, kept to 53 bits
+        assert err < 2.0 ** max(48, base_log + 24), (b, np.log2(err))
 
 
 def test_cmux_semantics(engine, fft):
@@ -163,7 +164,10 @@ def test_cmux_semantics(engine, fft):
 def test_pbs_config4_full_batch_real_keys(engine, fft, order):
     """The default shortint PBS at PARAM_MESSAGE_2_CARRY_2's shape (n = 918, N = 2048, B = 2^23, l = 1, 2+2-bit
     messages with padding, TUniform 2^45 LWE / 2^17 GLWE noise) on the f64-FFT path: all 4096 outputs decrypt
-    to f(m); 4 of them within the FFT noise of the numpy restatement."""
+    to f(m), and their phase noise matches the numpy restatement's.  The output ciphertexts themselves are NOT
+    comparable bit for bit with any other f64 implementation (the reference's included): once FFT rounding flips
+    one decomposition digit, the masks differ by a GGSW row, i.e. by an encryption of zero — both results are
+    valid encryptions of f(m) with the same noise distribution."""
     import torch
     n_lwe, base_log, level, msg_mod, batch = 918, 23, 1, 16, 4096
     delta = (1 << 63) // msg_mod
@@ -181,14 +185,19 @@ def test_pbs_config4_full_batch_real_keys(engine, fft, order):
     out = dev(np.zeros((batch, N + 1), np.uint64))
     engine.fft64.programmable_bootstrap_lwe_ciphertext(dev(lwe), out, dev(lut), key)
     got = host(out)
-    pts = H.lwe_decrypt_batch(got, H.glwe_sk_as_lwe_sk(glwe_sk))
+    sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    pts = H.lwe_decrypt_batch(got, sk)
+    want_pt = np.array([f(int(m)) for m in msgs], np.uint64) * np.uint64(delta)
     with np.errstate(over="ignore"):
         dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
-    assert np.array_equal(dec, np.array([f(int(m)) for m in msgs], np.uint64))
-    idx = np.array([0, 1, 2047, batch - 1])
-    want = F.pbs(lwe[idx], lut, F.forward_as_torus(bsk), base_log, level)
-    err = F.signed_diff(got[idx], want).max()
-    assert err < 2.0 ** 54, np.log2(err)
+    assert np.array_equal(dec, want_pt // np.uint64(delta))
+    noise = F.signed_diff(pts, want_pt)
+    assert noise.max() < 2.0 ** 54, np.log2(noise.max())
+    idx = np.array([0, 1, 2, 3, 2047, batch - 1])
+    ref = F.pbs(lwe[idx], lut, F.forward_as_torus(bsk), base_log, level)
+    ref_noise = F.signed_diff(H.lwe_decrypt_batch(ref, sk), want_pt[idx])
+    rms = lambda e: float(np.sqrt(np.mean(e ** 2)))
+    assert rms(ref_noise) / 4 < rms(noise) < 4 * rms(ref_noise), (np.log2(rms(noise)), np.log2(rms(ref_noise)))
 
 
 @pytest.mark.parametrize("k,level,base_log", [(1, 2, 12), (2, 1, 23), (2, 2, 12)])
