@@ -10,7 +10,7 @@ namespace mi {
 //   t1  [16][64]  w^j omega^(j k1), w = exp(i pi / 2M), omega = exp(-2 pi i / M), M = 1024
 //   t2  [4][16]   nu^(j1 k2), nu = exp(-2 pi i / 64)
 //   cm  [16]      exp(i pi m / 32)
-//   cmi [16]      exp(-i pi m / 32) / M
+//   cmi [16]      exp(-i pi m / 32) 2^64 / M
 struct FftTables {
   const double* t1;
   const double* t2;

@@ -20,7 +20,7 @@
 //           the per-m part of the twist, exp(i pi m / 32), is applied before the DFT16)
 //   LDS transpose 1 (row stride 68 complex: conflict-free ds_write_b128 / ds_read_b128)
 //   pass 2  lane 4 k1 + j1 holds the 16 values j = j1 + 4 j2: DFT16 over j2, twiddle nu^(j1 k2) (nu = omega^16)
-//   LDS transpose 2 (slot 16 L + (k2 ^ (4 (L & 3) + ((L >> 2) & 3))): conflict-free both ways)
+//   LDS transpose 2 (slot 17 L + swap2(k2): conflict-free both ways, tools/lds_layout_check.py)
 //   pass 3  lane 4 k1 + c holds (g, j1) for k2 = 4 c + g: DFT4 over j1 -> k3
 // Fourier position (lane 4 k1 + c, register 4 g + k3) holds frequency 256 k3 + 16 (4 c + g) + k1.  The inverse
 // runs the passes backwards with conjugate twiddles.  All f64 arithmetic is FMA-contracted by hand where the
@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fft64_decomp.hpp"
 #include "fft64_launch.hpp"
 
 namespace mi {
@@ -120,7 +121,12 @@ __device__ __forceinline__ void dft16(cplx (&a)[16]) {
 
 constexpr int ROW1 = 68;               // transpose-1 row stride (complex)
 constexpr int BUF = 16 * ROW1;         // per-wave LDS buffer (complex): 17 KiB
-__device__ __forceinline__ int t2f(int L) { return 4 * (L & 3) + ((L >> 2) & 3); }
+constexpr int ROW2 = 17;              // transpose-2 row stride (complex)
+constexpr int T2S = 17;               // row stride of the LDS copy of the pass-2 twiddles
+// transpose-2 slot of element (pass-2 lane L, k2): rows of 17, the two 2-bit halves of k2 swapped — with the
+// b128 lane groups of MI355X_MICROARCH.md §LDS, conflict-free for all four accesses (forward write / read,
+// inverse write / read; found by exhaustive check, tools/lds_layout_check.py)
+__device__ __forceinline__ int t2slot(int L, int k2) { return ROW2 * L + (((k2 >> 2) | (k2 << 2)) & 15); }
 
 // Forward: u[m] = folded value at n = lane + 64 m (untwisted); out: Fourier layout (see header).
 // `cm` = exp(i pi m / 32) (m < 16), `t1` = T1[k1 * 64 + j], `t2` = nu^(j1 k2) at [j1 * 16 + k2] (LDS).
@@ -139,13 +145,12 @@ __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __
   for (int j2 = 0; j2 < 16; ++j2) u[j2] = buf[k1 * ROW1 + j1 + 4 * j2];
   dft16<false>(u);
 #pragma unroll
-  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmul(u[k2], t2[j1 * 16 + k2]);
+  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmul(u[k2], t2[j1 * T2S + k2]);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int f = t2f(lane);
 #pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) buf[lane * 16 + (k2 ^ f)] = u[k2];
+  for (int k2 = 0; k2 < 16; ++k2) buf[t2slot(lane, k2)] = u[k2];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -154,8 +159,7 @@ __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int L = 4 * k1 + jj;
-      u[4 * g + jj] = buf[L * 16 + ((4 * c + g) ^ t2f(L))];
+      u[4 * g + jj] = buf[t2slot(4 * k1 + jj, 4 * c + g)];
     }
 #pragma unroll
   for (int g = 0; g < 4; ++g) dft4<false>(u, 4 * g, 1);
@@ -164,7 +168,8 @@ __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Inverse of fft_fwd including the 1/M normalisation and the untwist (`cmi` = exp(-i pi m / 32) / M).
+// Inverse of fft_fwd including the 1/M normalisation and the untwist (`cmi` = exp(-i pi m / 32) 2^64 / M: the
+// output is 2^64 times the torus value, ready for from_torus_scaled).
 __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
                                         const cplx* __restrict__ cmi, int lane) {
   const int k1 = lane >> 2, c = lane & 3;
@@ -174,17 +179,16 @@ __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int L = 4 * k1 + jj;
-      buf[L * 16 + ((4 * c + g) ^ t2f(L))] = u[4 * g + jj];
+      buf[t2slot(4 * k1 + jj, 4 * c + g)] = u[4 * g + jj];
     }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int f = t2f(lane), j1 = lane & 3;
+  const int j1 = lane & 3;
 #pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) u[k2] = buf[lane * 16 + (k2 ^ f)];
+  for (int k2 = 0; k2 < 16; ++k2) u[k2] = buf[t2slot(lane, k2)];
 #pragma unroll
-  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmulc(u[k2], t2[j1 * 16 + k2]);
+  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmulc(u[k2], t2[j1 * T2S + k2]);
   dft16<true>(u);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -208,16 +212,20 @@ __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __
 // u64 -> i64 -> f64 (into_signed().cast_into()); exact int64 -> double rounding as Rust's `as f64`
 __device__ __forceinline__ double s64_to_f64(u64 x) { return (double)(int64_t)x; }
 
-// Scalar::from_torus (commons/math/torus/mod.rs:72-78): fract = x - round(x); round(fract * 2^64) as i64 as u64.
-// round-half-even instead of half-away-from-zero: they differ only for fract exactly +-1/2 (and x an exact
-// half-integer), where the reference itself saturates 2^63 to i64::MAX.
-__device__ __forceinline__ u64 from_torus(double x) {
-  const double fr = x - __builtin_rint(x);
-  const double v = __builtin_rint(fr * 18446744073709551616.0);  // |v| <= 2^63, integral
-  const double hi = __builtin_floor(v * (1.0 / 4294967296.0));   // exact
-  const double lo = __fma_rn(-hi, 4294967296.0, v);             // in [0, 2^32), exact
-  const int32_t h = (hi >= 2147483648.0) ? 0x7fffffff : (int32_t)hi;
-  return ((u64)(uint32_t)h << 32) + (u64)(uint32_t)lo;
+// Scalar::from_torus (commons/math/torus/mod.rs:72-78) of x = y / 2^64, taking y = x 2^64 (the 2^64 is folded
+// into the inverse transform's last twiddles): round(fract(x) 2^64) mod 2^64 = round(y) mod 2^64.  All steps
+// exact: r = rint(y); z = r - rint(r 2^-64) 2^64 in [-2^63, 2^63]; z = hi 2^32 + lo with lo in [0, 2^32); the
+// words are read from the mantissas of hi + 1.5 2^52 and lo + 2^52.  round-half-even instead of half-away-from-
+// zero: different only for an exact half-integer y, where the reference also saturates +2^63 (to i64::MAX; here
+// it wraps to 2^63).
+__device__ __forceinline__ u64 from_torus_scaled(double y) {
+  const double r = __builtin_rint(y);
+  const double z = __fma_rn(-__builtin_rint(r * 0x1p-64), 0x1p64, r);
+  const double hi = __builtin_floor(z * 0x1p-32);
+  const double lo = __fma_rn(-hi, 0x1p32, z);
+  const uint32_t h = (uint32_t)__double_as_longlong(hi + 0x1.8p52);
+  const uint32_t l = (uint32_t)__double_as_longlong(lo + 0x1p52);
+  return ((u64)h << 32) | l;
 }
 
 // ---- decomposition (commons/math/decomposition/decomposer.rs:156-185, iter.rs:131-151) ------------
@@ -249,7 +257,7 @@ struct Tables {
   const cplx* t1;   // [16][64] forward pass-1 twiddles (twist folded in)
   const cplx* t2;   // [4][16]
   const cplx* cm;   // [16] exp(i pi m / 32)
-  const cplx* cmi;  // [16] exp(-i pi m / 32) / M
+  const cplx* cmi;  // [16] exp(-i pi m / 32) 2^64 / M (the torus -> u64 scale folded in)
 };
 
 constexpr int N = 2048, M = 1024, NPL = N / 64;  // 32 coefficients per lane
@@ -259,9 +267,9 @@ constexpr int N = 2048, M = 1024, NPL = N / 64;  // 32 coefficients per lane
 __global__ __launch_bounds__(64) void fwd_torus_kernel(cplx* __restrict__ fourier, const u64* __restrict__ std_,
                                                        uint64_t batch, Tables tb) {
   __shared__ cplx buf[BUF];
-  __shared__ cplx t2[64];
+  __shared__ cplx t2[4 * T2S];
   const int lane = threadIdx.x;
-  t2[lane] = tb.t2[lane];
+  t2[(lane >> 4) * T2S + (lane & 15)] = tb.t2[lane];
   __syncthreads();
   const uint64_t b = blockIdx.x;
   if (b >= batch) return;
@@ -279,9 +287,9 @@ __global__ __launch_bounds__(64) void fwd_torus_kernel(cplx* __restrict__ fourie
 __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, const cplx* __restrict__ fourier,
                                                        uint64_t batch, int add, Tables tb) {
   __shared__ cplx buf[BUF];
-  __shared__ cplx t2[64];
+  __shared__ cplx t2[4 * T2S];
   const int lane = threadIdx.x;
-  t2[lane] = tb.t2[lane];
+  t2[(lane >> 4) * T2S + (lane & 15)] = tb.t2[lane];
   __syncthreads();
   const uint64_t b = blockIdx.x;
   if (b >= batch) return;
@@ -293,46 +301,82 @@ __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, c
   u64* x = std_ + b * N;
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    const u64 re = from_torus(u[m].re), im = from_torus(u[m].im);
+    const u64 re = from_torus_scaled(u[m].re), im = from_torus_scaled(u[m].im);
     x[lane + 64 * m] = add ? x[lane + 64 * m] + re : re;
     x[M + lane + 64 * m] = add ? x[M + lane + 64 * m] + im : im;
   }
 }
 
 // ---- external product on registers ----------------------------------------------------------------
-// Wave w (< K + 1) owns GLWE polynomial w.  in: ct1[NPL] = this wave's polynomial of the GLWE to decompose
-// (coefficient lane + 64 r); out: y[16] = the Fourier-domain contribution to polynomial w, then converted:
-// acc[r] += from_torus(...).  `ggsw`: level x (K+1) rows x (K+1) cols x M complex (Fourier layout), highest
-// level first, as the reference's FourierGgswCiphertext.  `bufs` = (K+1) per-wave buffers.
+// Wave w (< K + 1, wave-uniform) owns GLWE polynomial w.  in: ct1[NPL] = this wave's polynomial of the GLWE
+// to decompose (coefficient lane + 64 r); acc[r] += from_torus(the product's polynomial w).  `ggsw`: level x
+// (K+1) rows x (K+1) cols x M complex (Fourier layout), highest level first, as the reference's
+// FourierGgswCiphertext.  `pair` = this ciphertext's (K+1) per-wave LDS buffers; t1 / t2 the twiddle tables
+// (LDS copies in the PBS / external-product kernels).
 template <int K, bool L1>
 __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1)[NPL], const cplx* __restrict__ ggsw,
-                                                int base_log, int level, cplx* bufs, const cplx* t2, const Tables& tb,
-                                                int w, int lane) {
-  cplx* buf = bufs + w * BUF;
+                                                int base_log, int level, cplx* pair, const cplx* t1, const cplx* t2,
+                                                const cplx* cm, const cplx* cmi, int w, int lane) {
+  cplx* buf = pair + w * BUF;
   cplx y[16];
   if (L1) {
     cplx u[16];
+    if (base_log <= 31) {  // uniform: digits from the high words, exact in int32
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      u64 s0 = decomp_init_native(ct1[m], base_log, 1), s1 = decomp_init_native(ct1[m + 16], base_log, 1);
-      const u64 d0 = decompose_one_level(base_log, s0), d1 = decompose_one_level(base_log, s1);
-      u[m] = {s64_to_f64(d0), s64_to_f64(d1)};  // convert_forward_integer: into_signed as f64
+      for (int m = 0; m < 16; ++m)
+        u[m] = {(double)decompose_l1_hi((uint32_t)(ct1[m] >> 32), base_log),
+                (double)decompose_l1_hi((uint32_t)(ct1[m + 16] >> 32), base_log)};
+    } else {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        u64 s0 = decomp_init_native(ct1[m], base_log, 1), s1 = decomp_init_native(ct1[m + 16], base_log, 1);
+        const u64 d0 = decompose_one_level(base_log, s0), d1 = decompose_one_level(base_log, s1);
+        u[m] = {s64_to_f64(d0), s64_to_f64(d1)};  // convert_forward_integer: into_signed as f64
+      }
     }
-    fft_fwd(u, buf, tb.t1, t2, tb.cm, lane);
+    fft_fwd(u, buf, t1, t2, cm, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
+    // update_with_fmadd: y_w = sum_rr X_rr * G[rr][w] (own transform from registers, the other K from LDS).
+    // Branch-free (the other rows are rr = o + (o >= w), o < K); the key rows are loaded in two batches of 8
+    // positions, the first issued before the exchange barrier so its latency overlaps the wait.
+    const cplx* gw = ggsw + (size_t)(w * (K + 1) + w) * M + lane;
+    const cplx* go[K];
+    const cplx* xo[K];
+#pragma unroll
+    for (int o = 0; o < K; ++o) {
+      const int rr = o + (o >= w ? 1 : 0);
+      go[o] = ggsw + (size_t)(rr * (K + 1) + w) * M + lane;
+      xo[o] = pair + rr * BUF + lane;
+    }
+    constexpr int HB = 2;
+    cplx kw[HB], ko[K][HB];
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
+      kw[j] = gw[j * 64];
+#pragma unroll
+      for (int o = 0; o < K; ++o) ko[o][j] = go[o][j * 64];
+    }
     __syncthreads();
-    // update_with_fmadd: y_w = sum_rr X_rr * G[rr][w]
-    const cplx* mat = ggsw;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      cplx a = cmul(u[r], mat[((size_t)w * (K + 1) + w) * M + r * 64 + lane]);
+    for (int h = 0; h < 16 / HB; ++h) {
 #pragma unroll
-      for (int rr = 0; rr <= K; ++rr) {
-        if (rr == w) continue;
-        a = cfma(bufs[rr * BUF + r * 64 + lane], mat[((size_t)rr * (K + 1) + w) * M + r * 64 + lane], a);
+      for (int j = 0; j < HB; ++j) {
+        const int r = h * HB + j;
+        cplx a = cmul(u[r], kw[j]);
+#pragma unroll
+        for (int o = 0; o < K; ++o) a = cfma(xo[o][r * 64], ko[o][j], a);
+        y[r] = a;
       }
-      y[r] = a;
+      if (h + 1 < 16 / HB) {
+#pragma unroll
+        for (int j = 0; j < HB; ++j) {
+          const int r = (h + 1) * HB + j;
+          kw[j] = gw[r * 64];
+#pragma unroll
+          for (int o = 0; o < K; ++o) ko[o][j] = go[o][r * 64];
+        }
+      }
     }
     __syncthreads();
   } else {
@@ -349,7 +393,7 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
         const u64 d0 = decompose_one_level(base_log, st[m]), d1 = decompose_one_level(base_log, st[m + 16]);
         u[m] = {s64_to_f64(d0), s64_to_f64(d1)};
       }
-      fft_fwd(u, buf, tb.t1, t2, tb.cm, lane);
+      fft_fwd(u, buf, t1, t2, cm, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
       __syncthreads();
@@ -360,92 +404,119 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
         cplx a = y[r];
 #pragma unroll
         for (int rr = 0; rr <= K; ++rr)
-          a = cfma(bufs[rr * BUF + r * 64 + lane], mat[((size_t)rr * (K + 1) + w) * M + r * 64 + lane], a);
+          a = cfma(pair[rr * BUF + r * 64 + lane], mat[(size_t)(rr * (K + 1) + w) * M + r * 64 + lane], a);
         y[r] = a;
       }
       __syncthreads();
     }
   }
-  fft_inv(y, buf, tb.t1, t2, tb.cmi, lane);
+  fft_inv(y, buf, t1, t2, cmi, lane);
 #pragma unroll
   for (int m = 0; m < 16; ++m) {  // convert_add_backward_torus
-    acc[m] += from_torus(y[m].re);
-    acc[m + 16] += from_torus(y[m].im);
+    acc[m] += from_torus_scaled(y[m].re);
+    acc[m + 16] += from_torus_scaled(y[m].im);
   }
+}
+
+// Workgroup layout of the batched kernels: CT ciphertexts x (K + 1) waves; LDS = CT (K + 1) transpose /
+// exchange buffers + the two twiddle tables, copied once per workgroup.
+template <int K, int CT>
+struct Wg {
+  static constexpr int WAVES = CT * (K + 1), THREADS = 64 * WAVES;
+  cplx bufs[WAVES * BUF];
+  cplx t1[16 * 64];
+  cplx t2[4 * T2S];
+  cplx cm[16], cmi[16];
+};
+
+template <int K, int CT>
+__device__ __forceinline__ void load_tables(Wg<K, CT>& wg, const Tables& tb) {
+  for (int i = threadIdx.x; i < 16 * 64; i += Wg<K, CT>::THREADS) wg.t1[i] = tb.t1[i];
+  if (threadIdx.x < 64) wg.t2[(threadIdx.x >> 4) * T2S + (threadIdx.x & 15)] = tb.t2[threadIdx.x];
+  if (threadIdx.x < 16) {
+    wg.cm[threadIdx.x] = tb.cm[threadIdx.x];
+    wg.cmi[threadIdx.x] = tb.cmi[threadIdx.x];
+  }
+  __syncthreads();
 }
 
 // EXT : out[b] += GGSW (.) glwe[b]                       (add_external_product_assign)
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]    (cmux: ct1 -= ct0; ct0 += ext(ct1))
-template <int K, bool CMUX, bool L1>
+template <int K, bool CMUX, bool L1, int CT>
 __device__ __forceinline__ void ext_product_body(u64* __restrict__ out, u64* __restrict__ glwe,
                                                  const cplx* __restrict__ ggsw, uint32_t batch, int base_log,
-                                                 int level, const Tables& tb, cplx* bufs, cplx* t2) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (threadIdx.x < 64) t2[lane] = tb.t2[lane];
-  __syncthreads();
-  const uint32_t b = blockIdx.x;
-  if (b >= batch) return;  // uniform per workgroup
+                                                 int level, const Tables& tb, Wg<K, CT>& wg) {
+  load_tables(wg, tb);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ct = wave / (K + 1), w = wave % (K + 1);
+  const uint32_t b0 = blockIdx.x * CT + ct;
+  const bool valid = b0 < batch;  // every wave takes part in the barriers
+  const uint32_t b = valid ? b0 : batch - 1;
   u64* in = glwe + ((size_t)b * (K + 1) + w) * N;
   u64* o = out + ((size_t)b * (K + 1) + w) * N;
-  u64 ct[NPL], acc[NPL];
+  u64 ct1[NPL], acc[NPL];
 #pragma unroll
   for (int r = 0; r < NPL; ++r) {
-    ct[r] = in[lane + 64 * r];
+    ct1[r] = in[lane + 64 * r];
     acc[r] = o[lane + 64 * r];
     if (CMUX) {
-      ct[r] -= acc[r];
-      in[lane + 64 * r] = ct[r];
+      ct1[r] -= acc[r];
+      if (valid) in[lane + 64 * r] = ct1[r];
     }
   }
-  ext_product_add<K, L1>(acc, ct, ggsw, base_log, level, bufs, t2, tb, w, lane);
+  ext_product_add<K, L1>(acc, ct1, ggsw, base_log, level, wg.bufs + ct * (K + 1) * BUF, wg.t1, wg.t2, wg.cm, wg.cmi, w, lane);
+  if (valid) {
 #pragma unroll
-  for (int r = 0; r < NPL; ++r) o[lane + 64 * r] = acc[r];
+    for (int r = 0; r < NPL; ++r) o[lane + 64 * r] = acc[r];
+  }
 }
 
-// The shortint shape (k = 1, one level) is held to 256 registers for 2 waves per SIMD; the coverage shapes
-// keep the compiler's choice (more registers, 1 wave per SIMD) instead of spilling.
+// The shortint shape (k = 1, one level) runs 4 ciphertexts per workgroup (8 waves, 153 KiB of LDS, 256
+// registers: 2 waves per SIMD, the twiddle tables shared and the key rows read once per 4 ciphertexts from
+// L1); the coverage shapes one ciphertext per workgroup with the compiler's register choice.
 template <int K, bool CMUX, bool L1>
 __global__ __launch_bounds__(64 * (K + 1)) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                                    const cplx* __restrict__ ggsw, uint32_t batch,
                                                                    int base_log, int level, Tables tb) {
-  __shared__ cplx bufs[(K + 1) * BUF];
-  __shared__ cplx t2[64];
-  ext_product_body<K, CMUX, L1>(out, glwe, ggsw, batch, base_log, level, tb, bufs, t2);
+  __shared__ Wg<K, 1> wg;
+  ext_product_body<K, CMUX, L1, 1>(out, glwe, ggsw, batch, base_log, level, tb, wg);
 }
+constexpr int CT_FAST = 4;
 template <bool CMUX>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void ext_product_kernel_k1l1(
+__global__ __launch_bounds__(128 * CT_FAST) __attribute__((amdgpu_waves_per_eu(2))) void ext_product_kernel_k1l1(
     u64* __restrict__ out, u64* __restrict__ glwe, const cplx* __restrict__ ggsw, uint32_t batch, int base_log,
     int level, Tables tb) {
-  __shared__ cplx bufs[2 * BUF];
-  __shared__ cplx t2[64];
-  ext_product_body<1, CMUX, true>(out, glwe, ggsw, batch, base_log, level, tb, bufs, t2);
+  __shared__ Wg<1, CT_FAST> wg;
+  ext_product_body<1, CMUX, true, CT_FAST>(out, glwe, ggsw, batch, base_log, level, tb, wg);
 }
 
-// algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the workgroup
-template <int T>
-__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int t,
+// algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the TG threads of
+// one ciphertext (gt = index within them; sh = 2 TG u64 of that ciphertext's LDS).  Every thread of the
+// workgroup calls it (barriers).
+template <int TG>
+__device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_lwe, unsigned log_mod, int gt,
                                         u64* sh) {
   u64 sum_half = 0;
   int64_t sum_hed = 0;
-  for (uint32_t i = t; i < n_lwe; i += T) {
+  for (uint32_t i = gt; i < n_lwe; i += TG) {
     const u64 a = lwe[i];
     const int64_t err = (int64_t)((modulus_switch(a, log_mod) << (64u - log_mod)) - a);
     const int64_t half = err / 2;
     sum_half += (u64)half;
     sum_hed += 2 * half - err;
   }
-  sh[t] = sum_half;
-  sh[T + t] = (u64)sum_hed;
+  sh[gt] = sum_half;
+  sh[TG + gt] = (u64)sum_hed;
   __syncthreads();
-  for (int s = T / 2; s > 0; s >>= 1) {
-    if (t < s) {
-      sh[t] += sh[t + s];
-      sh[T + t] = (u64)((int64_t)sh[T + t] + (int64_t)sh[T + t + s]);
+  for (int s = TG / 2; s > 0; s >>= 1) {
+    if (gt < s) {
+      sh[gt] += sh[gt + s];
+      sh[TG + gt] = (u64)((int64_t)sh[TG + gt] + (int64_t)sh[TG + gt + s]);
     }
     __syncthreads();
   }
   const u64 total_half = sh[0];
-  const int64_t total_hed = (int64_t)sh[T];
+  const int64_t total_hed = (int64_t)sh[TG];
   __syncthreads();
   const u64 sum_halving = (u64)(total_hed / 2);
   const u64 half_case = 1ull << (64u - log_mod - 1u);
@@ -455,25 +526,30 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
 // ---- programmable bootstrap (bootstrap.rs:481-521 + blind_rotate_assign :294-381) -------------------
 // lwe_in: batch x (n + 1); lut: (K+1) x N shared; fbsk: n x level x (K+1) x (K+1) x M complex;
 // lwe_out: batch x (K N + 1).  ms_mode: 0 standard, 1 centered, 2 pre-switched (values in [0, 2N)).
-template <int K, bool L1>
+// With several ciphertexts per workgroup a mask element that switches to 0 is not skipped (the reference
+// skips it, bootstrap.rs:336): its CMUX difference is the zero polynomial, whose digits, transforms and
+// products are exactly 0, so the accumulator is unchanged bit for bit either way.
+template <int K, bool L1, int CT>
 __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                          const u64* __restrict__ lut, const cplx* __restrict__ fbsk, uint32_t n_lwe,
                                          uint32_t batch, int base_log, int level, int ms_mode, const Tables& tb,
-                                         cplx* bufs, cplx* t2) {
-  constexpr int T = 64 * (K + 1);
+                                         Wg<K, CT>& wg) {
+  constexpr int TG = 64 * (K + 1);
   constexpr unsigned LOG_MOD = 12;  // PolynomialSize(2048)::to_blind_rotation_input_modulus_log
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t < 64) t2[lane] = tb.t2[lane];
-  __syncthreads();
-  const uint32_t b = blockIdx.x;
-  if (b >= batch) return;
+  load_tables(wg, tb);
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ct = wave / (K + 1), w = wave % (K + 1);
+  const uint32_t b0 = blockIdx.x * CT + ct;
+  const bool valid = b0 < batch;  // every wave takes part in the barriers
+  const uint32_t b = valid ? b0 : batch - 1;
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
   const size_t ggsw_len = (size_t)level * (K + 1) * (K + 1) * M;
-  u64* sh = reinterpret_cast<u64*>(bufs);        // all waves: reductions
-  u64* mine = reinterpret_cast<u64*>(bufs + w * BUF);  // this wave's rotation buffer (2048 u64 = 16 KiB)
+  cplx* pair = wg.bufs + ct * (K + 1) * BUF;
+  u64* mine = reinterpret_cast<u64*>(pair + w * BUF);  // this wave's rotation buffer (2048 u64 = 16 KiB)
 
   u64 body_corr = 0;
-  if (ms_mode == 1) body_corr = centered_body_correction<T>(lwe, n_lwe, LOG_MOD, t, sh);
+  if (ms_mode == 1)
+    body_corr = centered_body_correction<TG>(lwe, n_lwe, LOG_MOD, w * 64 + lane, reinterpret_cast<u64*>(pair));
   const u64 body = (ms_mode == 2) ? (lwe[n_lwe] & (2 * N - 1)) : modulus_switch(lwe[n_lwe] + body_corr, LOG_MOD);
 
   // local accumulator = LUT / X^body (polynomial_wrapping_monic_monomial_div)
@@ -490,27 +566,34 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
     }
   }
 
+  const uint32_t lane_bytes = (uint32_t)lane * 8u;
   for (uint32_t i = 0; i < n_lwe; ++i) {
-    const u64 a = (ms_mode == 2) ? (lwe[i] & (2 * N - 1)) : modulus_switch(lwe[i], LOG_MOD);
-    if (a == 0) continue;  // bootstrap.rs:336 (uniform per workgroup)
-    const int full = (int)(a / N) & 1, rem = (int)(a % N);
+    const uint32_t a = (uint32_t)((ms_mode == 2) ? (lwe[i] & (2 * N - 1)) : modulus_switch(lwe[i], LOG_MOD));
+    if (CT == 1 && a == 0) continue;  // bootstrap.rs:336 (uniform per workgroup)
+    const bool full = (a >> 11) & 1u;
+    const int rem = (int)(a & (N - 1));
 #pragma unroll
     for (int r = 0; r < NPL; ++r) mine[lane + 64 * r] = acc[r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // polynomial_wrapping_monic_monomial_mul_and_subtract: ct1[e] = s_e acc[(e - rem) mod N] - acc[e], s_e = -1 iff
+    // full ^ (e < rem).  With m = s_e < 0 ? ~0 : 0:  s_e v - acc = (v ^ m) - (acc + m).
+    const uint32_t rot = (lane_bytes - (uint32_t)rem * 8u) & (8u * N - 1u);  // byte offset of e = lane, r = 0
+    const char* mbase = reinterpret_cast<const char*>(mine);
     u64 ct1[NPL];
 #pragma unroll
-    for (int r = 0; r < NPL; ++r) {  // polynomial_wrapping_monic_monomial_mul_and_subtract
-      const int e = lane + 64 * r;
-      u64 v = mine[(e - rem) & (N - 1)];
-      if (full ^ (e < rem)) v = (u64)0 - v;
-      ct1[r] = v - acc[r];
+    for (int r = 0; r < NPL; ++r) {
+      const u64 v = *reinterpret_cast<const u64*>(mbase + ((rot + 512u * r) & (8u * N - 1u)));
+      const bool wrapped = lane < rem - 64 * r;
+      const uint32_t m = (wrapped != full) ? ~0u : 0u;
+      const u64 mm = ((u64)m << 32) | m;
+      ct1[r] = (v ^ mm) - (acc[r] + mm);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    ext_product_add<K, L1>(acc, ct1, fbsk + (size_t)i * ggsw_len, base_log, level, bufs, t2, tb, w, lane);
+    ext_product_add<K, L1>(acc, ct1, fbsk + (size_t)i * ggsw_len, base_log, level, pair, wg.t1, wg.t2, wg.cm, wg.cmi, w, lane);
   }
 
   // extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160), nth = 0
@@ -521,12 +604,14 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (valid) {
 #pragma unroll
-    for (int r = 0; r < NPL; ++r) {
-      const int j = lane + 64 * r;
-      out[(size_t)w * N + j] = (j == 0) ? mine[0] : (u64)0 - mine[N - j];
+      for (int r = 0; r < NPL; ++r) {
+        const int j = lane + 64 * r;
+        out[(size_t)w * N + j] = (j == 0) ? mine[0] : (u64)0 - mine[N - j];
+      }
     }
-  } else if (lane == 0) {
+  } else if (lane == 0 && valid) {
     out[(size_t)K * N] = acc[0];
   }
 }
@@ -536,16 +621,14 @@ __global__ __launch_bounds__(64 * (K + 1)) void pbs_kernel(u64* __restrict__ lwe
                                                            const u64* __restrict__ lut, const cplx* __restrict__ fbsk,
                                                            uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                            int ms_mode, Tables tb) {
-  __shared__ cplx bufs[(K + 1) * BUF];
-  __shared__ cplx t2[64];
-  pbs_body<K, L1>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, bufs, t2);
+  __shared__ Wg<K, 1> wg;
+  pbs_body<K, L1, 1>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
 }
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void pbs_kernel_k1l1(
+__global__ __launch_bounds__(128 * CT_FAST) __attribute__((amdgpu_waves_per_eu(2))) void pbs_kernel_k1l1(
     u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in, const u64* __restrict__ lut,
     const cplx* __restrict__ fbsk, uint32_t n_lwe, uint32_t batch, int base_log, int level, int ms_mode, Tables tb) {
-  __shared__ cplx bufs[2 * BUF];
-  __shared__ cplx t2[64];
-  pbs_body<1, true>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, bufs, t2);
+  __shared__ Wg<1, CT_FAST> wg;
+  pbs_body<1, true, CT_FAST>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
 }
 
 }  // namespace fft
@@ -576,8 +659,8 @@ template <int K, bool CMUX, bool L1>
 static hipError_t ext_one(uint64_t* out, uint64_t* glwe, const fft::cplx* g, size_t batch, int base_log, int level,
                           const FftTables& t, hipStream_t s) {
   if (K == 1 && L1)
-    hipLaunchKernelGGL((fft::ext_product_kernel_k1l1<CMUX>), dim3((unsigned)batch), dim3(128), 0, s, out, glwe, g,
-                       (uint32_t)batch, base_log, level, tables(t));
+    hipLaunchKernelGGL((fft::ext_product_kernel_k1l1<CMUX>), dim3((unsigned)((batch + fft::CT_FAST - 1) / fft::CT_FAST)),
+                       dim3(128 * fft::CT_FAST), 0, s, out, glwe, g, (uint32_t)batch, base_log, level, tables(t));
   else
     hipLaunchKernelGGL((fft::ext_product_kernel<K, CMUX, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out,
                        glwe, g, (uint32_t)batch, base_log, level, tables(t));
@@ -607,8 +690,9 @@ template <int K, bool L1>
 static hipError_t pbs_one(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const fft::cplx* g, size_t n_lwe,
                           size_t batch, int base_log, int level, int ms_mode, const FftTables& t, hipStream_t s) {
   if (K == 1 && L1)
-    hipLaunchKernelGGL(fft::pbs_kernel_k1l1, dim3((unsigned)batch), dim3(128), 0, s, out, lwe_in, lut, g,
-                       (uint32_t)n_lwe, (uint32_t)batch, base_log, level, ms_mode, tables(t));
+    hipLaunchKernelGGL(fft::pbs_kernel_k1l1, dim3((unsigned)((batch + fft::CT_FAST - 1) / fft::CT_FAST)),
+                       dim3(128 * fft::CT_FAST), 0, s, out, lwe_in, lut, g, (uint32_t)n_lwe, (uint32_t)batch, base_log,
+                       level, ms_mode, tables(t));
   else
     hipLaunchKernelGGL((fft::pbs_kernel<K, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out, lwe_in, lut, g,
                        (uint32_t)n_lwe, (uint32_t)batch, base_log, level, ms_mode, tables(t));

@@ -68,6 +68,35 @@
 #define I_ADDPAIR(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n s_nop 1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
 #define I_ADDPAIR_NONOP(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
 
+// f64 (FFT PBS path)
+#define I_FADD(x, k) asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(fb));
+#define I_FMUL(x, k) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(x) : "v"(fb));
+#define I_FFMA(x, k) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x) : "v"(fb), "v"(fc));
+#define I_FFMAC(x, k) asm volatile("v_fmac_f64_e32 %0, %1, %2" : "+v"(x) : "v"(fb), "v"(fc));
+#define I_FRND(x, k) asm volatile("v_rndne_f64 %0, %0" : "+v"(x));
+#define I_FCVT(x, k) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(x) : "v"(b));
+#define I_FPKFMA(x, k) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(fb), "v"(fc));
+#define FKERNEL(NAME, INS)                                                                   \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t s0, uint32_t s1, uint64_t* clk) { \
+    double a0 = s0 + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7; \
+    double fb = 1.0000001 * s1, fc = 0.5 * s0;                                               \
+    uint32_t b = s1 ^ threadIdx.x;                                                           \
+    uint64_t t0 = __builtin_amdgcn_s_memtime();                                              \
+    uint64_t r0 = __builtin_amdgcn_s_memrealtime();                                          \
+    for (int i = 0; i < ITERS; ++i) { BODY8(INS) }                                           \
+    uint64_t t1 = __builtin_amdgcn_s_memtime();                                              \
+    uint64_t r1 = __builtin_amdgcn_s_memrealtime();                                          \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7); \
+    if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t1 - t0; clk[2 * blockIdx.x + 1] = r1 - r0; } \
+  }
+FKERNEL(k_fadd, I_FADD)
+FKERNEL(k_fmul, I_FMUL)
+FKERNEL(k_ffma, I_FFMA)
+FKERNEL(k_ffmac, I_FFMAC)
+FKERNEL(k_frnd, I_FRND)
+FKERNEL(k_fcvt, I_FCVT)
+FKERNEL(k_fpkfma, I_FPKFMA)
+
 KERNEL(k_add, uint32_t, I_ADD)
 KERNEL(k_xor, uint32_t, I_XOR)
 KERNEL(k_mov, uint32_t, I_MOV)
@@ -119,6 +148,8 @@ int main(int argc, char** argv) {
       {"v_sub_u32_e32", k_subu32}, {"v_lshrrev_b32_e32", k_lshr32}, {"v_lshrrev_b64", k_lshr64}, {"v_not_b32", k_not32},
       {"v_mul_u32_u24_e32", k_mul24}, {"v_mul_hi_u32_u24_e32", k_mulhi24}, {"v_mul_lo_u32", k_mullo}, {"v_bfi_b32", k_bfi},
       {"v_perm_b32", k_perm}, {"s_nop 1", k_nop1}, {"addco+nop1+addc (3 ins)", k_addpair}, {"addco+addc no nop", k_addpair_nonop},
+      {"v_add_f64", k_fadd}, {"v_mul_f64", k_fmul}, {"v_fma_f64", k_ffma}, {"v_fmac_f64_e32", k_ffmac},
+      {"v_rndne_f64", k_frnd}, {"v_cvt_f64_i32", k_fcvt}, {"v_pk_fma_f32", k_fpkfma},
   };
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
