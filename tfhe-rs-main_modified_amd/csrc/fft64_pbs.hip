@@ -218,14 +218,27 @@ __device__ __forceinline__ double s64_to_f64(u64 x) { return (double)(int64_t)x;
 // words are read from the mantissas of hi + 1.5 2^52 and lo + 2^52.  round-half-even instead of half-away-from-
 // zero: different only for an exact half-integer y, where the reference also saturates +2^63 (to i64::MAX; here
 // it wraps to 2^63).
-__device__ __forceinline__ u64 from_torus_scaled(double y) {
+__device__ __forceinline__ void torus_words(double y, uint32_t& h, uint32_t& l) {
   const double r = __builtin_rint(y);
   const double z = __fma_rn(-__builtin_rint(r * 0x1p-64), 0x1p64, r);
   const double hi = __builtin_floor(z * 0x1p-32);
   const double lo = __fma_rn(-hi, 0x1p32, z);
-  const uint32_t h = (uint32_t)__double_as_longlong(hi + 0x1.8p52);
-  const uint32_t l = (uint32_t)__double_as_longlong(lo + 0x1p52);
+  h = (uint32_t)__double_as_longlong(hi + 0x1.8p52);
+  l = (uint32_t)__double_as_longlong(lo + 0x1p52);
+}
+__device__ __forceinline__ u64 from_torus_scaled(double y) {
+  uint32_t h, l;
+  torus_words(y, h, l);
   return ((u64)h << 32) | l;
+}
+// acc += from_torus_scaled(y) as one 32-bit add with carry per word
+__device__ __forceinline__ void add_torus_scaled(u64& acc, double y) {
+  uint32_t h, l;
+  torus_words(y, h, l);
+  const uint32_t alo = (uint32_t)acc, ahi = (uint32_t)(acc >> 32);
+  const uint32_t nlo = alo + l;
+  const uint32_t nhi = ahi + h + (nlo < alo ? 1u : 0u);
+  acc = ((u64)nhi << 32) | nlo;
 }
 
 // ---- decomposition (commons/math/decomposition/decomposer.rs:156-185, iter.rs:131-151) ------------
@@ -307,16 +320,60 @@ __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, c
   }
 }
 
+// Synchronisation of the (K + 1) waves of one ciphertext.  A workgroup holding one ciphertext uses its barrier;
+// with several ciphertexts per workgroup each wave publishes a step counter in LDS and waits for its partners'
+// (s_sleep between polls), so the ciphertexts of a workgroup do not have to run in lockstep.
+template <int K, bool WG_BARRIER>
+struct PairSync {
+  uint32_t* flags;  // this ciphertext's K + 1 counters (LDS)
+  int w;
+  uint32_t count;
+  __device__ __forceinline__ void sync() {
+    if (WG_BARRIER) {
+      __syncthreads();
+      return;
+    }
+    ++count;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    *reinterpret_cast<volatile uint32_t*>(flags + w) = count;
+    // wait (in one asm block, so the register allocator sees straight-line code) until every partner's counter
+    // has reached ours: poll with ds_read_b32, the decision on the first lane's value (all lanes read the same
+    // address), s_sleep between polls
+#pragma unroll
+    for (int o = 0; o < K; ++o) {
+      const int rr = o + (o >= w ? 1 : 0);
+      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(flags + rr);
+      uint32_t v, sv;
+      asm volatile(
+          "s_waitcnt lgkmcnt(0)\n"
+          "1:\n\t"
+          "ds_read_b32 %0, %2\n\t"
+          "s_waitcnt lgkmcnt(0)\n\t"
+          "v_readfirstlane_b32 %1, %0\n\t"
+          "s_cmp_ge_u32 %1, %3\n\t"
+          "s_cbranch_scc1 2f\n\t"
+          "s_sleep 1\n\t"
+          "s_branch 1b\n"
+          "2:"
+          : "=&v"(v), "=&s"(sv)
+          : "v"(lds), "s"(count)
+          : "memory", "scc");
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+};
+
 // ---- external product on registers ----------------------------------------------------------------
 // Wave w (< K + 1, wave-uniform) owns GLWE polynomial w.  in: ct1[NPL] = this wave's polynomial of the GLWE
 // to decompose (coefficient lane + 64 r); acc[r] += from_torus(the product's polynomial w).  `ggsw`: level x
 // (K+1) rows x (K+1) cols x M complex (Fourier layout), highest level first, as the reference's
 // FourierGgswCiphertext.  `pair` = this ciphertext's (K+1) per-wave LDS buffers; t1 / t2 the twiddle tables
 // (LDS copies in the PBS / external-product kernels).
-template <int K, bool L1>
+template <int K, bool L1, bool WGB>
 __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1)[NPL], const cplx* __restrict__ ggsw,
                                                 int base_log, int level, cplx* pair, const cplx* t1, const cplx* t2,
-                                                const cplx* cm, const cplx* cmi, int w, int lane) {
+                                                const cplx* cm, const cplx* cmi, int w, int lane,
+                                                PairSync<K, WGB>& ps) {
   cplx* buf = pair + w * BUF;
   cplx y[16];
   if (L1) {
@@ -357,7 +414,7 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
 #pragma unroll
       for (int o = 0; o < K; ++o) ko[o][j] = go[o][j * 64];
     }
-    __syncthreads();
+    ps.sync();
 #pragma unroll
     for (int h = 0; h < 16 / HB; ++h) {
 #pragma unroll
@@ -378,7 +435,7 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
         }
       }
     }
-    __syncthreads();
+    ps.sync();
   } else {
     u64 st[NPL];
 #pragma unroll
@@ -396,7 +453,7 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
       fft_fwd(u, buf, t1, t2, cm, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
-      __syncthreads();
+      ps.sync();
       // the decomposition iterator yields the least significant level first, which the GGSW stores first
       const cplx* mat = ggsw + (size_t)li * (K + 1) * (K + 1) * M;
 #pragma unroll
@@ -407,14 +464,14 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
           a = cfma(pair[rr * BUF + r * 64 + lane], mat[(size_t)(rr * (K + 1) + w) * M + r * 64 + lane], a);
         y[r] = a;
       }
-      __syncthreads();
+      ps.sync();
     }
   }
   fft_inv(y, buf, t1, t2, cmi, lane);
 #pragma unroll
   for (int m = 0; m < 16; ++m) {  // convert_add_backward_torus
-    acc[m] += from_torus_scaled(y[m].re);
-    acc[m + 16] += from_torus_scaled(y[m].im);
+    add_torus_scaled(acc[m], y[m].re);
+    add_torus_scaled(acc[m + 16], y[m].im);
   }
 }
 
@@ -427,6 +484,7 @@ struct Wg {
   cplx t1[16 * 64];
   cplx t2[4 * T2S];
   cplx cm[16], cmi[16];
+  uint32_t flags[WAVES];
 };
 
 template <int K, int CT>
@@ -437,6 +495,7 @@ __device__ __forceinline__ void load_tables(Wg<K, CT>& wg, const Tables& tb) {
     wg.cm[threadIdx.x] = tb.cm[threadIdx.x];
     wg.cmi[threadIdx.x] = tb.cmi[threadIdx.x];
   }
+  if (threadIdx.x < Wg<K, CT>::WAVES) wg.flags[threadIdx.x] = 0;
   __syncthreads();
 }
 
@@ -464,7 +523,9 @@ __device__ __forceinline__ void ext_product_body(u64* __restrict__ out, u64* __r
       if (valid) in[lane + 64 * r] = ct1[r];
     }
   }
-  ext_product_add<K, L1>(acc, ct1, ggsw, base_log, level, wg.bufs + ct * (K + 1) * BUF, wg.t1, wg.t2, wg.cm, wg.cmi, w, lane);
+  PairSync<K, CT == 1> ps{wg.flags + ct * (K + 1), w, 0u};
+  ext_product_add<K, L1>(acc, ct1, ggsw, base_log, level, wg.bufs + ct * (K + 1) * BUF, wg.t1, wg.t2, wg.cm, wg.cmi, w,
+                         lane, ps);
   if (valid) {
 #pragma unroll
     for (int r = 0; r < NPL; ++r) o[lane + 64 * r] = acc[r];
@@ -567,6 +628,8 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
   }
 
   const uint32_t lane_bytes = (uint32_t)lane * 8u;
+  PairSync<K, CT == 1> ps{wg.flags + ct * (K + 1), w, 0u};
+
   for (uint32_t i = 0; i < n_lwe; ++i) {
     const uint32_t a = (uint32_t)((ms_mode == 2) ? (lwe[i] & (2 * N - 1)) : modulus_switch(lwe[i], LOG_MOD));
     if (CT == 1 && a == 0) continue;  // bootstrap.rs:336 (uniform per workgroup)
@@ -579,13 +642,18 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // polynomial_wrapping_monic_monomial_mul_and_subtract: ct1[e] = s_e acc[(e - rem) mod N] - acc[e], s_e = -1 iff
     // full ^ (e < rem).  With m = s_e < 0 ? ~0 : 0:  s_e v - acc = (v ^ m) - (acc + m).
-    const uint32_t rot = (lane_bytes - (uint32_t)rem * 8u) & (8u * N - 1u);  // byte offset of e = lane, r = 0
-    const char* mbase = reinterpret_cast<const char*>(mine);
+    // Source of e = lane + 64 r: (e - rem) mod N at byte rot + 512 r (no wrap: e >= rem) or that minus 16 KiB.
+    // Lanes >= rem never wrap; below rem, e < rem holds exactly for the wrapped sources, which are the
+    // in-range ones — so one per-lane base (A or A - 16 KiB) selected by the same compare as the sign, and the
+    // 512 r in the instruction's offset field.
+    const uint32_t rot = (lane_bytes - (uint32_t)rem * 8u) & (8u * N - 1u);
+    const char* base_a = reinterpret_cast<const char*>(mine) + rot;
+    const char* base_b = lane >= rem ? base_a : base_a - 8 * N;
     u64 ct1[NPL];
 #pragma unroll
     for (int r = 0; r < NPL; ++r) {
-      const u64 v = *reinterpret_cast<const u64*>(mbase + ((rot + 512u * r) & (8u * N - 1u)));
       const bool wrapped = lane < rem - 64 * r;
+      const u64 v = *reinterpret_cast<const u64*>((wrapped ? base_a : base_b) + 512 * r);
       const uint32_t m = (wrapped != full) ? ~0u : 0u;
       const u64 mm = ((u64)m << 32) | m;
       ct1[r] = (v ^ mm) - (acc[r] + mm);
@@ -593,7 +661,8 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    ext_product_add<K, L1>(acc, ct1, fbsk + (size_t)i * ggsw_len, base_log, level, pair, wg.t1, wg.t2, wg.cm, wg.cmi, w, lane);
+    ext_product_add<K, L1>(acc, ct1, fbsk + (size_t)i * ggsw_len, base_log, level, pair, wg.t1, wg.t2, wg.cm, wg.cmi, w,
+                           lane, ps);
   }
 
   // extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160), nth = 0
