@@ -524,6 +524,52 @@ def bench_ks_pbs(args, eng, torch, dev, world, barrier):
                        "batch_per_gpu": batch}}
 
 
+def bench_ks_pbs_fft(args, eng, torch, dev, world, barrier):
+    """The shortint server key's KS-PBS as tfhe-rs runs it by default: keyswitch (2048 -> 918, B 2^4, L 4) then the
+    f64-FFT PBS (n 918, N 2048, B 2^23, L 1), both keys resident, one stream."""
+    KS, F = eng.lwe_keyswitch, eng.fft64
+    batch, n_lwe = args.pbs_batch, PBS_N_LWE
+    ksk = torch.empty((KS_IN, KS_LEVEL, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ksk, SEED + 40, 0)
+    kkey = KS.LweKeyswitchKey(ksk, KS_BASE_LOG, KS_LEVEL)
+    del ksk
+    fft = F.Fft(N, dev.index)
+    std = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(std, SEED + 80, 0)
+    fbsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N // 2, 2), dtype=torch.float64, device=dev)
+    F.convert_standard_lwe_bootstrap_key_to_fourier(std, fbsk, fft)
+    del std
+    bkey = F.FourierLweBootstrapKey(fbsk, PBS_BASE_LOG, PBS_LEVEL, fft)
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 11, 0)
+    big = torch.empty((batch, KS_IN + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(big, SEED + 42, 0)
+    small = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+
+    def run():
+        KS.keyswitch_lwe_ciphertext(kkey, big, small)
+        F.programmable_bootstrap_lwe_ciphertext(small, out, lut, bkey)
+
+    run()
+    torch.cuda.synchronize()
+    K = args.pbs_steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        run()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    del bkey, kkey
+    return {"metric": "KS-PBS/sec, default shortint path (keyswitch then f64-FFT PBS), PARAM_MESSAGE_2_CARRY_2 shape",
+            "value": world * batch * K / el, "unit": "KS-PBS/s", "ms_per_step": el / K * 1e3, "steps": K,
+            "config": {"workload": "keyswitch_lwe_ciphertext 2048 -> 918 (B 2^4, L 4) then "
+                                   "programmable_bootstrap_lwe_ciphertext (f64 FFT; n 918, N 2048, B 2^23, L 1), one stream",
+                       "batch_per_gpu": batch}}
+
+
 def cpu_baseline_ks(seconds: float):
     """Oracle restatement of keyswitch_lwe_ciphertext_native_mod_compatible, OpenMP over ciphertexts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -702,6 +748,7 @@ def main():
         out["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, world, barrier)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
         out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
+        out["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier)
         out["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
