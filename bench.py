@@ -718,6 +718,7 @@ def main():
             "batch_per_gpu": batch,
             "global_batch": batch * world,
             "parallelism": f"independent shards x{world} (no data-path collective)",
+            "hip_runtime": eng._lib.hip_runtimes(),
         },
         "kernels": {"timed_launch_ms": launch_ms, "fwd_ms": fwd_ms, "inv_ms": inv_ms,
                     "note": "timed_launch_ms: HIP events around the timed region / (2 K launches); "

@@ -64,3 +64,17 @@ def test_header_compiles_as_c(tmp_path):
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c",
                         str(src), "-o", str(tmp_path / "t.o")], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_single_hip_runtime_in_process(engine):
+    """The engine shares the process's HIP runtime (SONAME libamdhip64.so.7): after torch and the engine have both
+    run GPU work, exactly one libamdhip64 is mapped ('two HIP runtimes' — this pins that there is one
+    per process, whichever the process loaded first)."""
+    import torch
+    plan = engine.Plan.try_new(64, 0xFFFFFFFF00000001)
+    t = torch.zeros(4 * 64, dtype=torch.int64, device="cuda")
+    plan.fwd(t.view(4, 64))
+    torch.cuda.synchronize()
+    paths = engine._lib.hip_runtimes()
+    assert len(paths) == 1, paths

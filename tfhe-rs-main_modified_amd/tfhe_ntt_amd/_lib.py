@@ -152,6 +152,21 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+def hip_runtimes() -> list[str]:
+    """Paths of every libamdhip64 mapped into this process (/proc/self/maps).  The engine links
+    ``libamdhip64.so.7`` by SONAME, so in a process where torch has already loaded its bundled runtime the engine
+    shares that one (one HIP runtime per process); without torch it resolves /opt/rocm's through its RUNPATH."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return sorted(paths)
+
+
 def check(status: int) -> None:
     if status != MI_OK:
         L = lib()
