@@ -176,17 +176,19 @@ inline void convert_standard_lwe_bootstrap_key_to_ntt64(const prime64::Plan& pla
   check(mi_bsk_to_ntt64(plan.raw(), bsk_std, bsk_ntt, n_polys, in_modulus_width, normalize ? 1 : 0, stream));
 }
 
-// ntt64_pbs.rs:553-663 / ntt64_bnf_pbs.rs:541-681: out[b] += GGSW (.) glwe[b]
+// ntt64_pbs.rs:553-663 / ntt64_bnf_pbs.rs:541-681: out[b] += GGSW (.) glwe[b]; `glwe_dimension` = k
 inline void add_external_product_ntt64_assign(const prime64::Plan& plan, uint64_t* out, const uint64_t* glwe,
                                               const uint64_t* ggsw_ntt, int base_log, int level, size_t batch,
-                                              int variant, void* stream = nullptr) {
-  check(mi_ext_product_ntt64_batch(plan.raw(), out, glwe, ggsw_ntt, 1, base_log, level, batch, variant, stream));
+                                              int variant, void* stream = nullptr, int glwe_dimension = 1) {
+  check(mi_ext_product_ntt64_batch(plan.raw(), out, glwe, ggsw_ntt, glwe_dimension, base_log, level, batch, variant,
+                                   stream));
 }
 
 // ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705 (ct1 is left holding ct1 - ct0, as the reference)
 inline void cmux_ntt64_assign(const prime64::Plan& plan, uint64_t* ct0, uint64_t* ct1, const uint64_t* ggsw_ntt,
-                              int base_log, int level, size_t batch, int variant, void* stream = nullptr) {
-  check(mi_cmux_ntt64_batch(plan.raw(), ct0, ct1, ggsw_ntt, 1, base_log, level, batch, variant, stream));
+                              int base_log, int level, size_t batch, int variant, void* stream = nullptr,
+                              int glwe_dimension = 1) {
+  check(mi_cmux_ntt64_batch(plan.raw(), ct0, ct1, ggsw_ntt, glwe_dimension, base_log, level, batch, variant, stream));
 }
 
 // An NTT-domain bootstrap key bound to a plan (entities/ntt_lwe_bootstrap_key.rs); move-only.
@@ -194,9 +196,9 @@ class NttBootstrapKey {
  public:
   // `stream`: the stream that produced bsk_ntt (the BNF preparation is ordered after it)
   NttBootstrapKey(const prime64::Plan& plan, const uint64_t* bsk_ntt, size_t n_lwe, int base_log, int level,
-                  int variant, void* stream = nullptr)
+                  int variant, void* stream = nullptr, int glwe_dimension = 1)
       : n_lwe_(n_lwe), variant_(variant) {
-    check(mi_pbs_ntt64_key_create(plan.raw(), bsk_ntt, n_lwe, 1, base_log, level, variant, stream, &raw_));
+    check(mi_pbs_ntt64_key_create(plan.raw(), bsk_ntt, n_lwe, glwe_dimension, base_log, level, variant, stream, &raw_));
   }
   // Serialised key bytes (MI_NTT_BSK_PLAIN / MI_NTT_BSK_VERSIONED) loaded straight into HBM
   // (mi_pbs_ntt64_key_load); `variant` is explicit: Raw (BNF) and Normalize (Solinas) keys store the same fields.
@@ -293,6 +295,76 @@ inline NttBskFields deserialize_ntt_bsk(const uint8_t* buf, size_t len, std::vec
 }
 
 }  // namespace core_crypto
+
+// ---- the f64-FFT path (tfhe/src/core_crypto/fft_impl/fft64, algorithms/lwe_programmable_bootstrapping/
+// fft64_pbs.rs): Fourier buffers are interleaved (re, im) doubles in the engine's frequency order ------------
+namespace fft64 {
+
+// Fft::new (fft_impl/fft64/math/fft/mod.rs:170-223): the process-wide plan of a polynomial size on a device.
+class Fft {
+ public:
+  explicit Fft(size_t polynomial_size, int device = 0) { check(mi_fft64_plan_cached(polynomial_size, device, &raw_)); }
+  const mi_fft64_plan* raw() const noexcept { return raw_; }
+  // FftView::forward_as_torus / backward_as_torus / add_backward_as_torus over `batch` polynomials
+  void forward_as_torus(double* fourier, const uint64_t* standard, size_t batch, void* stream = nullptr) const {
+    check(mi_fft64_forward_torus_batch(raw_, fourier, standard, batch, stream));
+  }
+  void backward_as_torus(uint64_t* standard, const double* fourier, size_t batch, bool add = false,
+                         void* stream = nullptr) const {
+    check(mi_fft64_backward_torus_batch(raw_, standard, fourier, batch, add ? 1 : 0, stream));
+  }
+
+ private:
+  const mi_fft64_plan* raw_ = nullptr;
+};
+
+// convert_standard_lwe_bootstrap_key_to_fourier (algorithms/lwe_bootstrap_key_conversion.rs:20-43)
+inline void convert_standard_lwe_bootstrap_key_to_fourier(const Fft& fft, const uint64_t* bsk_std, double* bsk_fourier,
+                                                          size_t n_polys, void* stream = nullptr) {
+  check(mi_bsk_to_fourier64(fft.raw(), bsk_std, bsk_fourier, n_polys, stream));
+}
+
+// add_external_product_assign / cmux_assign (fft64_pbs.rs:270-330, 510-560)
+inline void add_external_product_assign(const Fft& fft, uint64_t* out, const uint64_t* glwe, const double* ggsw_fourier,
+                                        int base_log, int level, size_t batch, void* stream = nullptr,
+                                        int glwe_dimension = 1) {
+  check(mi_fft64_ext_product_batch(fft.raw(), out, glwe, ggsw_fourier, glwe_dimension, base_log, level, batch, stream));
+}
+inline void cmux_assign(const Fft& fft, uint64_t* ct0, uint64_t* ct1, const double* ggsw_fourier, int base_log,
+                        int level, size_t batch, void* stream = nullptr, int glwe_dimension = 1) {
+  check(mi_fft64_cmux_batch(fft.raw(), ct0, ct1, ggsw_fourier, glwe_dimension, base_log, level, batch, stream));
+}
+
+// FourierLweBootstrapKey bound to a plan (the Fourier key buffer is referenced; keep it alive); move-only
+class FourierBootstrapKey {
+ public:
+  FourierBootstrapKey(const Fft& fft, const double* fbsk, size_t n_lwe, int base_log, int level,
+                      int glwe_dimension = 1)
+      : n_lwe_(n_lwe) {
+    check(mi_fft64_pbs_key_create(fft.raw(), fbsk, n_lwe, glwe_dimension, base_log, level, &raw_));
+  }
+  FourierBootstrapKey(FourierBootstrapKey&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_) {}
+  FourierBootstrapKey(const FourierBootstrapKey&) = delete;
+  FourierBootstrapKey& operator=(const FourierBootstrapKey&) = delete;
+  ~FourierBootstrapKey() {
+    if (raw_) (void)mi_fft64_pbs_key_destroy(raw_);
+  }
+  const mi_fft64_pbs_key* raw() const noexcept { return raw_; }
+  size_t input_lwe_dimension() const noexcept { return n_lwe_; }
+
+ private:
+  mi_fft64_pbs_key* raw_ = nullptr;
+  size_t n_lwe_;
+};
+
+// programmable_bootstrap_lwe_ciphertext (fft64_pbs.rs:924-1060) over a batch
+inline void programmable_bootstrap_lwe_ciphertext(const FourierBootstrapKey& key, const uint64_t* lwe_in,
+                                                  uint64_t* lwe_out, const uint64_t* lut, size_t batch,
+                                                  int ms_mode = MI_MS_STANDARD, void* stream = nullptr) {
+  check(mi_fft64_pbs_batch(key.raw(), lwe_out, lwe_in, lut, batch, ms_mode, stream));
+}
+
+}  // namespace fft64
 }  // namespace tfhe_ntt_amd
 
 // The staging buffer uses the HIP runtime directly (the only HIP dependency of this header).

@@ -5,10 +5,13 @@
 //   add_external_product_ntt64_assign (BNF)        ntt64_bnf_pbs.rs:541-681
 //   programmable_bootstrap_ntt64_lwe_ciphertext    ntt64_bnf_pbs.rs:469-540 (standard modulus switch)
 //   keyswitch_lwe_ciphertext                       lwe_keyswitch.rs:137-227 (2048 -> 918, B 2^4, L 4)
+// and the f64-FFT mirror (namespace fft64) against exact integer arithmetic within the f64 error bound:
+//   forward_as_torus -> backward_as_torus round trip, add_external_product_assign vs the exact negacyclic product
 // Needs a HIP device.  Build: make -C tests/cpp.
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -129,6 +132,65 @@ int main() {
       threw = e.status() == MI_ERR_INVALID_ARG;
     }
     EXPECT(threw);
+  }
+
+  // f64 FFT: round trip and an external product (k = 1, level 1, base 2^23) vs the exact product in Z_2^64[X]/(X^N+1)
+  {
+    tfhe_ntt_amd::fft64::Fft fft(N);
+    const size_t batch = 2;
+    const auto x = uniform(109, 0, batch * N);
+    Dev d_x(x), d_back(batch * N);
+    double* four = nullptr;
+    EXPECT(hipMalloc(reinterpret_cast<void**>(&four), batch * N * 8) == hipSuccess);
+    fft.forward_as_torus(four, d_x.p, batch);
+    fft.backward_as_torus(d_back.p, four, batch);
+    const auto back = d_back.host();
+    int64_t worst = 0;
+    for (size_t i = 0; i < x.size(); ++i) {
+      const int64_t d = (int64_t)(back[i] - x[i]);
+      worst = std::max(worst, d < 0 ? -d : d);
+    }
+    EXPECT(worst < (int64_t(1) << 16));
+    (void)hipFree(four);
+
+    const int bl = 23;
+    const auto ggsw = uniform(110, 0, 4 * N), glwe = uniform(111, 0, 2 * N), out0 = uniform(112, 0, 2 * N);
+    double* fg = nullptr;
+    EXPECT(hipMalloc(reinterpret_cast<void**>(&fg), 4 * N * 8) == hipSuccess);
+    Dev d_g(ggsw), d_in(glwe), d_out(out0);
+    tfhe_ntt_amd::fft64::convert_standard_lwe_bootstrap_key_to_fourier(fft, d_g.p, fg, 4);
+    tfhe_ntt_amd::fft64::add_external_product_assign(fft, d_out.p, d_in.p, fg, bl, 1, 1);
+    const auto got = d_out.host();
+    // exact: decomposition digit (decomposer.rs, level 1) of each GLWE coefficient, negacyclic products mod 2^64
+    std::vector<int64_t> dig(2 * N);
+    for (size_t i = 0; i < 2 * N; ++i) {
+      const uint64_t v = glwe[i];
+      uint64_t res = v >> (64 - bl - 1);
+      const uint64_t rb = res & 1;
+      res = ((res + 1) >> 1) & ((1ull << bl) - 1);
+      const uint64_t nb = (((res - 1) | (rb << (bl - 1))) & res) >> (bl - 1);
+      const int64_t st = (int64_t)(res - (nb << bl));
+      const uint64_t r = (uint64_t)st & ((1ull << bl) - 1);
+      const uint64_t s2 = (uint64_t)(st >> bl);
+      const uint64_t carry = (((r - 1) | s2) & r) >> (bl - 1);
+      dig[i] = (int64_t)(r - (carry << bl));
+    }
+    worst = 0;
+    for (int c = 0; c < 2; ++c)
+      for (size_t e = 0; e < N; ++e) {
+        uint64_t acc = out0[c * N + e];
+        for (int r = 0; r < 2; ++r)
+          for (size_t j = 0; j < N; ++j) {  // coefficient e of X^j * G[r][c], times digit j of row r
+            const size_t src = (e + N - j) % N;
+            const uint64_t g = ggsw[(r * 2 + c) * N + src];
+            const uint64_t t = (uint64_t)dig[r * N + j] * g;
+            acc += (e >= j) ? t : (uint64_t)0 - t;
+          }
+        const int64_t d = (int64_t)(got[c * N + e] - acc);
+        worst = std::max(worst, d < 0 ? -d : d);
+      }
+    EXPECT(worst < (int64_t(1) << 48));
+    (void)hipFree(fg);
   }
 
   if (g_failures) {
