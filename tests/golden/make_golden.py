@@ -13,7 +13,8 @@ each fixture is self-checked here against those properties before it is written:
 Moduli: the six primes of the reference's test_product (prime64.rs:1308-1315) plus the 61-bit
 prime of the pointwise tests (prime64.rs:1460) and the prime32 doc-example prime (lib.rs:31).
 
-Run:  python tests/golden/make_golden.py     (writes tests/golden/prime64_p<p>_n<n>.npz)
+Run:  python tests/golden/make_golden.py     (writes tests/golden/prime64_p<p>_n<n>.npz, large_solinas_n*.npz and
+      consumers_n2048.npz — the external product / CMUX / key conversion / PBS cases)
 """
 import os
 import sys
@@ -89,7 +90,57 @@ def make_large(n):
 LARGE_SIZES = [32768]
 
 
+def make_consumers():
+    """The core_crypto consumers at the hot shape (N = 2048, k = 1, Solinas NTT), one fixed-seed case each
+    (an external-product case and a BNF CMUX step with a fixed-seed GGSW; plus key conversion and
+    a short PBS of both variants).  The oracle's outputs are written with their inputs; the PBS case is
+    self-checked by the blind-rotation identity with a zero mask (the result is the LUT rotated by the body)."""
+    n, p, k = 2048, O.SOLINAS_P, 1
+    ctx = O.NttContext(n)
+    s = SEED + 0xC0
+    u = lambda seed, q, shape: O.fill_uniform(seed, q, int(np.prod(shape))).reshape(shape)
+    d = {}
+    # key conversion (Raw, native input) and (Normalize, mod-p input)
+    d["bsk_std_native"] = u(s + 1, 0, (2, 1, 2, 2, n))
+    d["bsk_ntt_raw"] = ctx.bsk_to_ntt(d["bsk_std_native"].reshape(-1), 64, False).reshape(2, 1, 2, 2, n)
+    d["bsk_std_solinas"] = u(s + 2, p, (2, 1, 2, 2, n))
+    d["bsk_ntt_normalize"] = ctx.bsk_to_ntt(d["bsk_std_solinas"].reshape(-1), 0, True).reshape(2, 1, 2, 2, n)
+    # external products: BNF level 1 (B 23) and level 2 (B 12); Solinas level 1
+    d["ggsw_l1"] = u(s + 3, p, (1, 2, 2, n))
+    d["ggsw_l2"] = u(s + 4, p, (2, 2, 2, n))
+    d["glwe_native"], d["out_native"] = u(s + 5, 0, (2, n)), u(s + 6, 0, (2, n))
+    d["glwe_solinas"], d["out_solinas"] = u(s + 7, p, (2, n)), u(s + 8, p, (2, n))
+    d["ext_bnf_l1"] = ctx.ext_product(d["out_native"], d["ggsw_l1"], d["glwe_native"], k, 23, 1, bnf=True)
+    d["ext_bnf_l2"] = ctx.ext_product(d["out_native"], d["ggsw_l2"], d["glwe_native"], k, 12, 2, bnf=True)
+    d["ext_solinas_l1"] = ctx.ext_product(d["out_solinas"], d["ggsw_l1"], d["glwe_solinas"], k, 23, 1, bnf=False)
+    # one BNF CMUX step
+    d["cmux_ct0"], d["cmux_ct1"] = u(s + 9, 0, (2, n)), u(s + 10, 0, (2, n))
+    d["cmux_bnf_ct0"] = ctx.cmux(d["cmux_ct0"], d["cmux_ct1"], d["ggsw_l1"], k, 23, 1, bnf=True)
+    # short PBS (n_lwe = 2) of both variants on the converted keys; a zero-mask input checks the identity
+    d["lut_native"], d["lut_solinas"] = u(s + 11, 0, (2, n)), u(s + 12, p, (2, n))
+    lwe_native = u(s + 13, 0, (3, 3))
+    lwe_native[0, :2] = 0
+    lwe_solinas = u(s + 14, p, (3, 3))
+    d["lwe_native"], d["lwe_solinas"] = lwe_native, lwe_solinas
+    d["pbs_bnf"] = np.stack([ctx.pbs(lwe_native[b], d["lut_native"], d["bsk_ntt_raw"], k, 23, 1, bnf=True)
+                             for b in range(3)])
+    d["pbs_solinas"] = np.stack([ctx.pbs(lwe_solinas[b], d["lut_solinas"], d["bsk_ntt_normalize"], k, 23, 1,
+                                         bnf=False) for b in range(3)])
+    # identity: zero mask -> sample extract of LUT * X^-round(b 2N / 2^64)
+    b0 = int(lwe_native[0, 2])
+    ms = ((b0 + (1 << 51)) >> 52) % (2 * n)
+    lut = d["lut_native"].astype(object)
+    rot = [[(lut[c][(m + ms) % n] if (m + ms) % (2 * n) < n else -lut[c][(m + ms) % n]) % 2**64 for m in range(n)]
+           for c in range(2)]
+    want0 = [rot[0][0]] + [(-rot[0][n - j]) % 2**64 for j in range(1, n)] + [rot[1][0]]
+    assert [int(v) for v in d["pbs_bnf"][0]] == want0
+    return d
+
+
 def main():
+    path = os.path.join(HERE, "consumers_n2048.npz")
+    np.savez_compressed(path, **make_consumers())
+    print("wrote", os.path.relpath(path, ROOT))
     for n in LARGE_SIZES:
         path = os.path.join(HERE, f"large_solinas_n{n}.npz")
         np.savez_compressed(path, **make_large(n))
