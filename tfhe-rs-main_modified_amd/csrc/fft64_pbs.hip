@@ -532,9 +532,8 @@ __device__ __forceinline__ void ext_product_body(u64* __restrict__ out, u64* __r
   }
 }
 
-// The shortint shape (k = 1, one level) runs 4 ciphertexts per workgroup (8 waves, 153 KiB of LDS, 256
-// registers: 2 waves per SIMD, the twiddle tables shared and the key rows read once per 4 ciphertexts from
-// L1); the coverage shapes one ciphertext per workgroup with the compiler's register choice.
+// One GLWE per workgroup (the external product / CMUX entry points; the PBS kernel below batches 4 ciphertexts
+// per workgroup for the shortint shape).
 template <int K, bool CMUX, bool L1>
 __global__ __launch_bounds__(64 * (K + 1)) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                                    const cplx* __restrict__ ggsw, uint32_t batch,
@@ -543,14 +542,6 @@ __global__ __launch_bounds__(64 * (K + 1)) void ext_product_kernel(u64* __restri
   ext_product_body<K, CMUX, L1, 1>(out, glwe, ggsw, batch, base_log, level, tb, wg);
 }
 constexpr int CT_FAST = 4;
-template <bool CMUX>
-__global__ __launch_bounds__(128 * CT_FAST) __attribute__((amdgpu_waves_per_eu(2))) void ext_product_kernel_k1l1(
-    u64* __restrict__ out, u64* __restrict__ glwe, const cplx* __restrict__ ggsw, uint32_t batch, int base_log,
-    int level, Tables tb) {
-  __shared__ Wg<1, CT_FAST> wg;
-  ext_product_body<1, CMUX, true, CT_FAST>(out, glwe, ggsw, batch, base_log, level, tb, wg);
-}
-
 // algorithms/modulus_switch.rs:60-104 centered_binary_ms_body_correction_to_add, reduced over the TG threads of
 // one ciphertext (gt = index within them; sh = 2 TG u64 of that ciphertext's LDS).  Every thread of the
 // workgroup calls it (barriers).
@@ -727,12 +718,8 @@ hipError_t launch_fft64_bwd_torus(uint64_t* std_, const double* fourier, size_t 
 template <int K, bool CMUX, bool L1>
 static hipError_t ext_one(uint64_t* out, uint64_t* glwe, const fft::cplx* g, size_t batch, int base_log, int level,
                           const FftTables& t, hipStream_t s) {
-  if (K == 1 && L1)
-    hipLaunchKernelGGL((fft::ext_product_kernel_k1l1<CMUX>), dim3((unsigned)((batch + fft::CT_FAST - 1) / fft::CT_FAST)),
-                       dim3(128 * fft::CT_FAST), 0, s, out, glwe, g, (uint32_t)batch, base_log, level, tables(t));
-  else
-    hipLaunchKernelGGL((fft::ext_product_kernel<K, CMUX, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out,
-                       glwe, g, (uint32_t)batch, base_log, level, tables(t));
+  hipLaunchKernelGGL((fft::ext_product_kernel<K, CMUX, L1>), dim3((unsigned)batch), dim3(64 * (K + 1)), 0, s, out, glwe,
+                     g, (uint32_t)batch, base_log, level, tables(t));
   return hipGetLastError();
 }
 
