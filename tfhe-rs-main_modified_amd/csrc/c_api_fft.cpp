@@ -21,7 +21,7 @@ struct mi_fft64_plan {
   size_t n = 0;
   int device = 0;
   bool cached = false;
-  double* d_tables = nullptr;  // t1 (2048) | t2 (128) | cm (32) | cmi (32) doubles
+  double* d_tables = nullptr;  // t1 (2048) | t2 (96, padded to 128) | cm (32) | cmi (32) doubles
   mi::FftTables tables{};
 };
 
@@ -51,10 +51,12 @@ std::vector<double> host_tables() {
   // t1[k1][j] = w^j omega^(j k1) = exp(i pi (j - 4 j k1) / 2048)
   for (int k1 = 0; k1 < 16; ++k1)
     for (int j = 0; j < 64; ++j) unit_root((long)j - 4L * j * k1, &h[2 * (k1 * 64 + j)], &h[2 * (k1 * 64 + j) + 1]);
-  // t2[j1][k2] = nu^(j1 k2) = exp(-2 pi i j1 k2 / 64) = exp(i pi (-64 j1 k2) / 2048)
-  for (int j1 = 0; j1 < 4; ++j1)
-    for (int k2 = 0; k2 < 16; ++k2)
-      unit_root(-64L * j1 * k2, &h[OFF_T2 + 2 * (j1 * 16 + k2)], &h[OFF_T2 + 2 * (j1 * 16 + k2) + 1]);
+  // t2[q1 - 1][jl] = W64^(jl q1) = exp(-2 pi i jl q1 / 64) = exp(i pi (-64 jl q1) / 2048), q1 = 1..3
+  for (int q1 = 1; q1 < 4; ++q1)
+    for (int jl = 0; jl < 16; ++jl) {
+      const size_t o = OFF_T2 + 2 * ((q1 - 1) * 16 + jl);
+      unit_root(-64L * jl * q1, &h[o], &h[o + 1]);
+    }
   for (int m = 0; m < 16; ++m) {
     unit_root(64L * m, &h[OFF_CM + 2 * m], &h[OFF_CM + 2 * m + 1]);  // exp(i pi m / 32)
     double re, im;

@@ -8,7 +8,7 @@ namespace mi {
 
 // Device twiddle tables of an N = 2048 plan (complex values as interleaved re, im doubles):
 //   t1  [16][64]  w^j omega^(j k1), w = exp(i pi / 2M), omega = exp(-2 pi i / M), M = 1024
-//   t2  [4][16]   nu^(j1 k2), nu = exp(-2 pi i / 64)
+//   t2  [3][16]   W64^(jl q1) = exp(-2 pi i jl q1 / 64), q1 = 1..3
 //   cm  [16]      exp(i pi m / 32)
 //   cmi [16]      exp(-i pi m / 32) 2^64 / M
 struct FftTables {
@@ -30,8 +30,8 @@ hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const 
 
 // position (register r, lane l) of the Fourier layout -> frequency index (see fft64_pbs.hip)
 inline uint32_t fft64_frequency(int r, int l) {
-  const int k1 = l >> 2, c = l & 3, g = r >> 2, k3 = r & 3;
-  return (uint32_t)(256 * k3 + 16 * (4 * c + g) + k1);
+  const int k1 = (l & 3) | (((l >> 4) & 3) << 2), q1 = ((l >> 3) & 1) | (((l >> 2) & 1) << 1);
+  return (uint32_t)(k1 + 16 * q1 + 64 * r);
 }
 
 }  // namespace mi

@@ -15,16 +15,11 @@
 // (parity is decryption + an error bound against a numpy restatement).
 //
 // MI355X mapping: one wave per polynomial, 16 complex values per lane in VGPRs (lane j holds u[j + 64 m],
-// m < 16), M = 16 x 64 split into three radix passes:
-//   pass 1  in-lane DFT16 over m, then twiddle T1[k1][j] = w^j omega^(j k1) (twist factor w^j folded in;
-//           the per-m part of the twist, exp(i pi m / 32), is applied before the DFT16)
-//   LDS transpose 1 (row stride 68 complex: conflict-free ds_write_b128 / ds_read_b128)
-//   pass 2  lane 4 k1 + j1 holds the 16 values j = j1 + 4 j2: DFT16 over j2, twiddle nu^(j1 k2) (nu = omega^16)
-//   LDS transpose 2 (slot 17 L + swap2(k2): conflict-free both ways, tools/lds_layout_check.py)
-//   pass 3  lane 4 k1 + c holds (g, j1) for k2 = 4 c + g: DFT4 over j1 -> k3
-// Fourier position (lane 4 k1 + c, register 4 g + k3) holds frequency 256 k3 + 16 (4 c + g) + k1.  The inverse
-// runs the passes backwards with conjugate twiddles.  All f64 arithmetic is FMA-contracted by hand where the
-// reference's pulp kernels use mul_add.
+// m < 16), M = 16 x 64 split into three radix passes (fft_fwd below): an in-lane DFT16 over m; a DFT4 over the
+// two top lane bits done in registers with gfx950's half-lane swaps (v_permlane32_swap / v_permlane16_swap);
+// one LDS transpose (rows of 17, conflict-free) and an in-lane DFT16 over the low four lane bits.  The inverse
+// runs the conjugate passes in reverse.  All f64 arithmetic is FMA-contracted by hand where the reference's pulp
+// kernels use mul_add.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -119,87 +114,126 @@ __device__ __forceinline__ void dft16(cplx (&a)[16]) {
   for (int i = 0; i < 16; ++i) a[i] = t[i];
 }
 
-constexpr int ROW1 = 68;               // transpose-1 row stride (complex)
-constexpr int BUF = 16 * ROW1;         // per-wave LDS buffer (complex): 17 KiB
-constexpr int ROW2 = 17;              // transpose-2 row stride (complex)
-constexpr int T2S = 17;               // row stride of the LDS copy of the pass-2 twiddles
-// transpose-2 slot of element (pass-2 lane L, k2): rows of 17, the two 2-bit halves of k2 swapped — with the
-// b128 lane groups of MI355X_MICROARCH.md §LDS, conflict-free for all four accesses (forward write / read,
-// inverse write / read; found by exhaustive check, tools/lds_layout_check.py)
-__device__ __forceinline__ int t2slot(int L, int k2) { return ROW2 * L + (((k2 >> 2) | (k2 << 2)) & 15); }
+constexpr int ROW = 17;                // transpose row stride (complex): conflict-free both ways
+constexpr int BUF = 64 * ROW;          // per-wave LDS buffer (complex): 17 KiB
+constexpr int TB = 48;                 // pass-3 twiddle table: [q1 - 1][jl], q1 = 1..3
 
-// Forward: u[m] = folded value at n = lane + 64 m (untwisted); out: Fourier layout (see header).
-// `cm` = exp(i pi m / 32) (m < 16), `t1` = T1[k1 * 64 + j], `t2` = nu^(j1 k2) at [j1 * 16 + k2] (LDS).
+// In-register exchanges across the lane halves (gfx950 v_permlane32_swap / v_permlane16_swap): lanes 32..63
+// of `a` trade places with lanes 0..31 of `b` (X = 32), or lanes 16..31 / 48..63 of `a` with lanes 0..15 /
+// 32..47 of `b` (X = 16).  For a pair of registers holding elements (r, r') this turns the lane bit into the
+// register bit: afterwards the low lanes hold (r: bit 0, r: bit 1) and the high lanes (r': bit 0, r': bit 1).
+template <int X>
+__device__ __forceinline__ void swap_dw(double& a, double& b) {
+  const u64 x = __double_as_longlong(a), y = __double_as_longlong(b);
+  uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32), yl = (uint32_t)y, yh = (uint32_t)(y >> 32);
+  if constexpr (X == 32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    xl = l[0], yl = l[1], xh = h[0], yh = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+    xl = l[0], yl = l[1], xh = h[0], yh = h[1];
+  }
+  a = __longlong_as_double((long long)(((u64)xh << 32) | xl));
+  b = __longlong_as_double((long long)(((u64)yh << 32) | yl));
+}
+template <int X>
+__device__ __forceinline__ void swap_c(cplx& a, cplx& b) {
+  swap_dw<X>(a.re, b.re);
+  swap_dw<X>(a.im, b.im);
+}
+
+// Forward: u[m] = folded value at n = lane + 64 m (untwisted); out: the Fourier layout.  M = 16 x 64 with
+// n = j + 64 m, j = jl + 16 jh (jl = lane & 15, jh = lane >> 4), frequency f = k1 + 16 q1 + 64 q2:
+//   pass 1  in-lane DFT16 over m -> k1 (register), twiddle T1[k1][j] = w^j omega^(j k1) (`t1`, twist folded in;
+//           the per-m twist factor `cm` = exp(i pi m / 32) goes before the DFT16)
+//   pass 2  DFT4 over jh (lane bits 5, 4) in registers: two radix-2 stages, each one half-lane swap of the
+//           register pairs (r, r + 8) / (r, r + 4) and a butterfly (the W4 twiddle -i is per register)
+//           -> q1 = q10 + 2 q11 in register bits 3, 2; lane bits 5, 4 now hold k1 bits 3, 2
+//   pass 3  twiddle W64^(jl q1) (`t2` = [q1 - 1][jl]), LDS transpose of lane bits 0..3 <-> register bits
+//           (rows of 17: conflict-free), in-lane DFT16 over jl -> q2
+// Position (lane L, register R) holds f = k1 + 16 q1 + 64 R with k1 = (L & 3) | ((L >> 4) & 3) << 2,
+// q1 = ((L >> 3) & 1) | ((L >> 2) & 1) << 1.
 __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
                                         const cplx* __restrict__ cm, int lane) {
 #pragma unroll
   for (int m = 1; m < 16; ++m) u[m] = cmul(u[m], cm[m]);
   dft16<false>(u);
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) buf[k1 * ROW1 + lane] = cmul(u[k1], t1[k1 * 64 + lane]);
-  const int k1 = lane >> 2, j1 = lane & 3;
+  for (int k1 = 0; k1 < 16; ++k1) u[k1] = cmul(u[k1], t1[k1 * 64 + lane]);
+  // radix 2 over jh1 (lane bit 5): (r, r + 8) = (jh1 = 0, jh1 = 1) -> (q10 = 0, q10 = 1)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    swap_c<32>(u[r], u[r + 8]);
+    const cplx a = u[r], b = u[r + 8];
+    u[r] = cadd(a, b);
+    u[r + 8] = csub(a, b);
+  }
+  // radix 2 over jh0 (lane bit 4) with W4^(jh0 q10): (r, r + 4) = (jh0 = 0, jh0 = 1) -> (q11 = 0, q11 = 1)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (r & 4) continue;
+    swap_c<16>(u[r], u[r + 4]);
+    const cplx a = u[r], b = (r & 8) ? mul_neg_i(u[r + 4]) : u[r + 4];
+    u[r] = cadd(a, b);
+    u[r + 4] = csub(a, b);
+  }
+  const int jl = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int q1 = ((r >> 3) & 1) | (((r >> 2) & 1) << 1);
+    if (q1) u[r] = cmul(u[r], t2[(q1 - 1) * 16 + jl]);
+    buf[ROW * lane + r] = u[r];
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int row = (lane & 48) * ROW + (lane & 15);  // element (lane' = 16 h + jl, r = lane & 15)
 #pragma unroll
-  for (int j2 = 0; j2 < 16; ++j2) u[j2] = buf[k1 * ROW1 + j1 + 4 * j2];
+  for (int j = 0; j < 16; ++j) u[j] = buf[row + ROW * j];
   dft16<false>(u);
-#pragma unroll
-  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmul(u[k2], t2[j1 * T2S + k2]);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) buf[t2slot(lane, k2)] = u[k2];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int c = lane & 3;
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      u[4 * g + jj] = buf[t2slot(4 * k1 + jj, 4 * c + g)];
-    }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) dft4<false>(u, 4 * g, 1);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Inverse of fft_fwd including the 1/M normalisation and the untwist (`cmi` = exp(-i pi m / 32) 2^64 / M: the
-// output is 2^64 times the torus value, ready for from_torus_scaled).
+// Inverse of fft_fwd (the conjugate transpose of every pass in reverse order), including the 1/M normalisation
+// and the untwist (`cmi` = exp(-i pi m / 32) 2^64 / M: the output is 2^64 times the torus value, ready for
+// from_torus_scaled).
 __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
                                         const cplx* __restrict__ cmi, int lane) {
-  const int k1 = lane >> 2, c = lane & 3;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) dft4<true>(u, 4 * g, 1);
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      buf[t2slot(4 * k1 + jj, 4 * c + g)] = u[4 * g + jj];
-    }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int j1 = lane & 3;
-#pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) u[k2] = buf[t2slot(lane, k2)];
-#pragma unroll
-  for (int k2 = 1; k2 < 16; ++k2) u[k2] = cmulc(u[k2], t2[j1 * T2S + k2]);
   dft16<true>(u);
+  const int row = (lane & 48) * ROW + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) buf[row + ROW * j] = u[j];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int jl = lane & 15;
 #pragma unroll
-  for (int j2 = 0; j2 < 16; ++j2) buf[k1 * ROW1 + j1 + 4 * j2] = u[j2];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int r = 0; r < 16; ++r) {
+    u[r] = buf[ROW * lane + r];
+    const int q1 = ((r >> 3) & 1) | (((r >> 2) & 1) << 1);
+    if (q1) u[r] = cmulc(u[r], t2[(q1 - 1) * 16 + jl]);
+  }
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) u[kk] = cmulc(buf[kk * ROW1 + lane], t1[kk * 64 + lane]);
+  for (int r = 0; r < 16; ++r) {
+    if (r & 4) continue;
+    const cplx a = u[r], b = u[r + 4];
+    u[r] = cadd(a, b);
+    u[r + 4] = (r & 8) ? mul_pos_i(csub(a, b)) : csub(a, b);
+    swap_c<16>(u[r], u[r + 4]);
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const cplx a = u[r], b = u[r + 8];
+    u[r] = cadd(a, b);
+    u[r + 8] = csub(a, b);
+    swap_c<32>(u[r], u[r + 8]);
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) u[k1] = cmulc(u[k1], t1[k1 * 64 + lane]);
   dft16<true>(u);
 #pragma unroll
   for (int m = 0; m < 16; ++m) u[m] = cmul(u[m], cmi[m]);
@@ -268,7 +302,7 @@ __device__ __forceinline__ u64 modulus_switch(u64 input, unsigned log_modulus) {
 
 struct Tables {
   const cplx* t1;   // [16][64] forward pass-1 twiddles (twist folded in)
-  const cplx* t2;   // [4][16]
+  const cplx* t2;   // [3][16] W64^(jl q1), q1 = 1..3
   const cplx* cm;   // [16] exp(i pi m / 32)
   const cplx* cmi;  // [16] exp(-i pi m / 32) 2^64 / M (the torus -> u64 scale folded in)
 };
@@ -280,9 +314,9 @@ constexpr int N = 2048, M = 1024, NPL = N / 64;  // 32 coefficients per lane
 __global__ __launch_bounds__(64) void fwd_torus_kernel(cplx* __restrict__ fourier, const u64* __restrict__ std_,
                                                        uint64_t batch, Tables tb) {
   __shared__ cplx buf[BUF];
-  __shared__ cplx t2[4 * T2S];
+  __shared__ cplx t2[TB];
   const int lane = threadIdx.x;
-  t2[(lane >> 4) * T2S + (lane & 15)] = tb.t2[lane];
+  if (lane < TB) t2[lane] = tb.t2[lane];
   __syncthreads();
   const uint64_t b = blockIdx.x;
   if (b >= batch) return;
@@ -300,9 +334,9 @@ __global__ __launch_bounds__(64) void fwd_torus_kernel(cplx* __restrict__ fourie
 __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, const cplx* __restrict__ fourier,
                                                        uint64_t batch, int add, Tables tb) {
   __shared__ cplx buf[BUF];
-  __shared__ cplx t2[4 * T2S];
+  __shared__ cplx t2[TB];
   const int lane = threadIdx.x;
-  t2[(lane >> 4) * T2S + (lane & 15)] = tb.t2[lane];
+  if (lane < TB) t2[lane] = tb.t2[lane];
   __syncthreads();
   const uint64_t b = blockIdx.x;
   if (b >= batch) return;
@@ -482,7 +516,7 @@ struct Wg {
   static constexpr int WAVES = CT * (K + 1), THREADS = 64 * WAVES;
   cplx bufs[WAVES * BUF];
   cplx t1[16 * 64];
-  cplx t2[4 * T2S];
+  cplx t2[TB];
   cplx cm[16], cmi[16];
   uint32_t flags[WAVES];
 };
@@ -490,7 +524,7 @@ struct Wg {
 template <int K, int CT>
 __device__ __forceinline__ void load_tables(Wg<K, CT>& wg, const Tables& tb) {
   for (int i = threadIdx.x; i < 16 * 64; i += Wg<K, CT>::THREADS) wg.t1[i] = tb.t1[i];
-  if (threadIdx.x < 64) wg.t2[(threadIdx.x >> 4) * T2S + (threadIdx.x & 15)] = tb.t2[threadIdx.x];
+  if (threadIdx.x < TB) wg.t2[threadIdx.x] = tb.t2[threadIdx.x];
   if (threadIdx.x < 16) {
     wg.cm[threadIdx.x] = tb.cm[threadIdx.x];
     wg.cmi[threadIdx.x] = tb.cmi[threadIdx.x];
