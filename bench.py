@@ -204,7 +204,9 @@ def bench_pbs(args, eng, torch, dev, rank, world, barrier, dist):
         "cpu_baseline": None,
     }
     if dist is not None:
-        res["sharded"] = bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk)
+        res["sharded"] = bench_pbs_sharded(
+            args, eng, torch, dev, rank, world, barrier,
+            lambda li, lo: M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(li, lo, lut, key), bsk)
     del key
     return res
 
@@ -244,7 +246,7 @@ def bench_pbs_solinas(args, eng, torch, dev, world, barrier):
                        "batch_per_gpu": batch}}
 
 
-def bench_pbs_fft(args, eng, torch, dev, world, barrier):
+def bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist):
     """The default shortint PBS, f64-FFT path (programmable_bootstrap_lwe_ciphertext, fft64_pbs.rs:924-1060)
     at PARAM_MESSAGE_2_CARRY_2's shape: native 2^64 ciphertexts, Fourier key (60 MB of complex f64) resident."""
     F = eng.fft64
@@ -259,7 +261,7 @@ def bench_pbs_fft(args, eng, torch, dev, world, barrier):
     lut = torch.empty((2, N), dtype=torch.int64, device=dev)
     eng.fill_uniform(lut, SEED + 81, 0)
     lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
-    eng.fill_uniform(lwe, SEED + 82, 0)
+    eng.fill_uniform(lwe, SEED + 82 + rank * 0x1000, 0)
     out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
     run = lambda: F.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, key)
     run()
@@ -276,19 +278,27 @@ def bench_pbs_fft(args, eng, torch, dev, world, barrier):
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    if dist is not None:
+        el = eng.multi_gpu.max_over_ranks(el, dev)
+    res = {"metric": "PBS/sec, f64-FFT path (default shortint PBS), PARAM_MESSAGE_2_CARRY_2 shape",
+           "value": world * batch * K / el, "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3,
+           "kernel_ms": e0.elapsed_time(e1) / K, "dtype": "f64",
+           "config": {"workload": "programmable_bootstrap_lwe_ciphertext (tfhe-fft path), n=918 k=1 N=2048 "
+                                  "base_log=23 level=1, standard modulus switch", "batch_per_gpu": batch}}
+    if dist is not None:
+        res["sharded"] = bench_pbs_sharded(
+            args, eng, torch, dev, rank, world, barrier,
+            lambda li, lo: F.programmable_bootstrap_lwe_ciphertext(li, lo, lut, key), fbsk)
     del key
-    return {"metric": "PBS/sec, f64-FFT path (default shortint PBS), PARAM_MESSAGE_2_CARRY_2 shape",
-            "value": world * batch * K / el, "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3,
-            "kernel_ms": e0.elapsed_time(e1) / K, "dtype": "f64",
-            "config": {"workload": "programmable_bootstrap_lwe_ciphertext (tfhe-fft path), n=918 k=1 N=2048 "
-                                   "base_log=23 level=1, standard modulus switch", "batch_per_gpu": batch}}
+    return res
 
 
-def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, bsk):
+def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, pbs, bsk):
     """Config 5: one global batch of PBS (default 65,536) held on the root, scattered over the ranks,
     bootstrapped, gathered back (strong scaling).  The transfers are grouped point-to-point sends from
     the root (multi_gpu.scatter_batch / gather_batch: RCCL over xGMI, the root feeding each peer over
-    its own link); the key broadcast is timed once, outside the steady state."""
+    its own link); the key broadcast is timed once, outside the steady state.  `pbs(lwe_in, lwe_out)` runs
+    the bootstrap of one shard with the resident key; `bsk` is the key tensor whose broadcast is timed."""
     mg = eng.multi_gpu
     n_lwe, G, K = PBS_N_LWE, args.pbs_global, args.pbs_steps
     gloo = args.dist_backend == "gloo"  # rehearsal: gloo point-to-point needs host tensors
@@ -319,7 +329,7 @@ def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, M, key, lut, 
             mg.scatter_batch(lwe_all, shard_in, src=0)
             if gloo:
                 work_in.copy_(shard_in)
-        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(work_in, shard_out, lut, key)
+        pbs(work_in, shard_out)
         if transfer:
             mg.gather_batch(shard_out if not gloo else shard_out.cpu(), out_all, dst=0)
 
@@ -746,7 +756,7 @@ def main():
         out["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier)
         out["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
         out["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier)
-        out["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, world, barrier)
+        out["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist)
         out["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier)
         out["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier)
         out["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier)

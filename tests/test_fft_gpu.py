@@ -235,3 +235,35 @@ def test_errors(engine):
     with pytest.raises(engine.MiError) as e:
         M_.Fft(1000)
     assert e.value.status == 1
+
+
+@pytest.mark.parametrize("batch", [1, 5, 7])
+@pytest.mark.parametrize("ms_mode", [0, 1, 2])
+def test_pbs_k1_l1_ragged_batches(engine, fft, batch, ms_mode):
+    """The k = 1, level-1 shape runs the 4-ciphertexts-per-workgroup kernel: batches that do not fill the last
+    workgroup (its idle waves still take part in the step synchronisation) under every modulus-switch mode."""
+    import torch
+    n_lwe, msg_mod, base_log = 40, 4, 23
+    delta = (1 << 63) // msg_mod
+    g = H.rng(900 + 10 * batch + ms_mode)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (1, N))
+    bsk = H.bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, 17)
+    fbsk = torch.zeros((n_lwe, 1, 2, 2, M, 2), dtype=torch.float64, device="cuda")
+    engine.fft64.convert_standard_lwe_bootstrap_key_to_fourier(dev(bsk), fbsk, fft)
+    f = lambda x: (3 * x + 1) % msg_mod
+    lut = H.pbs_lut(N, 1, msg_mod, delta, f)
+    msgs = np.arange(batch) % msg_mod
+    lwe = H.lwe_encrypt_batch(g, msgs.astype(np.uint64) * np.uint64(delta), lwe_sk, 30)
+    if ms_mode == 2:
+        lwe = F.modulus_switch(lwe, 12)
+    key = engine.fft64.FourierLweBootstrapKey(fbsk, base_log, 1, fft)
+    sentinel = np.full((batch + 1, N + 1), 0x5A5A5A5A5A5A5A5A, np.uint64)
+    out = dev(sentinel)
+    engine.fft64.programmable_bootstrap_lwe_ciphertext(dev(lwe), out[:batch], dev(lut), key, ms_mode)
+    got = host(out)
+    assert np.array_equal(got[batch], sentinel[batch])  # nothing written past the batch
+    pts = H.lwe_decrypt_batch(got[:batch], H.glwe_sk_as_lwe_sk(glwe_sk))
+    with np.errstate(over="ignore"):
+        dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
+    assert list(dec) == [f(int(m)) for m in msgs]
