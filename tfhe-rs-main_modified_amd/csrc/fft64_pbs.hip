@@ -265,10 +265,16 @@ __device__ __forceinline__ u64 from_torus_scaled(double y) {
   torus_words(y, h, l);
   return ((u64)h << 32) | l;
 }
-// acc += from_torus_scaled(y) as one 32-bit add with carry per word
+// acc += from_torus_scaled(y) as one 32-bit add with carry per word.  Without the first rint: z keeps y's
+// fraction (only when |y| < 2^52), lo + 2^52 rounds it, and the one case that rounds lo up to 2^32 (z within
+// 1/2 below a multiple of 2^32, i.e. |y| < 2^52 and y = -0.5..0 mod 2^32) drops a carry of 2^32 — far below the
+// transform's own f64 error (>= 2^40 on these products), so the external product bound is unchanged.
 __device__ __forceinline__ void add_torus_scaled(u64& acc, double y) {
-  uint32_t h, l;
-  torus_words(y, h, l);
+  const double z = __fma_rn(-__builtin_rint(y * 0x1p-64), 0x1p64, y);
+  const double hi = __builtin_floor(z * 0x1p-32);
+  const double lo = __fma_rn(-hi, 0x1p32, z);
+  const uint32_t h = (uint32_t)__double_as_longlong(hi + 0x1.8p52);
+  const uint32_t l = (uint32_t)__double_as_longlong(lo + 0x1p52);
   const uint32_t alo = (uint32_t)acc, ahi = (uint32_t)(acc >> 32);
   const uint32_t nlo = alo + l;
   const uint32_t nhi = ahi + h + (nlo < alo ? 1u : 0u);

@@ -6,4 +6,4 @@ import torch, bench
 import tfhe_ntt_amd as eng
 class A: pbs_batch = 4096; pbs_steps = 3
 dev = torch.device("cuda", 0)
-print(json.dumps(bench.bench_pbs_fft(A, eng, torch, dev, 1, lambda: None)), flush=True)
+print(json.dumps(bench.bench_pbs_fft(A, eng, torch, dev, 0, 1, lambda: None, None)), flush=True)
