@@ -61,8 +61,8 @@ std::vector<double> host_tables() {
     unit_root(64L * m, &h[OFF_CM + 2 * m], &h[OFF_CM + 2 * m + 1]);  // exp(i pi m / 32)
     double re, im;
     unit_root(-64L * m, &re, &im);
-    h[OFF_CMI + 2 * m] = re * 0x1p64 / (double)FFT_M;  // exact scalings (powers of two): 2^64 / M
-    h[OFF_CMI + 2 * m + 1] = im * 0x1p64 / (double)FFT_M;
+    h[OFF_CMI + 2 * m] = re / (double)FFT_M;  // exact scaling (a power of two): 1 / M
+    h[OFF_CMI + 2 * m + 1] = im / (double)FFT_M;
   }
   return h;
 }

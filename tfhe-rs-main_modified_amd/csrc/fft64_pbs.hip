@@ -199,8 +199,8 @@ __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __
 }
 
 // Inverse of fft_fwd (the conjugate transpose of every pass in reverse order), including the 1/M normalisation
-// and the untwist (`cmi` = exp(-i pi m / 32) 2^64 / M: the output is 2^64 times the torus value, ready for
-// from_torus_scaled).
+// and the untwist (`cmi` = exp(-i pi m / 32) / M: the output is the torus value, ready for add_torus /
+// from_torus).
 __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
                                         const cplx* __restrict__ cmi, int lane) {
   dft16<true>(u);
@@ -246,8 +246,8 @@ __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __
 // u64 -> i64 -> f64 (into_signed().cast_into()); exact int64 -> double rounding as Rust's `as f64`
 __device__ __forceinline__ double s64_to_f64(u64 x) { return (double)(int64_t)x; }
 
-// Scalar::from_torus (commons/math/torus/mod.rs:72-78) of x = y / 2^64, taking y = x 2^64 (the 2^64 is folded
-// into the inverse transform's last twiddles): round(fract(x) 2^64) mod 2^64 = round(y) mod 2^64.  All steps
+// Scalar::from_torus (commons/math/torus/mod.rs:72-78) of x = y / 2^64, taking y = x 2^64 (an exact power-of-two
+// scaling by the caller): round(fract(x) 2^64) mod 2^64 = round(y) mod 2^64.  All steps
 // exact: r = rint(y); z = r - rint(r 2^-64) 2^64 in [-2^63, 2^63]; z = hi 2^32 + lo with lo in [0, 2^32); the
 // words are read from the mantissas of hi + 1.5 2^52 and lo + 2^52.  round-half-even instead of half-away-from-
 // zero: different only for an exact half-integer y, where the reference also saturates +2^63 (to i64::MAX; here
@@ -265,16 +265,16 @@ __device__ __forceinline__ u64 from_torus_scaled(double y) {
   torus_words(y, h, l);
   return ((u64)h << 32) | l;
 }
-// acc += from_torus_scaled(y) as one 32-bit add with carry per word.  Without the first rint: z keeps y's
-// fraction (only when |y| < 2^52), lo + 2^52 rounds it, and the one case that rounds lo up to 2^32 (z within
-// 1/2 below a multiple of 2^32, i.e. |y| < 2^52 and y = -0.5..0 mod 2^32) drops a carry of 2^32 — far below the
-// transform's own f64 error (>= 2^40 on these products), so the external product bound is unchanged.
-__device__ __forceinline__ void add_torus_scaled(u64& acc, double y) {
-  const double z = __fma_rn(-__builtin_rint(y * 0x1p-64), 0x1p64, y);
-  const double hi = __builtin_floor(z * 0x1p-32);
-  const double lo = __fma_rn(-hi, 0x1p32, z);
-  const uint32_t h = (uint32_t)__double_as_longlong(hi + 0x1.8p52);
-  const uint32_t l = (uint32_t)__double_as_longlong(lo + 0x1p52);
+// acc += from_torus(t) (t in torus units) as one 32-bit add with carry per word: f = fract(t) in [0, 1) is
+// exact (t's bits below 2^0); s = f 2^32 exact; the high word is trunc(s), the low word fract(s) 2^32 rounded
+// through the mantissa of fract(s) 2^32 + 2^52.  Differences from the exact from_torus, all far below the
+// transform's own f64 error (>= 2^40 on these products): for |t| < 2^-12 the fraction rounds (and a low word that
+// rounds up to 2^32 drops its carry), and fract of a tiny negative t clamps below 1.
+__device__ __forceinline__ void add_torus(u64& acc, double t) {
+  const double f = __builtin_amdgcn_fract(t);
+  const double s = f * 0x1p32;
+  const uint32_t h = (uint32_t)s;
+  const uint32_t l = (uint32_t)__double_as_longlong(__fma_rn(__builtin_amdgcn_fract(s), 0x1p32, 0x1p52));
   const uint32_t alo = (uint32_t)acc, ahi = (uint32_t)(acc >> 32);
   const uint32_t nlo = alo + l;
   const uint32_t nhi = ahi + h + (nlo < alo ? 1u : 0u);
@@ -310,7 +310,7 @@ struct Tables {
   const cplx* t1;   // [16][64] forward pass-1 twiddles (twist folded in)
   const cplx* t2;   // [3][16] W64^(jl q1), q1 = 1..3
   const cplx* cm;   // [16] exp(i pi m / 32)
-  const cplx* cmi;  // [16] exp(-i pi m / 32) 2^64 / M (the torus -> u64 scale folded in)
+  const cplx* cmi;  // [16] exp(-i pi m / 32) / M
 };
 
 constexpr int N = 2048, M = 1024, NPL = N / 64;  // 32 coefficients per lane
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, c
   u64* x = std_ + b * N;
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    const u64 re = from_torus_scaled(u[m].re), im = from_torus_scaled(u[m].im);
+    const u64 re = from_torus_scaled(u[m].re * 0x1p64), im = from_torus_scaled(u[m].im * 0x1p64);
     x[lane + 64 * m] = add ? x[lane + 64 * m] + re : re;
     x[M + lane + 64 * m] = add ? x[M + lane + 64 * m] + im : im;
   }
@@ -510,8 +510,8 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
   fft_inv(y, buf, t1, t2, cmi, lane);
 #pragma unroll
   for (int m = 0; m < 16; ++m) {  // convert_add_backward_torus
-    add_torus_scaled(acc[m], y[m].re);
-    add_torus_scaled(acc[m + 16], y[m].im);
+    add_torus(acc[m], y[m].re);
+    add_torus(acc[m + 16], y[m].im);
   }
 }
 
