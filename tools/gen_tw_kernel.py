@@ -395,8 +395,10 @@ class Body:
             sl.append(Slot(b, SG0 + 6 * i))
         return sl
 
-    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None):
-        """canon: list of 32 flags (logical registers known canonical), updated in place."""
+    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None, by_reg=False):
+        """canon: list of 32 flags (logical registers known canonical), updated in place.  The twiddle
+        exponent of the butterfly on registers (r, r + dist) is exps[r // (2 dist)] (one per group, the
+        natural-in CT / GS stages), or exps[r] with by_reg (one per position, the DIT stages)."""
         sg = Seg()
         slots = self.slots(free_blocks)
         bf = 0
@@ -405,7 +407,7 @@ class Body:
         for r in range(32):
             if r & dist:
                 continue
-            S = exps[r // (2 * dist)]
+            S = exps[r] if by_reg else exps[r // (2 * dist)]
             sl = slots[bf % len(slots)]
             a, b = X(dmap, r), X(dmap, r + dist)
             if kind == "ct":
@@ -474,11 +476,18 @@ def gen_bases(src, dst):
     return lines
 
 
+# cache-policy bits appended to the data row loads / stores (gfx950: "nt", "sc0", "sc1"); the product
+# bodies use the default policy unless tools/variant_probe measures another one faster
+LOAD_POLICY = ""
+STORE_POLICY = ""
+INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
+
+
 def load_rows(dmap, base, voff="%[l8]"):
     out = []
     for r in range(32):
         out.append(f"global_load_dwordx2 {pv(dmap[r])}, {voff}, s[{base + 2 * (r // 8)}:{base + 2 * (r // 8) + 1}] "
-                   f"offset:{512 * (r % 8)}")
+                   f"offset:{512 * (r % 8)}{LOAD_POLICY}")
     return out
 
 
@@ -486,7 +495,7 @@ def store_rows(dmap, base):
     out = []
     for r in range(32):
         out.append(f"global_store_dwordx2 %[l8], {pv(dmap[r])}, s[{base + 2 * (r // 8)}:{base + 2 * (r // 8) + 1}] "
-                   f"offset:{512 * (r % 8)}")
+                   f"offset:{512 * (r % 8)}{STORE_POLICY}")
     return out
 
 
@@ -845,6 +854,23 @@ INV_PRE_LW = 40          # v40..v43: the inverse lane-pair table twiddles, loade
 INV_PRE_TW = 40          # v40..v55: the first untwist batch, loaded during the lane-pair stage
 
 
+def dit_exps(s):
+    """Exponents of DIT stage s = 1..5 of the inverse cyclic blocks (register distance 2^(s-1), storage
+    bit s of j = 2 reg + j0), indexed by the butterfly's first register r.
+
+    The inverse of the natural-in / bit-reversed-out cyclic DFT (omega = 8) is computed from its
+    bit-reversed input by decimation in time: stage s joins j and j + 2^s with the twiddle
+    w = omega^-(k 64 / 2^(s+1)), k = j mod 2^s, so CT butterflies need no canonical inputs (GS ones need a
+    canonical subtrahend).  k holds the lane bit j0, so the odd lanes' twiddle would differ from the even
+    lanes' by omega^-(64 / 2^(s+1)) at every stage; instead the odd lanes enter stage 1 scaled by the
+    product of those factors over the stages to come, sigma(j) = omega^-bitrev5(j >> 1), which the first
+    (lane-pair) stage applies as a GS butterfly with exactly the CYC_INV[5] twiddles (a scale common to a
+    butterfly's two inputs passes through it; the factor pending for bit s is used up at stage s, so the
+    outputs come out unscaled).  Every lane then uses the even-lane twiddle: k = 2 (r mod 2^(s-1))."""
+    d = 1 << (s - 1)
+    return [(-3 * (64 >> s) * (r % d)) % 192 for r in range(32)]
+
+
 def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False):
     """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  `prefetch`
     (standalone kernel, see fwd_core): the caller has loaded the lane-pair table twiddles into
@@ -859,8 +885,12 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False):
         B.raw(*[ad.tw_load(0, k, INV_PRE_TW + 2 * k) for k in range(8)])
     fb = free_blocks_except(dmap, busy)
     cf = [False] * 32
-    for q in range(4, -1, -1):
-        B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
+    if INV_CYC_DIT:
+        for s in range(1, 6):
+            B.stage("ct", 1 << (s - 1), dit_exps(s), dmap, fb, cf, by_reg=True)
+    else:  # r2 form (GS, canonical subtrahends), kept for tools/variant_probe A/B runs
+        for q in range(4, -1, -1):
+            B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
     dmap = t_iw0(B, dmap, False, 96, 64, ad)
     # untwist: table rows and multiply slots in the registers the data does not occupy
     free = free_blocks_except(dmap, busy)
