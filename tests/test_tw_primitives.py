@@ -147,3 +147,27 @@ def test_gmul_and_canon():
     G.canon(sg, slot(), G.X([X_A], 0))
     out = run_seg(sg, {X_A: xs}, [X_A])[X_A]
     assert out == [x % P for x in xs]
+
+
+@pytest.mark.parametrize("S", [0, 3, 24, 30, 33, 48, 63, 64, 72, 93, 96, 99, 120, 144, 168, 189])
+@pytest.mark.parametrize("shuffle", range(4))
+def test_ct_butterfly_canonical_outputs(S, shuffle):
+    """The forward's last stage: canon(a), t = tmul(b), ct_core_canon -> both outputs canonical."""
+    rnd = random.Random(S * 8 + shuffle)
+    a = corner_values(rnd, False)
+    b = corner_values(random.Random(rnd.random()), False)
+    rnd.shuffle(a)
+    rnd.shuffle(b)
+    if shuffle == 0:  # the largest sums / differences of canonical values
+        a[:4], b[:4] = [P - 1, P - 1, 0, M64], [P - 1, 0, P - 1, M64]
+    sg = G.Seg()
+    sl = slot()
+    A, B = G.X([X_A, X_B], 0), G.X([X_A, X_B], 1)
+    G.canon(sg, sl, A)
+    neg = G.tmul(sg, S, B[0], B[1], B[2], sl, sl.v[2], sl.v[3])
+    G.ct_core_canon(sg, sl, A, B, neg)
+    out = run_seg(sg, {X_A: a, X_B: b}, [X_A, X_B])
+    w = pow(2, S, P)
+    for x, y, s, d in zip(a, b, out[X_A], out[X_B]):
+        assert s < P and d < P, (S, hex(x), hex(y), hex(s), hex(d))
+        assert s == (x + y * w) % P and d == (x - y * w) % P, (S, hex(x), hex(y))

@@ -290,6 +290,27 @@ def ct_core(sg, sl, a, b, neg, tsrc=None):
         add_part2(sg, sl, bp)
 
 
+def ct_core_canon(sg, sl, a, b, neg):
+    """ct_core for a canonical a and the canonical t in sl.v2:v3, with canonical outputs: the difference of
+    two canonical values needs only the borrow fix (sub_seq), and their sum is canonical after one select
+    between s and U = s + EPS (U when the add carried, s + 2^64 = U mod p, or when U carried, s >= p)."""
+    alo, ahi, ap = a
+    blo, bhi, bp = b
+    v, P, c = sl.v, sl.P, sl.c
+    tlo, thi = v[2], v[3]
+    add_part1(sg, sl, alo, ahi, tlo, thi)                 # s = a + t in P0, carry c2
+    if not neg:
+        sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)      # b = a - t
+        dlo, dhi = alo, ahi
+    else:
+        sub_seq(sg, sl, alo, ahi, alo, ahi, tlo, thi)      # a = a - t (t stands for -w b)
+        dlo, dhi = blo, bhi
+    sg.add(f"v_mad_u64_u32 {P[3]}, {c[0]}, -1, 1, {P[0]}", [P[0]], [P[3], c[0]])
+    sg.add(f"s_or_b64 {c[0]}, {c[0]}, {c[2]}", [c[0], c[2]], [c[0], "scc"], "salu")
+    sg.add(f"v_cndmask_b32_e64 {dlo}, {v[0]}, {v[6]}, {c[0]}", [v[0], v[6], c[0]], [dlo])
+    sg.add(f"v_cndmask_b32_e64 {dhi}, {v[1]}, {v[7]}, {c[0]}", [v[1], v[7], c[0]], [dhi])
+
+
 def ct(sg, sl, a, b, S):
     neg = tmul(sg, S, b[0], b[1], b[2], sl, sl.v[2], sl.v[3])
     ct_core(sg, sl, a, b, neg)
@@ -740,9 +761,12 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
             regroup(sg, dmap, k, tmp, True)
             a, b = X(dmap, k), X(dmap, k + 16)
             if fwd:
+                # last stage: canonical outputs from a canonical a (3 VALU) and a canonicalising add /
+                # borrow-fixed subtract (12 VALU per butterfly instead of 14 for add, sub and two canons)
+                canon(sg, sl, a)
                 if lane:
                     neg = tmul_lane(sg, E[k], E[k + 16], b, sl, sl.v[2], sl.v[3], par3, (wlo, whi))
-                    ct_core(sg, sl, a, b, neg)
+                    ct_core_canon(sg, sl, a, b, neg)
                 else:
                     # t = b * w into the slot's Z1 pair, then CT with t viewed as v2:v3
                     gmul(sg, m, b, wlo, whi, m.v[8], m.v[9])
@@ -750,9 +774,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
                     ct_sl.v = [m.v[0], m.v[1], m.v[8], m.v[9], m.v[4], m.v[5], m.v[6], m.v[7]]
                     ct_sl.P = [m.P[0], None, None, m.P[3]]
                     ct_sl.c = sl.c
-                    ct_core(sg, ct_sl, a, b, False)
-                canon(sg, sl, a)
-                canon(sg, sl, b)
+                    ct_core_canon(sg, ct_sl, a, b, False)
             else:
                 # inputs are canonical (loaded data), so either may be the subtrahend: a' = a + b and
                 # d = a - b, or d = b - a when the shift twiddle is negative (the product stays positive)
