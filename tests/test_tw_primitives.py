@@ -105,12 +105,15 @@ def test_gs_butterfly(S, ac, bc):
     a = corner_values(rnd, ac)
     b = corner_values(random.Random(rnd.random()), bc)
     rnd.shuffle(b)
+    if ac and bc:  # the largest sums / differences of canonical values
+        a[:3], b[:3] = [P - 1, P - 1, 0], [P - 1, 0, P - 1]
     sg = G.Seg()
-    assert G.gs(sg, slot(), G.X([X_A, X_B], 0), G.X([X_A, X_B], 1), S, ac, bc)
+    sc, dc = G.gs(sg, slot(), G.X([X_A, X_B], 0), G.X([X_A, X_B], 1), S, ac, bc)
+    assert dc and sc == (ac and bc)
     out = run_seg(sg, {X_A: a, X_B: b}, [X_A, X_B])
     w = pow(2, S, P)
     for x, y, s, d in zip(a, b, out[X_A], out[X_B]):
-        assert s % P == (x + y) % P
+        assert s % P == (x + y) % P and (s < P or not sc)
         assert d < P and d == (x - y) * w % P
 
 

@@ -336,12 +336,25 @@ def gs(sg, sl, a, b, S, ac=False, bc=False):
     (a - b) w = (b - a) |w| when w < 0, so the subtrahend is b for w > 0 and a for w < 0.  That operand is
     canonicalised in place when it is not known canonical (a + b only needs one canonical operand, the
     same one), so the new b is always the canonical, positive tmul magnitude: no negation is ever
-    emitted.  Returns True (new b canonical)."""
+    emitted.  When both inputs are canonical the sum is made canonical too (one select after the add:
+    +1 VALU, and the next stage needs no canonicalisation).  Returns (new a canonical, new b canonical)."""
     alo, ahi, ap = a
     blo, bhi, bp = b
     v, P, c = sl.v, sl.P, sl.c
     e = S % 96
     neg = (S >= 96) != (e >= 64)
+    if ac and bc:
+        add_part1(sg, sl, alo, ahi, blo, bhi)              # s = a + b in P0, carry c2
+        if neg:
+            sub_seq(sg, sl, blo, bhi, blo, bhi, alo, ahi)  # d = b - a
+        else:
+            sub_seq(sg, sl, blo, bhi, alo, ahi, blo, bhi)  # d = a - b
+        sg.add(f"v_mad_u64_u32 {P[3]}, {c[0]}, -1, 1, {P[0]}", [P[0]], [P[3], c[0]])
+        sg.add(f"s_or_b64 {c[0]}, {c[0]}, {c[2]}", [c[0], c[2]], [c[0], "scc"], "salu")
+        sg.add(f"v_cndmask_b32_e64 {alo}, {v[0]}, {v[6]}, {c[0]}", [v[0], v[6], c[0]], [alo])
+        sg.add(f"v_cndmask_b32_e64 {ahi}, {v[1]}, {v[7]}, {c[0]}", [v[1], v[7], c[0]], [ahi])
+        tmul(sg, S, blo, bhi, bp, sl, blo, bhi)
+        return True, True
     sub_a = neg  # subtrahend: a when w < 0 (d = b - a), b otherwise (d = a - b)
     if sub_a and not ac:
         canon(sg, sl, a)
@@ -355,7 +368,7 @@ def gs(sg, sl, a, b, S, ac=False, bc=False):
         sub_seq(sg, sl, blo, bhi, alo, ahi, blo, bhi)  # d = a - b
     add_part2(sg, sl, ap)
     tmul(sg, S, blo, bhi, bp, sl, blo, bhi)  # |w| d, canonical; the sign is absorbed by the orientation
-    return True
+    return False, True
 
 
 def gmul(sg, ms, x, wlo, whi, olo, ohi, zero_hi=True):
@@ -438,8 +451,7 @@ class Body:
                     ct(sg, sl, a, b, S)
                 canon[r] = canon[r + dist] = False
             else:
-                canon[r + dist] = gs(sg, sl, a, b, S, canon[r], canon[r + dist])
-                canon[r] = False
+                canon[r], canon[r + dist] = gs(sg, sl, a, b, S, canon[r], canon[r + dist])
             bf += 1
         for i, op in enumerate(sg.ops):
             op.idx = i
