@@ -514,6 +514,8 @@ def gen_bases(src, dst):
 LOAD_POLICY = ""
 STORE_POLICY = ""
 INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
+FWD_STORE = "t2"     # forward output: "t2" LDS transpose to W0 + coalesced rows; "x2" / "x4": each lane stores its
+                     # 32 consecutive outputs from the lane-pair layout directly (8- / 16-byte stores, %[pso])
 
 
 def load_rows(dmap, base, voff="%[l8]"):
@@ -876,12 +878,38 @@ def gen_fwd(tabs, stop=None):
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    if FWD_STORE != "t2" and not stop:
+        dmap = fwd_core(B, tabs, dmap, stop="last", prefetch=True)
+        B.raw(*direct_stores(dmap, FWD_STORE))
+        return B
     dmap = fwd_core(B, tabs, dmap, stop=stop, prefetch=True)
     if stop:
         B.raw(*store_raw(dmap))
         return B
     B.raw(*store_rows(dmap, S_GB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
+
+
+def direct_stores(dmap, mode):
+    """After the lane-pair stage lane 2 i + par holds (x[k], x[k+16]) = outputs 64 i + 32 par + 2 k, + 1
+    (k < 16): store them straight from registers at %[pso] = 512 i + 256 par (bytes) + 16 k."""
+    out = []
+    if mode == "x2":
+        for k in range(16):
+            out.append(f"global_store_dwordx2 %[pso], {pv(dmap[k])}, s[{S_GB}:{S_GB + 1}] offset:{16 * k}")
+            out.append(f"global_store_dwordx2 %[pso], {pv(dmap[k + 16])}, s[{S_GB}:{S_GB + 1}] offset:{16 * k + 8}")
+        return out
+    busy = set()
+    for b in dmap:
+        busy.update((b, b + 1))
+    quads = [q for q in range(VLO, VHI, 4) if not any(r in busy for r in range(q, q + 4))]
+    assert len(quads) >= 4, quads
+    for k in range(16):
+        q = quads[k % len(quads)]
+        out.append(f"v_mov_b64 v[{q}:{q + 1}], {pv(dmap[k])}")
+        out.append(f"v_mov_b64 v[{q + 2}:{q + 3}], {pv(dmap[k + 16])}")
+        out.append(f"global_store_dwordx4 %[pso], v[{q}:{q + 3}], s[{S_GB}:{S_GB + 1}] offset:{16 * k}")
+    return out
 
 
 INV_PRE_LW = 40          # v40..v43: the inverse lane-pair table twiddles, loaded with the data

@@ -22,7 +22,8 @@ static constexpr int WAVE_LDS2 = 1088;
 
 #define FWD_ARGS                                                                                              \
   [g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8),          \
-      [t1w] "v"(t1w), [t1r] "v"(t1r), [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r), [lwo] "v"(lwo)
+      [t1w] "v"(t1w), [t1r] "v"(t1r), [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r), [lwo] "v"(lwo),        \
+      [pso] "v"(pso)
 #define INV_ARGS                                                                                              \
   [g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8),          \
       [t1w] "v"(t1w), [t1r] "v"(t1r), [t4w] "v"(t4w), [t4r] "v"(t4r), [lwo] "v"(lwo)
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(64 * W) void probe_kernel(u64* __restrict__ data, u
     const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
     const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
     const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
+    const uint32_t pso = i * 512 + par * 256;
     if constexpr (V == 0) MI_TW_BODY_FWD_V0(FWD_ARGS);
     if constexpr (V == 1) MI_TW_BODY_FWD_V1(FWD_ARGS);
     if constexpr (V == 2) MI_TW_BODY_FWD_V2(FWD_ARGS);
@@ -147,11 +149,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (int it = 0; it < 20000; ++it) launch_v(0, it & 1 ? false : true, data, batch, twist, s);  // clock settles
-  const int K = 1000, R = 5;
+  // rounds visit the variants in a rotated order, so no variant always follows the same one (the power-capped
+  // clock carries heat from one timed block into the next)
+  const int K = 300, R = 2 * nv + 1;
   std::vector<std::vector<double>> fw(nv), iv(nv);
   for (int r = 0; r < R; ++r)
-    for (int v = 0; v < nv; ++v)
+    for (int vi = 0; vi < nv; ++vi)
       for (int d = 0; d < 2; ++d) {
+        const int v = (vi + r) % nv;
         CK(hipEventRecord(e0, s));
         for (int it = 0; it < K; ++it) launch_v(v, d == 0, data, batch, twist, s);
         CK(hipEventRecord(e1, s));
