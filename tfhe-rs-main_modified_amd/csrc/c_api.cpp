@@ -157,11 +157,20 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
           b = mi::host::mul_mod(b, rho_inv, p);
         }
       }
-      // one allocation [fwd | inverse | inverse with N^-1 folded into the untwist rows]; the PBS /
-      // external-product bodies address all three from one base (pbs_tw.hip)
+      // one allocation [fwd | inverse | inverse with N^-1 folded into the untwist rows | the inverse's
+      // last-DIT-stage twiddles]; the PBS / external-product bodies address the first three from one base
+      // (pbs_tw.hip), the standalone inverse its untwist rows and the last region (ntt64_tw.hip)
       std::vector<u64> tn(ti);
       for (unsigned e = 0; e < n; ++e) tn[e] = mi::host::mul_mod(ti[e], plan->n_inv, p);
-      if (hipMalloc(&plan->d_twist_f, 3 * (n + 32) * sizeof(u64)) == hipSuccess &&
+      // the standalone inverse's last DIT stage (joins j and j + 32 across a lane pair): entry m + 16 par is
+      // 2^e with e = -3 (2 m + par) mod 192 = omega^-(2 m + par) (tools/gen_tw_kernel.py inv_last_exp)
+      std::vector<u64> tl(32);
+      for (unsigned m = 0; m < 16; ++m)
+        for (unsigned par = 0; par < 2; ++par)
+          tl[m + 16 * par] = mi::host::exp_mod(2, (u64)((192 - 3 * (2 * m + par) % 192) % 192), p);
+      if (hipMalloc(&plan->d_twist_f, (3 * (n + 32) + 32) * sizeof(u64)) == hipSuccess &&
+          hipMemcpy(plan->d_twist_f + 3 * (n + 32), tl.data(), 32 * sizeof(u64), hipMemcpyHostToDevice) ==
+              hipSuccess &&
           hipMemcpy(plan->d_twist_f, tf.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess &&
           hipMemcpy(plan->d_twist_f + n + 32, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
               hipSuccess &&

@@ -42,19 +42,25 @@ namespace tw {
 // wrapper only derives the wave's polynomial and the per-lane LDS / global addresses.
 static constexpr int WAVE_LDS2 = 1088;  // u64: max(32 x 34, 16 x 66)
 
-// One wave per workgroup: a finished wave frees its slot (and its 8.5 KiB of LDS) at once instead of waiting for
-// the other waves of a 4-wave group, so the next polynomial starts sooner.  tools/variant_probe.hip, same process,
-// rotated order: forward 57.5 vs 59.8 us, inverse 60.4 vs 61.3 us per 8192-poly launch (2-wave groups in between,
-// 8-wave groups 9 % slower).
+// Waves per workgroup, measured (tools/variant_probe.hip: same process, rotated order, identical-body controls):
+// the forward runs best with one wave per group (a finished wave frees its slot and its 8.5 KiB of LDS at once:
+// 57.5 vs 59.8 us per 8192-poly launch with 4-wave groups); the inverse, whose W1'' transposes read with half
+// the lanes, with four (60.5 vs 62.4 us with one).
 template <bool FWD>
-__global__ __launch_bounds__(64) void ntt_tw_body_kernel(u64* __restrict__ data, uint32_t batch, uint64_t stride,
-                                                         const u64* __restrict__ twist) {
-  __shared__ u64 lds[WAVE_LDS2];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t poly = blockIdx.x;
+constexpr uint32_t tw_waves() { return FWD ? 1u : 4u; }
+
+template <bool FWD>
+__global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* __restrict__ data, uint32_t batch,
+                                                                          uint64_t stride,
+                                                                          const u64* __restrict__ twist) {
+  constexpr uint32_t W = tw_waves<FWD>();
+  __shared__ u64 lds[W * WAVE_LDS2];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t poly = blockIdx.x * W + wv;
   if (poly >= batch) return;
   u64* p = data + (uint64_t)poly * stride;
-  const uint32_t S = (uint32_t)(uintptr_t)lds;
+  const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
   const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
   const uint32_t t1w = S + (lane & 31) * 8;
@@ -62,7 +68,9 @@ __global__ __launch_bounds__(64) void ntt_tw_body_kernel(u64* __restrict__ data,
   const uint32_t lwo = par * 128;
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
-  const u64* lw = twist + 2048;
+  // forward: the lane-pair twiddles follow the twist rows; inverse: the last-DIT-stage table, two regions on
+  // (the plan's allocation: [fwd + 32 | inverse + 32 | inverse N^-1 + 32 | 32], `twist` = the inverse region)
+  const u64* lw = FWD ? twist + 2048 : twist + 2 * (2048 + 32);
   if constexpr (FWD) {
     const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
     const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
@@ -72,10 +80,10 @@ __global__ __launch_bounds__(64) void ntt_tw_body_kernel(u64* __restrict__ data,
                    [t2r] "v"(t2r), [lwo] "v"(lwo));
   } else {
     const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
-    const uint32_t t4r = S + lane * 8;
+    const uint32_t t1x = S + (lane + (lane >> 5)) * 8;        // W0 side of the W1'' transposes
+    const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;  // W1'' side
     MI_TW_BODY_INV([g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw),
-                   [l8] "v"(l8), [t1w] "v"(t1w), [t1r] "v"(t1r), [t4w] "v"(t4w), [t4r] "v"(t4r),
-                   [lwo] "v"(lwo));
+                   [l8] "v"(l8), [t4w] "v"(t4w), [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo));
   }
 }
 
@@ -87,10 +95,15 @@ hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, 
   for (size_t off = 0; off < batch; off += CHUNK) {
     const uint32_t n = (uint32_t)std::min(CHUNK, batch - off);
     uint64_t* d = data + off * stride;
-    if (fwd)
-      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<true>), dim3(n), dim3(64), 0, s, d, n, (uint64_t)stride, twist);
-    else
-      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<false>), dim3(n), dim3(64), 0, s, d, n, (uint64_t)stride, twist);
+    if (fwd) {
+      constexpr uint32_t W = tw::tw_waves<true>();
+      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<true>), dim3((n + W - 1) / W), dim3(64 * W), 0, s, d, n,
+                         (uint64_t)stride, twist);
+    } else {
+      constexpr uint32_t W = tw::tw_waves<false>();
+      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<false>), dim3((n + W - 1) / W), dim3(64 * W), 0, s, d, n,
+                         (uint64_t)stride, twist);
+    }
   }
   return hipGetLastError();
 }

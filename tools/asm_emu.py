@@ -390,7 +390,8 @@ def run_body(hdr, name, poly, twist_tab, fwd=True):
     w = Wave(None, mem)
     vin = {"l8": lane * 8, "t1w": S + (lane & 31) * 8, "t1r": S + (i * 34 + par) * 8, "lwo": par * 128,
            "t2wl": S + ((i & 15) * 66 + 33 * par) * 8, "t2wh": S + ((i & 15) * 66 + 31 * par + 1) * 8,
-           "t2r": S + (lane ^ (lane >> np.uint64(5))) * 8, "t4w": S + ((i & 15) * 66 + par) * 8, "t4r": S + lane * 8}
+           "t2r": S + (lane ^ (lane >> np.uint64(5))) * 8, "t4w": S + ((i & 15) * 66 + par) * 8, "t4r": S + lane * 8,
+           "t1x": S + (lane + (lane >> np.uint64(5))) * 8, "t1y": S + ((i & 15) * 66 + 33 * par) * 8}
     for k, (name_, val) in enumerate(vin.items()):
         w.v[200 + k] = val.astype(np.uint64)   # outside the body's v8..v127
         ops[name_] = f"v{200 + k}"

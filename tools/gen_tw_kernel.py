@@ -429,7 +429,7 @@ class Body:
             sl.append(Slot(b, SG0 + 6 * i))
         return sl
 
-    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None, by_reg=False):
+    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None, by_reg=False, group_waits=None):
         """canon: list of 32 flags (logical registers known canonical), updated in place.  The twiddle
         exponent of the butterfly on registers (r, r + dist) is exps[r // (2 dist)] (one per group, the
         natural-in CT / GS stages), or exps[r] with by_reg (one per position, the DIT stages)."""
@@ -441,6 +441,12 @@ class Body:
         for r in range(32):
             if r & dist:
                 continue
+            if group_waits and bf % 4 == 0:  # flush the previous group, wait for the next group's rows
+                for i, op in enumerate(sg.ops):
+                    op.idx = i
+                self.out(sg.schedule())
+                self.raw(group_waits[bf // 4])
+                sg = Seg()
             S = exps[r] if by_reg else exps[r // (2 * dist)]
             sl = slots[bf % len(slots)]
             a, b = X(dmap, r), X(dmap, r + dist)
@@ -514,6 +520,9 @@ def gen_bases(src, dst):
 LOAD_POLICY = ""
 STORE_POLICY = ""
 INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
+PROGRESSIVE = True   # forward: start the first stage as the data rows arrive (4 waits) instead of one vmcnt(0):
+                     # 0.6 % faster (tools/variant_probe); the same per row in the inverse's T1 was 0.8 % slower
+PROGRESSIVE_INV = False
 FWD_STORE = "t2"     # forward output: "t2" LDS transpose to W0 + coalesced rows; "x2" / "x4": each lane stores its
                      # 32 consecutive outputs from the lane-pair layout directly (8- / 16-byte stores, %[pso])
 
@@ -555,14 +564,17 @@ class Addr:
 
 NTT_ADDR = Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] "
                                    f"offset:{512 * k}",
-                **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw")})
+                **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw", "t1x", "t1y")})
 
 
-def t1(body, dmap, ybase, newhi, ad=NTT_ADDR):
-    """W0 -> W1 (split by j half).  Returns the new dmap (x[q] in y for q < 16, x[16+q] at newhi)."""
+def t1(body, dmap, ybase, newhi, ad=NTT_ADDR, row_waits=None):
+    """W0 -> W1 (split by j half).  Returns the new dmap (x[q] in y for q < 16, x[16+q] at newhi).
+    row_waits: a wait line before each first-half row write (rows written as their loads land)."""
     L = []
     L += [f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"]
     for r in range(32):
+        if row_waits:
+            L.append(row_waits[r])
         L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * 34 * 8}")
     L += EXEC_ALL
     for q in range(16):
@@ -605,12 +617,12 @@ def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
     return [ybase + 2 * r for r in range(16)] + [newhi + 2 * r for r in range(16)]
 
 
-def regroup(sg, dmap, k, tmp, to_pairs):
-    """W1 <-> W1' for register pair (k, k+16) of this lane and its partner (lane ^ 1).
-    to_pairs: even lane ends with (a_k, b_k), odd lane with (a_{k+16}, b_{k+16}).
-    back:     even lane ends with (a_k, a_{k+16}), odd lane with (b_k, b_{k+16})."""
+def regroup(sg, dmap, k, tmp, to_pairs, k2=None):
+    """W1 <-> W1' for register pair (k, k2 = k+16) of this lane and its partner (lane ^ 1).
+    to_pairs: even lane ends with (a_k, b_k), odd lane with (a_{k2}, b_{k2}).
+    back:     even lane ends with (a_k, a_{k2}), odd lane with (b_k, b_{k2})."""
     lo0, hi0, p0 = X(dmap, k)
-    lo1, hi1, p1 = X(dmap, k + 16)
+    lo1, hi1, p1 = X(dmap, k + 16 if k2 is None else k2)
     T0, T1, U0, U1 = tmp
     par = f"s[{S_PAR}:{S_PAR + 1}]"
     dpp = "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
@@ -841,7 +853,10 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False):
         B.raw(*[ad.tw_load(0, k, 8 + 2 * k) for k in range(8)])
     fb = free_blocks_except(dmap, busy)
     for s in range(5):
-        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb)
+        gw = None
+        if s == 0 and PROGRESSIVE and prefetch:  # rows issued as pairs (k, k + 16), then the 8 twist-row loads
+            gw = [f"s_waitcnt vmcnt({40 - 8 * (g + 1)})" for g in range(4)]
+        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb, group_waits=gw)
     if stop == "g1":
         return dmap
     # twist: 4 batches of 8 rows; table rows double-buffered in v8..v23 / v48..v63 (batch bt + 1
@@ -877,7 +892,11 @@ def gen_fwd(tabs, stop=None):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
-    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    if PROGRESSIVE and not stop:
+        rows = load_rows(dmap, S_GB)
+        B.raw(*[rows[r] for k in range(16) for r in (k, k + 16)])
+    else:
+        B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     if FWD_STORE != "t2" and not stop:
         dmap = fwd_core(B, tabs, dmap, stop="last", prefetch=True)
         B.raw(*direct_stores(dmap, FWD_STORE))
@@ -933,27 +952,146 @@ def dit_exps(s):
     return [(-3 * (64 >> s) * (r % d)) % 192 for r in range(32)]
 
 
-def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False):
+INV_W1PP = True  # standalone inverse: cyclic blocks in the W1'' layout (t1_w1pp / dit_exps_pp / pair_stage_dit)
+
+
+def inv_last_exp(r):
+    """Twiddle exponent of the last DIT stage (j, j + 32) of the inverse cyclic blocks, k = j mod 32 = r."""
+    return (-3 * r) % 192
+
+
+def dit_exps_pp(s):
+    """DIT stage s = 0..4 of the inverse cyclic blocks in W1'' (register r = j & 31, distance 2^s):
+    w = omega^-(k 64 / 2^(s+1)), k = r mod 2^s, compile-time per register (the lane bit j5 is not in k)."""
+    return [(-3 * (32 >> s) * (r % (1 << s))) % 192 for r in range(32)]
+
+
+def t1_w1pp(body, dmap, dst, ad=NTT_ADDR):
+    """W0 (lane = j, register = block i) -> W1'' (lane = 2 i + j5, register r = j & 31) through LDS, halves split
+    by i: every lane writes rows i = 16 h .. 16 h + 15 at (i & 15) 66 + j + (j >> 5) (%[t1x]); lanes 32 h .. 32 h + 31
+    (blocks 16 h ..) read their 32 values at (i & 15) 66 + 33 j5 + r (%[t1y]).  Rows 16.. stay live in half 0, so
+    `dst` may reuse only the registers of rows 0..15.  Conflict-free both ways (tools/lds_layout_check.py)."""
+    L = []
+    for h in range(2):
+        for rho in range(16):
+            L.append(f"ds_write_b64 {ad.t1x}, {pv(dmap[16 * h + rho])} offset:{rho * 66 * 8}")
+        L.append("s_waitcnt lgkmcnt(0)")
+        L += EXEC_LO if h == 0 else EXEC_HI
+        for r in range(32):
+            L.append(f"ds_read_b64 {pv(dst[r])}, {ad.t1y} offset:{r * 8}")
+        L += EXEC_ALL
+        L.append("s_waitcnt lgkmcnt(0)")
+    body.raw(*L)
+    return list(dst)
+
+
+def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR):
+    """After pair_stage_dit lane 2 i + par holds output n = 2 m + par + 32 q in register 2 m + q: -> W0 through
+    LDS, halves split by i (rows (i & 15) 66, columns n + (n >> 5)); reads at %[t1x] + 66 rho."""
+    L = []
+    for h in range(2):
+        L += EXEC_LO if h == 0 else EXEC_HI
+        for R in range(32):
+            off = 2 * (R >> 1) + 33 * (R & 1)
+            L.append(f"ds_write_b64 {ad.t4w}, {pv(dmap[R])} offset:{off * 8}")
+        L += EXEC_ALL
+        L.append("s_waitcnt lgkmcnt(0)")
+        dst = ybase if h == 0 else newhi
+        for rho in range(16):
+            L.append(f"ds_read_b64 {pv(dst + 2 * rho)}, {ad.t1x} offset:{rho * 66 * 8}")
+        L.append("s_waitcnt lgkmcnt(0)")
+    body.raw(*L)
+    return [ybase + 2 * r for r in range(16)] + [newhi + 2 * r for r in range(16)]
+
+
+def pair_stage_dit_gmul_ms():
+    return [m for m in range(16) if not lane_tmul_applies(inv_last_exp(2 * m), inv_last_exp(2 * m + 1))]
+
+
+def pair_stage_dit(B, dmap, ad, pre, busy):
+    """Last DIT stage of the inverse cyclic blocks in W1'': j and j + 32 sit in the two lanes of a pair (register
+    r = j & 31).  Regroup registers (2 m, 2 m + 1) across the pair (even lane: elements 2 m, 2 m + 32; odd lane:
+    2 m + 1, 2 m + 33), then a CT butterfly whose twiddle exponent differs by 3 between the lanes (tmul_lane), or
+    a general multiply by the lane's table value (entry m + 16 par of the inverse's DIT table, preloaded into
+    `pre`[m]).  Outputs: register 2 m + q holds n = 2 m + par + 32 q."""
+    regs = []
+    for b in free_blocks_except(dmap, busy):
+        regs += list(range(b, b + 8))
+    assert len(regs) >= 40, len(regs)
+    tmps = [regs[0:4], regs[4:8]]
+    amts = [regs[8:10], regs[10:12]]
+    msl = [MulSlot(regs[16], SG0), MulSlot(regs[28], SG0 + 6)]
+    c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
+    par3 = f"v{regs[12]}"
+    B.raw(f"v_cndmask_b32_e64 {par3}, 0, 3, s[{S_PAR}:{S_PAR + 1}]")
+    if pre:
+        B.raw(ad.lw_wait or ad.tw_wait)
+    for half in range(2):
+        sg = Seg()
+        for i, m in enumerate(range(8 * half, 8 * half + 8)):
+            tmp = [f"v{r}" for r in tmps[i % 2]]
+            mm = msl[i % 2]
+            sl = slot_view(mm, c23[i % 2])
+            Se, So = inv_last_exp(2 * m), inv_last_exp(2 * m + 1)
+            regroup(sg, dmap, 2 * m, tmp, True, k2=2 * m + 1)
+            a, b = X(dmap, 2 * m), X(dmap, 2 * m + 1)
+            if lane_tmul_applies(Se, So):
+                neg = tmul_lane(sg, Se, So, b, sl, sl.v[2], sl.v[3], par3, tuple(f"v{r}" for r in amts[i % 2]))
+                ct_core(sg, sl, a, b, neg)
+            else:
+                gmul(sg, mm, b, f"v{pre[m]}", f"v{pre[m] + 1}", mm.v[8], mm.v[9])
+                ct_sl = Slot.__new__(Slot)
+                ct_sl.v = [mm.v[0], mm.v[1], mm.v[8], mm.v[9], mm.v[4], mm.v[5], mm.v[6], mm.v[7]]
+                ct_sl.P = [mm.P[0], None, None, mm.P[3]]
+                ct_sl.c = sl.c
+                ct_core(sg, ct_sl, a, b, False)
+        for j, op in enumerate(sg.ops):
+            op.idx = j
+        B.out(sg.schedule())
+
+
+def inv_cyc_w1pp(B, dmap, ad):
+    """Standalone inverse: W0 data -> T1'' -> DIT stages 0..4 in registers -> the lane-pair DIT stage -> W0.
+    The lane-pair stage's table twiddles load right after T1'' (into v72..), five stages ahead of their use."""
+    dmap = t1_w1pp(B, dmap, [8 + 2 * r for r in range(32)], ad)
+    ms = pair_stage_dit_gmul_ms()
+    pre = {m: 72 + 2 * i for i, m in enumerate(ms)}
+    assert len(ms) <= 4
+    busy = tuple(range(72, 80))
+    B.raw(*[ad.lw_load(r, m) for m, r in pre.items()])
+    fb = free_blocks_except(dmap, busy)
+    cf = [True] * 32  # loaded data is canonical
+    for s in range(5):
+        B.stage("ct", 1 << s, dit_exps_pp(s), dmap, fb, cf, by_reg=True)
+    pair_stage_dit(B, dmap, ad, pre, busy)
+    return t_w1pp_w0(B, dmap, 96, 64, ad)
+
+
+def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False):
     """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  `prefetch`
     (standalone kernel, see fwd_core): the caller has loaded the lane-pair table twiddles into
     v40..v43 with the data; the first untwist batch is loaded into v40..v55 after the lane-pair stage
     and stays there through the cyclic stages and T4 (the one register range free in both layouts)."""
-    dmap = t1(B, dmap, 8, 64, ad)
-    gks = pair_stage_gmul_ks(tabs, False)
-    pre = {k: INV_PRE_LW + 2 * i for i, k in enumerate(gks)} if prefetch else None
-    pair_stage(B, dmap, False, ad, tabs, pre, tuple(range(INV_PRE_LW, INV_PRE_LW + 8)) if prefetch else ())
-    busy = tuple(range(INV_PRE_TW, INV_PRE_TW + 16)) if prefetch else ()
-    if prefetch:
-        B.raw(*[ad.tw_load(0, k, INV_PRE_TW + 2 * k) for k in range(8)])
-    fb = free_blocks_except(dmap, busy)
-    cf = [False] * 32
-    if INV_CYC_DIT:
-        for s in range(1, 6):
-            B.stage("ct", 1 << (s - 1), dit_exps(s), dmap, fb, cf, by_reg=True)
-    else:  # r2 form (GS, canonical subtrahends), kept for tools/variant_probe A/B runs
-        for q in range(4, -1, -1):
-            B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
-    dmap = t_iw0(B, dmap, False, 96, 64, ad)
+    if w1pp:
+        dmap = inv_cyc_w1pp(B, dmap, ad)
+        prefetch, busy = False, ()
+    else:
+        dmap = t1(B, dmap, 8, 64, ad, row_waits)
+        gks = pair_stage_gmul_ks(tabs, False)
+        pre = {k: INV_PRE_LW + 2 * i for i, k in enumerate(gks)} if prefetch else None
+        pair_stage(B, dmap, False, ad, tabs, pre, tuple(range(INV_PRE_LW, INV_PRE_LW + 8)) if prefetch else ())
+        busy = tuple(range(INV_PRE_TW, INV_PRE_TW + 16)) if prefetch else ()
+        if prefetch:
+            B.raw(*[ad.tw_load(0, k, INV_PRE_TW + 2 * k) for k in range(8)])
+        fb = free_blocks_except(dmap, busy)
+        cf = [False] * 32
+        if INV_CYC_DIT:
+            for s in range(1, 6):
+                B.stage("ct", 1 << (s - 1), dit_exps(s), dmap, fb, cf, by_reg=True)
+        else:  # r2 form (GS, canonical subtrahends), kept for tools/variant_probe A/B runs
+            for q in range(4, -1, -1):
+                B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
+        dmap = t_iw0(B, dmap, False, 96, 64, ad)
     # untwist: table rows and multiply slots in the registers the data does not occupy
     free = free_blocks_except(dmap, busy)
     regs = []
@@ -988,10 +1126,19 @@ def gen_inv(tabs, stop=None):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    if INV_W1PP:
+        B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+        dmap = inv_core(B, tabs, dmap, w1pp=True)
+        B.raw(*store_rows(dmap, S_GB))
+        return B
     gks = pair_stage_gmul_ks(tabs, False)
-    B.raw(*load_rows(dmap, S_GB), *[NTT_ADDR.lw_load(INV_PRE_LW + 2 * i, k) for i, k in enumerate(gks)],
-          "s_waitcnt vmcnt(0)")
-    dmap = inv_core(B, tabs, dmap, prefetch=True)
+    B.raw(*load_rows(dmap, S_GB), *[NTT_ADDR.lw_load(INV_PRE_LW + 2 * i, k) for i, k in enumerate(gks)])
+    rw = None
+    if PROGRESSIVE_INV:  # row r is written to LDS once it has landed (the pair twiddles are waited for later)
+        rw = [f"s_waitcnt vmcnt({32 + len(gks) - 1 - r})" for r in range(32)]
+    else:
+        B.raw("s_waitcnt vmcnt(0)")
+    dmap = inv_core(B, tabs, dmap, prefetch=True, row_waits=rw)
     B.raw(*store_rows(dmap, S_GB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
 
