@@ -174,3 +174,19 @@ def test_ct_butterfly_canonical_outputs(S, shuffle):
     for x, y, s, d in zip(a, b, out[X_A], out[X_B]):
         assert s < P and d < P, (S, hex(x), hex(y), hex(s), hex(d))
         assert s == (x + y * w) % P and d == (x - y * w) % P, (S, hex(x), hex(y))
+
+
+def test_modswitch_native_corners():
+    """modswitch_native (the key conversion's native 2^64 -> Z_p switch) == (x p + 2^63) >> 64, ntt64.rs:166-178."""
+    rnd = random.Random(11)
+    for rep in range(4):
+        xs = corner_values(rnd, False)
+        if rep == 0:
+            xs[:12] = [0, 1, M64, M64 - 1, 1 << 63, (1 << 63) - 1, 0xFFFFFFFF00000000, 0x80000000FFFFFFFF,
+                       0x7FFFFFFF00000000, 0x7FFFFFFFFFFFFFFF, 0x80000000_80000000, 0x7FFFFFFF_80000000]
+        sg = G.Seg()
+        sg.add(f"s_mov_b32 s{G.S_H31}, 0x80000000", [], [f"s{G.S_H31}"], "salu")
+        G.modswitch_native(sg, slot(), G.X([X_A], 0))
+        out = run_seg(sg, {X_A: xs}, [X_A])[X_A]
+        for x, y in zip(xs, out):
+            assert y == (x * P + (1 << 63)) >> 64 and y < P, hex(x)

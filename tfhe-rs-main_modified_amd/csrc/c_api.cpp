@@ -158,8 +158,9 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
         }
       }
       // one allocation [fwd | inverse | inverse with N^-1 folded into the untwist rows | the inverse's
-      // last-DIT-stage twiddles]; the PBS / external-product bodies address the first three from one base
-      // (pbs_tw.hip), the standalone inverse its untwist rows and the last region (ntt64_tw.hip)
+      // last-DIT-stage twiddles | fwd with N^-1 folded into the twist rows]; the PBS / external-product bodies
+      // address the first three from one base (pbs_tw.hip), the standalone inverse its untwist rows and the
+      // fourth region, the normalising key conversion the last (ntt64_tw.hip)
       std::vector<u64> tn(ti);
       for (unsigned e = 0; e < n; ++e) tn[e] = mi::host::mul_mod(ti[e], plan->n_inv, p);
       // the standalone inverse's last DIT stage (joins j and j + 32 across a lane pair): entry m + 16 par is
@@ -168,15 +169,20 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
       for (unsigned m = 0; m < 16; ++m)
         for (unsigned par = 0; par < 2; ++par)
           tl[m + 16 * par] = mi::host::exp_mod(2, (u64)((192 - 3 * (2 * m + par) % 192) % 192), p);
-      if (hipMalloc(&plan->d_twist_f, (3 * (n + 32) + 32) * sizeof(u64)) == hipSuccess &&
+      std::vector<u64> tfn(tf);  // the normalising key conversion's forward twist (lane-pair twiddles unscaled)
+      for (unsigned e = 0; e < n; ++e) tfn[e] = mi::host::mul_mod(tf[e], plan->n_inv, p);
+      if (hipMalloc(&plan->d_twist_f, (4 * (n + 32) + 32) * sizeof(u64)) == hipSuccess &&
           hipMemcpy(plan->d_twist_f + 3 * (n + 32), tl.data(), 32 * sizeof(u64), hipMemcpyHostToDevice) ==
               hipSuccess &&
+          hipMemcpy(plan->d_twist_f + 3 * (n + 32) + 32, tfn.data(), (n + 32) * sizeof(u64),
+                    hipMemcpyHostToDevice) == hipSuccess &&
           hipMemcpy(plan->d_twist_f, tf.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess &&
           hipMemcpy(plan->d_twist_f + n + 32, ti.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
               hipSuccess &&
           hipMemcpy(plan->d_twist_f + 2 * (n + 32), tn.data(), (n + 32) * sizeof(u64), hipMemcpyHostToDevice) ==
               hipSuccess) {
         plan->d_twist_i = plan->d_twist_f + n + 32;
+        plan->d_twist_fn = plan->d_twist_f + 3 * (n + 32) + 32;
       } else {
         if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);
         plan->d_twist_f = plan->d_twist_i = nullptr;
@@ -382,6 +388,11 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
     return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {1024, 2048, 4096}");
   if (n_polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "too many polynomials");
   DeviceGuard g(plan->device);
+  if (plan->twisted && in_modulus_width == 64) {  // the fused twisted-body conversion (ntt64_tw.hip)
+    hipError_t e = mi::launch_ntt_tw_ms64(bsk_ntt, bsk_std, n_polys, normalize ? plan->d_twist_fn : plan->d_twist_f,
+                                          (hipStream_t)stream);
+    return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
+  }
   hipError_t e = mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0, plan->n_inv,
                                        plan->d_twid, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");

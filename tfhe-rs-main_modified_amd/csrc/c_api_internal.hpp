@@ -30,6 +30,7 @@ struct mi_ntt64_plan {
   // twisted N = 2048 Solinas transform (ntt64_tw.hip): rho_i^j and rho_i^-j, 64 i + j
   u64* d_twist_f = nullptr;
   u64* d_twist_i = nullptr;
+  u64* d_twist_fn = nullptr;  // forward twist rows x N^-1 + the forward lane-pair twiddles (normalising key conversion)
 };
 
 struct mi_pbs_ntt64_key {

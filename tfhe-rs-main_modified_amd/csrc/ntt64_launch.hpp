@@ -24,6 +24,9 @@ hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, con
 
 // Twisted shift-twiddle transform (ntt64_tw.hip): Solinas prime, N = 2048 only.  `twist` = the
 // plan's rho_i^j table (forward) or rho_i^-j table (inverse), 2048 u64 each.
+// key conversion of native-modulus polynomials (N = 2048 Solinas plan): dst = fwd(modswitch_{2^64 -> p}(src))
+hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
+                              hipStream_t s);
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
                          hipStream_t s);
 

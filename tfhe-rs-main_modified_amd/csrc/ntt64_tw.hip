@@ -87,7 +87,48 @@ __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* 
   }
 }
 
+// Key conversion, native 2^64 input (convert_standard_lwe_bootstrap_key_to_ntt64,
+// lwe_bootstrap_key_conversion.rs:294-365 with ntt64.rs:166-178): each wave loads one standard-domain polynomial,
+// switches it into Z_p, runs the forward body and writes the NTT-domain polynomial to `dst` (may equal `src`: a
+// wave reads its whole polynomial before writing).  `twist` = the plan's forward table, or its N^-1-scaled copy for
+// the Normalize variant (the twist multiplies every element exactly once, so the output is fwd(x) N^-1).
+__global__ __launch_bounds__(64) void ntt_tw_ms64_kernel(u64* dst, const u64* src, uint32_t n_polys,
+                                                         const u64* __restrict__ twist) {
+  __shared__ u64 lds[WAVE_LDS2];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t poly = blockIdx.x;
+  if (poly >= n_polys) return;
+  const u64* p = src + (uint64_t)poly * 2048;
+  u64* q = dst + (uint64_t)poly * 2048;
+  const uint32_t S = (uint32_t)(uintptr_t)lds;
+  const uint32_t par = lane & 1, i = lane >> 1;
+  const uint32_t l8 = lane * 8;
+  const uint32_t t1w = S + (lane & 31) * 8;
+  const uint32_t t1r = S + (i * 34 + par) * 8;
+  const uint32_t lwo = par * 128;
+  const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
+  const uint32_t olo = (uint32_t)(uintptr_t)q, ohi = (uint32_t)((uintptr_t)q >> 32);
+  const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
+  const u64* lw = twist + 2048;
+  const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
+  const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
+  const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
+  MI_TW_BODY_FWD_MS64([g_lo] "s"(glo), [g_hi] "s"(ghi), [o_lo] "s"(olo), [o_hi] "s"(ohi), [tw_lo] "s"(twlo),
+                      [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t1w] "v"(t1w), [t1r] "v"(t1r),
+                      [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r), [lwo] "v"(lwo));
+}
+
 }  // namespace tw
+
+hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
+                              hipStream_t s) {
+  constexpr size_t CHUNK = size_t(1) << 30;
+  for (size_t off = 0; off < n_polys; off += CHUNK) {
+    const uint32_t n = (uint32_t)std::min(CHUNK, n_polys - off);
+    hipLaunchKernelGGL(tw::ntt_tw_ms64_kernel, dim3(n), dim3(64), 0, s, dst + off * 2048, src + off * 2048, n, twist);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist, hipStream_t s) {
   if (batch == 0) return hipSuccess;

@@ -377,16 +377,19 @@ def body_lines(hdr, name, prefix="MI_TW_BODY_"):
     return [m.group(1) for m in re.finditer(r'"(.*?)\\n"', txt[start:end])]
 
 
-def run_body(hdr, name, poly, twist_tab, fwd=True):
-    """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial."""
+def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False):
+    """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial.  out_of_place: the body
+    writes another buffer (%[o_lo] / %[o_hi], the key-conversion body), which is returned."""
     data = np.array(poly, dtype=np.uint64).copy()
     tw = np.array(twist_tab, dtype=np.uint64)
-    GB, TB = 0x100000000, 0x200000000
-    mem = {GB: data, TB: tw}
+    GB, TB, OB = 0x100000000, 0x200000000, 0x300000000
+    out = np.zeros_like(data)
+    mem = {GB: data, TB: tw, OB: out}
     lane = np.arange(LANES, dtype=np.uint64)
     par, i = lane & np.uint64(1), lane >> np.uint64(1)
     S = 0
-    ops = {"g_lo": f"{GB & 0xFFFFFFFF}", "g_hi": f"{GB >> 32}", "tw_lo": f"{TB & 0xFFFFFFFF}", "tw_hi": f"{TB >> 32}"}
+    ops = {"g_lo": f"{GB & 0xFFFFFFFF}", "g_hi": f"{GB >> 32}", "tw_lo": f"{TB & 0xFFFFFFFF}", "tw_hi": f"{TB >> 32}",
+           "o_lo": f"{OB & 0xFFFFFFFF}", "o_hi": f"{OB >> 32}"}
     w = Wave(None, mem)
     vin = {"l8": lane * 8, "t1w": S + (lane & 31) * 8, "t1r": S + (i * 34 + par) * 8, "lwo": par * 128,
            "t2wl": S + ((i & 15) * 66 + 33 * par) * 8, "t2wh": S + ((i & 15) * 66 + 31 * par + 1) * 8,
@@ -396,11 +399,12 @@ def run_body(hdr, name, poly, twist_tab, fwd=True):
         w.v[200 + k] = val.astype(np.uint64)   # outside the body's v8..v127
         ops[name_] = f"v{200 + k}"
     lw = TB + 2048 * 8
-    w.s[100], w.s[101] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
-    ops["lw"] = "s[100:101]"
+    # an SGPR pair no body clobbers (the key-conversion body owns s94..s101)
+    w.s[104], w.s[105] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
+    ops["lw"] = "s[104:105]"
     w.ops = ops
     w.run(body_lines(hdr, name))
-    return data
+    return out if out_of_place else data
 
 
 def _lds_with_lane_pair_tables(tab, N):

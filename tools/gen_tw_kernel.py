@@ -909,6 +909,53 @@ def gen_fwd(tabs, stop=None):
     return B
 
 
+S_OB = 94      # s[94:101]: output row-group bases (the key-conversion body writes another buffer)
+S_H31 = 28     # s28 = 0x80000000 (a VOP3 operand cannot be a 32-bit literal on gfx950)
+MS_SGPRS = list(range(S_OB, S_OB + 8))
+
+
+def modswitch_native(sg, sl, x):
+    """x <- (x p + 2^63) >> 64, the native-modulus switch into Z_p of the key conversion (ntt64.rs:166-178,
+    lwe_bootstrap_key_conversion.rs:294-365, in_width 64).  With x = x_hi 2^32 + x_lo and p = 2^64 - 2^32 + 1:
+    x p + 2^63 = x 2^64 + (x + 2^63 - x_lo 2^32) - x_hi 2^64, so the result is x - x_hi + c1 - b2 with
+    c1 = carry(x_hi + 2^31) and b2 = borrow((x_hi + 2^31) mod 2^32 - x_lo); no intermediate wraps and the result
+    is canonical (x = 2^64 - 1 gives p - 1).  8 carry ops."""
+    xlo, xhi, _ = x
+    v, c = sl.v, sl.c
+    t = v[0]
+    sg.add(f"v_add_co_u32_e64 {t}, {c[0]}, {xhi}, s{S_H31}", [xhi, f"s{S_H31}"], [t, c[0]])
+    sg.add(f"v_sub_co_u32_e64 {t}, {c[1]}, {t}, {xlo}", [t, xlo], [t, c[1]])
+    sg.add(f"v_sub_co_u32_e64 {xlo}, {c[2]}, {xlo}, {xhi}", [xlo, xhi], [xlo, c[2]])
+    sg.add(f"v_subb_co_u32_e64 {xhi}, {c[2]}, {xhi}, 0, {c[2]}", [xhi, c[2]], [xhi, c[2]])
+    sg.add(f"v_addc_co_u32_e64 {xlo}, {c[2]}, {xlo}, 0, {c[0]}", [xlo, c[0]], [xlo, c[2]])
+    sg.add(f"v_addc_co_u32_e64 {xhi}, {c[2]}, {xhi}, 0, {c[2]}", [xhi, c[2]], [xhi, c[2]])
+    sg.add(f"v_subb_co_u32_e64 {xlo}, {c[2]}, {xlo}, 0, {c[1]}", [xlo, c[1]], [xlo, c[2]])
+    sg.add(f"v_subb_co_u32_e64 {xhi}, {c[2]}, {xhi}, 0, {c[2]}", [xhi, c[2]], [xhi, c[2]])
+
+
+def gen_fwd_ms64(tabs):
+    """Key conversion body: rows of a standard-domain key (native 2^64 torus) -> modswitch into Z_p -> forward
+    transform -> rows of another buffer (bases %[o_lo] / %[o_hi]).  With the plan's N^-1-scaled twist table the
+    output is also normalised (the twist multiplies every element exactly once)."""
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111",
+          f"s_mov_b32 s{S_H31}, 0x80000000")
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB), *gen_bases("o", S_OB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
+    sg = Seg()
+    sls = B.slots(free_blocks_except(dmap))
+    for r in range(32):
+        modswitch_native(sg, sls[r % len(sls)], X(dmap, r))
+    for i, op in enumerate(sg.ops):
+        op.idx = i
+    B.out(sg.schedule())
+    dmap = fwd_core(B, tabs, dmap, prefetch=True)
+    B.raw(*store_rows(dmap, S_OB))
+    return B
+
+
 def direct_stores(dmap, mode):
     """After the lane-pair stage lane 2 i + par holds (x[k], x[k+16]) = outputs 64 i + 32 par + 2 k, + 1
     (k < 16): store them straight from registers at %[pso] = 512 i + 256 par (bytes) + 16 k."""
@@ -1143,8 +1190,9 @@ def gen_inv(tabs, stop=None):
     return B
 
 
-def emit(name, body, ops_in):
-    clob = [f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in SGPR_CLOBBER] + ['"scc"', '"memory"']
+def emit(name, body, ops_in, sgpr_extra=()):
+    clob = ([f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in list(SGPR_CLOBBER) + list(sgpr_extra)] +
+            ['"scc"', '"memory"'])
     text = "\n".join(f'      "{l}\\n"' for l in body.lines)
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
             f"#define MI_TW_BODY_{name.upper()}(...) asm volatile(\\\n" +
@@ -1160,6 +1208,7 @@ def main():
     print("#pragma once")
     print(emit("fwd", f, None))
     print(emit("inv", i, None))
+    print(emit("fwd_ms64", gen_fwd_ms64(tabs), None, MS_SGPRS))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 
