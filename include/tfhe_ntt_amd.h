@@ -234,9 +234,9 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu *m, const mi_pbs_ntt64_key *const *keys,
  * :406-511): N real u64 coefficients -> N/2 complex values x[n] + i x[n + N/2], twisted by exp(i pi n / N),
  * transformed with an N/2-point DFT (exp(-2 pi i / (N/2)) kernel).  Fourier buffers hold interleaved
  * (re, im) doubles, N/2 complex per polynomial, in this engine's order: position p holds frequency
- * freq[p] (mi_fft64_fourier_order).  The reference's tfhe-fft "unordered" order is implementation defined,
- * so Fourier keys are converted by this engine for this engine.  Results are f64 computations: parity with
- * the reference is decryption-exact and within the FFT error bound, not bit-exact.  This build: N = 2048,
+ * freq[p] (mi_fft64_fourier_order).  The reference's tfhe-fft "unordered" in-memory order is implementation
+ * defined, but its serialised order is the natural one: mi_fft64_to/from_standard_order convert to and from
+ * it.  Results are f64 computations: parity with the reference is decryption-exact and within the FFT error bound, not bit-exact.  This build: N = 2048,
  * GLWE dimension k in {1, 2}, any decomposition with base_log * level < 64. */
 typedef struct mi_fft64_plan mi_fft64_plan;
 /* Fft::new (fft_impl/fft64/math/fft/mod.rs:170-223): MI_ERR_INVALID_ARG if n is not a power of two,
@@ -248,6 +248,16 @@ int mi_fft64_plan_destroy(mi_fft64_plan *plan);
 int mi_fft64_plan_info(const mi_fft64_plan *plan, size_t *n, int *device);
 /* freq[p] for p < n/2: the DFT frequency stored at Fourier position p (host call) */
 int mi_fft64_fourier_order(const mi_fft64_plan *plan, uint32_t *freq);
+/* The reference's serialised Fourier order (FourierPolynomialList's serde, fft_impl/fft64/math/fft/mod.rs:642-690,
+ * through tfhe-fft's Plan::serialize_fourier_buffer / deserialize_fourier_buffer, tfhe-fft/src/unordered.rs:943-1020):
+ * element i of a serialised polynomial is DFT frequency i, whatever the plan's internal order.  These convert
+ * `polys` polynomials of n/2 complex between that natural order and this engine's (device pointers, async; in place
+ * when the two pointers are equal), so a FourierLweBootstrapKey / FourierGgswCiphertext deserialised by the
+ * reference's own serde loads with one call, and a key converted here serialises as the reference expects. */
+int mi_fft64_to_standard_order(const mi_fft64_plan *plan, double *standard_order, const double *fourier, size_t polys,
+                               void *stream);
+int mi_fft64_from_standard_order(const mi_fft64_plan *plan, double *fourier, const double *standard_order,
+                                 size_t polys, void *stream);
 /* FftView::forward_as_torus / backward_as_torus (add != 0: add_backward_as_torus), per polynomial over a
  * batch of contiguous polynomials (device pointers, async): fourier = batch x n/2 x 2 doubles. */
 int mi_fft64_forward_torus_batch(const mi_fft64_plan *plan, double *fourier, const uint64_t *standard, size_t batch,

@@ -313,6 +313,13 @@ class Fft {
                          void* stream = nullptr) const {
     check(mi_fft64_backward_torus_batch(raw_, standard, fourier, batch, add ? 1 : 0, stream));
   }
+  // the reference's serialised natural order (tfhe-fft/src/unordered.rs:943-1020) <-> this engine's order
+  void to_standard_order(double* standard_order, const double* fourier, size_t polys, void* stream = nullptr) const {
+    check(mi_fft64_to_standard_order(raw_, standard_order, fourier, polys, stream));
+  }
+  void from_standard_order(double* fourier, const double* standard_order, size_t polys, void* stream = nullptr) const {
+    check(mi_fft64_from_standard_order(raw_, fourier, standard_order, polys, stream));
+  }
 
  private:
   const mi_fft64_plan* raw_ = nullptr;

@@ -143,6 +143,17 @@ int main() {
     double* four = nullptr;
     EXPECT(hipMalloc(reinterpret_cast<void**>(&four), batch * N * 8) == hipSuccess);
     fft.forward_as_torus(four, d_x.p, batch);
+    {  // serialised (natural) order and back: an exact permutation, out of place then in place
+      double* nat = nullptr;
+      EXPECT(hipMalloc(reinterpret_cast<void**>(&nat), batch * N * 8) == hipSuccess);
+      std::vector<double> h0(batch * N), h1(batch * N);
+      EXPECT(hipMemcpy(h0.data(), four, batch * N * 8, hipMemcpyDeviceToHost) == hipSuccess);
+      fft.to_standard_order(nat, four, batch);
+      fft.from_standard_order(nat, nat, batch);
+      EXPECT(hipMemcpy(h1.data(), nat, batch * N * 8, hipMemcpyDeviceToHost) == hipSuccess);
+      EXPECT(h0 == h1);
+      (void)hipFree(nat);
+    }
     fft.backward_as_torus(d_back.p, four, batch);
     const auto back = d_back.host();
     int64_t worst = 0;

@@ -267,3 +267,78 @@ def test_pbs_k1_l1_ragged_batches(engine, fft, batch, ms_mode):
     with np.errstate(over="ignore"):
         dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
     assert list(dec) == [f(int(m)) for m in msgs]
+
+
+# ---- the reference's serialised (natural) Fourier order and key bytes --------------------------------------
+def test_standard_order_is_the_natural_dft(engine, fft, order):
+    """to_standard_order(forward_as_torus(x)) is the natural-order DFT (what Plan::serialize_fourier_buffer emits,
+    tfhe-fft/src/unordered.rs:943-964; the reference's test_fwd pins it to rustfft's forward DFT), and the two
+    conversions are exact inverse permutations, out of place and in place."""
+    import torch
+    g = H.rng(13)
+    x = H.uniform_u64(g, (9, N))
+    four = torch.zeros((9, M, 2), dtype=torch.float64, device="cuda")
+    fft.forward_as_torus(four, dev(x))
+    std = torch.empty_like(four)
+    fft.to_standard_order(std, four)
+    a = std.cpu().numpy()
+    want = F.forward_as_torus(x)
+    assert np.abs((a[..., 0] + 1j * a[..., 1]) - want).max() / np.abs(want).max() < 1e-13
+    # the device permutation agrees with the host's fourier_order exactly
+    assert np.array_equal(from_engine(four, order), a[..., 0] + 1j * a[..., 1])
+    back = torch.empty_like(four)
+    fft.from_standard_order(back, std)
+    assert torch.equal(back, four)
+    inplace = four.clone()
+    fft.to_standard_order(inplace, inplace)
+    assert torch.equal(inplace, std)
+    fft.from_standard_order(inplace, inplace)
+    assert torch.equal(inplace, four)
+    with pytest.raises(engine.MiError):  # partial overlap is refused
+        engine._lib.check(engine._lib.lib().mi_fft64_to_standard_order(
+            fft.handle, engine.fft64._fdev(four[1:], "o"), engine.fft64._fdev(four[:-1], "i"), 8, None))
+
+
+@pytest.mark.parametrize("versioned", [False, True])
+def test_fourier_key_bytes_round_trip_and_reference_key(engine, fft, versioned):
+    """A key serialised by this engine reloads into an identical device key (so its PBS outputs are bit-identical),
+    and a key built the reference's way -- the natural-order DFT of every standard-key polynomial (numpy
+    restatement), written in the reference's bincode layout -- loads and bootstraps to f(m)."""
+    import torch
+    from tfhe_ntt_amd import fourier_bsk_format as FB
+    n_lwe, base_log, level, msg_mod = 32, 23, 1, 4
+    delta = (1 << 63) // msg_mod
+    g = H.rng(1400 + versioned)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (1, N))
+    bsk = H.bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, 17)
+    fbsk = torch.zeros((n_lwe, level, 2, 2, M, 2), dtype=torch.float64, device="cuda")
+    engine.fft64.convert_standard_lwe_bootstrap_key_to_fourier(dev(bsk), fbsk, fft)
+    key = engine.fft64.FourierLweBootstrapKey(fbsk, base_log, level, fft)
+    buf = key.serialize(versioned)
+    assert len(buf) == 24 + n_lwe * 4 * (8 + 16 * M) + 32 + (24 if versioned else 0)
+    key2 = engine.fft64.FourierLweBootstrapKey.deserialize(buf, versioned, device=0, fft=fft)
+    assert torch.equal(key2.fbsk, fbsk)
+    assert (key2.input_lwe_dimension, key2.base_log, key2.level) == (n_lwe, base_log, level)
+    f = lambda x: (x + 1) % msg_mod
+    lut = dev(H.pbs_lut(N, 1, msg_mod, delta, f))
+    msgs = np.arange(8) % msg_mod
+    lwe = dev(H.lwe_encrypt_batch(g, msgs.astype(np.uint64) * np.uint64(delta), lwe_sk, 30))
+    outs = []
+    for k_ in (key, key2):
+        out = dev(np.zeros((len(msgs), N + 1), np.uint64))
+        engine.fft64.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, k_)
+        outs.append(host(out))
+    assert np.array_equal(outs[0], outs[1])
+    # the reference's way: natural-order Fourier polynomials (numpy), the reference's bytes, loaded here
+    zn = F.forward_as_torus(bsk)                                   # (n_lwe, 1, 2, 2, M) complex, natural order
+    ref_bytes = FB.serialize_fourier_bsk(zn, N, 2, level, base_log, versioned)
+    key3 = engine.fft64.FourierLweBootstrapKey.deserialize(ref_bytes, versioned, device=0, fft=fft)
+    a3, a = key3.fbsk.cpu().numpy(), fbsk.cpu().numpy()
+    assert np.abs(a3 - a).max() / np.abs(a).max() < 1e-13  # the same key up to f64 rounding
+    out = dev(np.zeros((len(msgs), N + 1), np.uint64))
+    engine.fft64.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, key3)
+    pts = H.lwe_decrypt_batch(host(out), H.glwe_sk_as_lwe_sk(glwe_sk))
+    with np.errstate(over="ignore"):
+        dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
+    assert list(dec) == [f(int(m)) for m in msgs]

@@ -179,6 +179,29 @@ int mi_fft64_backward_torus_batch(const mi_fft64_plan* plan, uint64_t* standard,
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 backward launch");
 }
 
+static int reorder(const mi_fft64_plan* plan, double* out, const double* in, size_t polys, bool to_std,
+                   void* stream) {
+  if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
+  if (polys == 0) return MI_OK;
+  if (!out || !in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "polynomial count too large");
+  if (out != in && out < in + polys * 2 * FFT_M && in < out + polys * 2 * FFT_M)
+    return fail(MI_ERR_INVALID_ARG, "buffers overlap partially (in place must be out == in)");
+  DeviceGuard g(plan->device);
+  const hipError_t e = mi::launch_fft64_reorder(out, in, polys, to_std, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 reorder launch");
+}
+
+int mi_fft64_to_standard_order(const mi_fft64_plan* plan, double* standard_order, const double* fourier, size_t polys,
+                               void* stream) {
+  return reorder(plan, standard_order, fourier, polys, true, stream);
+}
+
+int mi_fft64_from_standard_order(const mi_fft64_plan* plan, double* fourier, const double* standard_order,
+                                 size_t polys, void* stream) {
+  return reorder(plan, fourier, standard_order, polys, false, stream);
+}
+
 int mi_bsk_to_fourier64(const mi_fft64_plan* plan, const uint64_t* bsk_std, double* bsk_fourier, size_t n_polys,
                         void* stream) {
   return mi_fft64_forward_torus_batch(plan, bsk_fourier, bsk_std, n_polys, stream);

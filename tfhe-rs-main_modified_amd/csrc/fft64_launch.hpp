@@ -27,6 +27,9 @@ hipError_t launch_fft64_ext_product(int k, bool cmux, uint64_t* out, uint64_t* g
 hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
                             size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftTables& t,
                             hipStream_t s);
+// Fourier order interchange of `polys` polynomials (N / 2 complex each; in place allowed): to_standard = engine
+// order -> the reference's serialised natural order (tfhe-fft/src/unordered.rs:943-964), else the reverse (:974-1020)
+hipError_t launch_fft64_reorder(double* out, const double* in, size_t polys, bool to_standard, hipStream_t s);
 
 // position (register r, lane l) of the Fourier layout -> frequency index (see fft64_pbs.hip)
 inline uint32_t fft64_frequency(int r, int l) {

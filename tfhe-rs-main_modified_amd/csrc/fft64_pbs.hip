@@ -360,6 +360,34 @@ __global__ __launch_bounds__(64) void bwd_torus_kernel(u64* __restrict__ std_, c
   }
 }
 
+// ---- Fourier order interchange (tfhe-fft/src/unordered.rs:943-1020, serialize / deserialize_fourier_buffer) ----
+// The reference serialises a Fourier polynomial in the natural DFT order (element i = frequency i), whatever its
+// plan's internal order.  Engine position p = 64 r + l holds frequency fft64_frequency(r, l) = 64 r + f(l), a
+// permutation of the low six bits only.  One 256-lane workgroup per polynomial stages it in LDS (coalesced 16-B
+// reads), then writes the other order coalesced; in place is safe (every read lands before the barrier).
+__device__ __forceinline__ int low6_frequency(int l) {  // f(l): see fft64_frequency (fft64_launch.hpp)
+  return (l & 3) | (((l >> 4) & 3) << 2) | (((l >> 3) & 1) << 4) | (((l >> 2) & 1) << 5);
+}
+__device__ __forceinline__ int low6_position(int k) {  // f^-1
+  return (k & 3) | (((k >> 5) & 1) << 2) | (((k >> 4) & 1) << 3) | (((k >> 2) & 3) << 4);
+}
+template <bool TO_STD>
+__global__ __launch_bounds__(256) void fourier_reorder_kernel(cplx* out, const cplx* in, uint64_t polys) {
+  __shared__ cplx buf[M];
+  const uint64_t b = blockIdx.x;
+  if (b >= polys) return;
+  const cplx* src = in + b * M;
+#pragma unroll
+  for (int i = 0; i < M / 256; ++i) buf[threadIdx.x + 256 * i] = src[threadIdx.x + 256 * i];
+  __syncthreads();
+  cplx* dst = out + b * M;
+#pragma unroll
+  for (int i = 0; i < M / 256; ++i) {
+    const int j = threadIdx.x + 256 * i, hi = j & ~63, lo = j & 63;
+    dst[j] = buf[hi | (TO_STD ? low6_position(lo) : low6_frequency(lo))];
+  }
+}
+
 // Synchronisation of the (K + 1) waves of one ciphertext.  A workgroup holding one ciphertext uses its barrier;
 // with several ciphertexts per workgroup each wave publishes a step counter in LDS and waits for its partners'
 // (s_sleep between polls), so the ciphertexts of a workgroup do not have to run in lockstep.
@@ -752,6 +780,17 @@ hipError_t launch_fft64_bwd_torus(uint64_t* std_, const double* fourier, size_t 
   if (batch == 0) return hipSuccess;
   hipLaunchKernelGGL(fft::bwd_torus_kernel, dim3((unsigned)batch), dim3(64), 0, s, std_,
                      reinterpret_cast<const fft::cplx*>(fourier), (uint64_t)batch, add ? 1 : 0, tables(t));
+  return hipGetLastError();
+}
+
+hipError_t launch_fft64_reorder(double* out, const double* in, size_t polys, bool to_standard, hipStream_t s) {
+  if (polys == 0) return hipSuccess;
+  auto* o = reinterpret_cast<fft::cplx*>(out);
+  const auto* i = reinterpret_cast<const fft::cplx*>(in);
+  if (to_standard)
+    hipLaunchKernelGGL(fft::fourier_reorder_kernel<true>, dim3((unsigned)polys), dim3(256), 0, s, o, i, (uint64_t)polys);
+  else
+    hipLaunchKernelGGL(fft::fourier_reorder_kernel<false>, dim3((unsigned)polys), dim3(256), 0, s, o, i, (uint64_t)polys);
   return hipGetLastError();
 }
 

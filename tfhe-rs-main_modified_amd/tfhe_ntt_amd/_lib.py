@@ -81,6 +81,8 @@ _SIGS = {
     "mi_fft64_plan_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int)]),
     "mi_fft64_fourier_order": (_int, [_vp, ctypes.POINTER(ctypes.c_uint32)]),
     "mi_fft64_forward_torus_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_fft64_to_standard_order": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_fft64_from_standard_order": (_int, [_vp, _vp, _vp, _sz, _vp]),
     "mi_fft64_backward_torus_batch": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
     "mi_bsk_to_fourier64": (_int, [_vp, _vp, _vp, _sz, _vp]),
     "mi_fft64_ext_product_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _vp]),

@@ -7,9 +7,13 @@ Names follow the reference (paths relative to /root/reference/tfhe/src/core_cryp
 * ``convert_standard_lwe_bootstrap_key_to_fourier``  algorithms/lwe_bootstrap_key_conversion.rs:20-43
 * ``add_external_product_assign`` / ``cmux_assign``  algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330, 510-560
 * ``FourierLweBootstrapKey``, ``programmable_bootstrap_lwe_ciphertext``  fft64_pbs.rs:924-1060
+* ``Fft.to_standard_order`` / ``from_standard_order``  the serialised (natural) Fourier order of
+  tfhe-fft/src/unordered.rs:943-1020; ``FourierLweBootstrapKey.serialize`` / ``deserialize``: the reference's
+  bytes of the key (``fourier_bsk_format``)
 
 Fourier buffers are float64 device tensors with a trailing (N/2, 2) = (complex, re/im) shape in this
-engine's frequency order (``Fft.fourier_order``); keys converted here are for this engine.  A leading batch
+engine's frequency order (``Fft.fourier_order``); ``to_standard_order`` / ``from_standard_order`` convert to and
+from the natural order the reference serialises, so keys move between the two in either direction.  A leading batch
 dimension is allowed everywhere.  Results are f64 computations: decryption-exact and within the FFT error
 bound of the reference, not bit-identical to it.
 """
@@ -72,6 +76,22 @@ class Fft:
 
     def add_backward_as_torus(self, standard, fourier) -> None:
         self.backward_as_torus(standard, fourier, add=True)
+
+    def _reorder(self, out, inp, to_std):
+        m = self.n // 2
+        if tuple(inp.shape[-2:]) != (m, 2) or out.shape != inp.shape:
+            raise ValueError(f"assertion failed: fourier shapes {tuple(out.shape)} / {tuple(inp.shape)} != (..., {m}, 2)")
+        fn = lib().mi_fft64_to_standard_order if to_std else lib().mi_fft64_from_standard_order
+        check(fn(self.handle, _fdev(out, "out"), _fdev(inp, "in"), inp.numel() // (2 * m), _stream(inp)))
+
+    def to_standard_order(self, out, fourier) -> None:
+        """out = fourier (this engine's order) in the natural DFT order the reference serialises
+        (Plan::serialize_fourier_buffer); ``out is fourier`` converts in place."""
+        self._reorder(out, fourier, True)
+
+    def from_standard_order(self, out, standard_order) -> None:
+        """The reverse (Plan::deserialize_fourier_buffer): natural order -> this engine's order."""
+        self._reorder(out, standard_order, False)
 
 
 def convert_standard_lwe_bootstrap_key_to_fourier(input_bsk, output_bsk, fft: Fft | None = None) -> None:
@@ -145,6 +165,37 @@ class FourierLweBootstrapKey:
 
     def output_lwe_size(self) -> int:
         return self.glwe_dimension * self.polynomial_size + 1
+
+    def serialize(self, versioned: bool = False) -> bytes:
+        """The reference's bytes of this key (``bincode::serialize(&FourierLweBootstrapKey)``, or of its
+        ``versionize()`` form): the Fourier polynomials in the natural order, see ``fourier_bsk_format``."""
+        from .fourier_bsk_format import serialize_fourier_bsk
+
+        import torch
+
+        std = torch.empty_like(self.fbsk)
+        self.fft.to_standard_order(std, self.fbsk)
+        host = std.cpu().numpy()
+        return serialize_fourier_bsk(host, self.polynomial_size, self.glwe_dimension + 1, self.level, self.base_log,
+                                     versioned)
+
+    @classmethod
+    def deserialize(cls, buf: bytes, versioned: bool = False, device=None, fft: Fft | None = None):
+        """A key from the reference's bytes: parsed on the host, copied to ``device`` once, reordered into this
+        engine's order in place on the device."""
+        from .fourier_bsk_format import deserialize_fourier_bsk
+
+        import torch
+
+        data, info = deserialize_fourier_bsk(buf, versioned)
+        if device is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        else:
+            dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        fft = fft or Fft(info["polynomial_size"], dev.index)
+        fbsk = torch.from_numpy(data).to(dev)
+        fft.from_standard_order(fbsk, fbsk)
+        return cls(fbsk, info["decomposition_base_log"], info["decomposition_level_count"], fft)
 
 
 def programmable_bootstrap_lwe_ciphertext(lwe_in, lwe_out, accumulator, key: FourierLweBootstrapKey,
