@@ -285,6 +285,21 @@ int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key *key);
 int mi_fft64_pbs_key_info(const mi_fft64_pbs_key *key, size_t *n_lwe, int *k, int *base_log, int *level);
 int mi_fft64_pbs_batch(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
+/* The reference's serialised FourierLweBootstrapKey (fft_impl/fft64/crypto/bootstrap.rs:30-39, the list's custom
+ * Serialize fft_impl/fft64/math/fft/mod.rs:642-690, bincode 1.3 defaults as for the NTT key): format
+ * MI_NTT_BSK_PLAIN = bincode::serialize(&key): u64 (2 + P), u64 polynomial_size, u64 P, then P polynomials each as
+ * u64 (N/2) and N/2 (re, im) f64 pairs in the natural DFT order (tfhe-fft/src/unordered.rs:943-964), then
+ * input_lwe_dimension, glwe_size, decomposition_base_log, decomposition_level_count as u64;
+ * MI_NTT_BSK_VERSIONED = bincode of key.versionize(): u32 1 (FourierLweBootstrapKeyVersions::V1), u32 0
+ * (FourierPolynomialListVersioned::V0), the same list, a u32 0 before each scalar field
+ * (backward_compatibility/fft_impl/mod.rs:14-70).  _load validates the bytes (length, tags, per-polynomial length,
+ * P = n_lwe level glwe_size^2, the plan's polynomial size), uploads them with one strided copy and reorders them
+ * into this engine's order on `stream` (synchronised before returning); the key owns that device copy.  _write
+ * produces exactly mi_fft64_bsk_serialized_size bytes from any key (a loaded one or one over a caller tensor). */
+int mi_fft64_bsk_serialized_size(size_t n_lwe, int k, int level, int format, size_t *out_len);
+int mi_fft64_pbs_key_load(const mi_fft64_plan *plan, const uint8_t *bytes, size_t len, int format, void *stream,
+                          mi_fft64_pbs_key **out_key);
+int mi_fft64_pbs_key_write(const mi_fft64_pbs_key *key, int format, uint8_t *out, size_t out_len, void *stream);
 
 /* ---- prime32::Plan (tfhe-ntt/src/prime32.rs:632-1025) ----------------------------------------
  * The same negacyclic transform and pointwise ops on u32 buffers for a prime p < 2^32.  try_new

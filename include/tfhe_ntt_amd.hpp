@@ -359,7 +359,29 @@ class FourierBootstrapKey {
   const mi_fft64_pbs_key* raw() const noexcept { return raw_; }
   size_t input_lwe_dimension() const noexcept { return n_lwe_; }
 
+  // the reference's FourierLweBootstrapKey bytes (plain or versioned bincode) -> a key owning its device copy
+  static FourierBootstrapKey load(const Fft& fft, const uint8_t* bytes, size_t len, bool versioned = false,
+                                  void* stream = nullptr) {
+    mi_fft64_pbs_key* k = nullptr;
+    check(mi_fft64_pbs_key_load(fft.raw(), bytes, len, versioned ? MI_NTT_BSK_VERSIONED : MI_NTT_BSK_PLAIN, stream, &k));
+    size_t n = 0;
+    check(mi_fft64_pbs_key_info(k, &n, nullptr, nullptr, nullptr));
+    return FourierBootstrapKey(k, n);
+  }
+  // this key as the reference's bytes
+  std::vector<uint8_t> serialize(bool versioned = false, void* stream = nullptr) const {
+    const int fmt = versioned ? MI_NTT_BSK_VERSIONED : MI_NTT_BSK_PLAIN;
+    int k = 0, level = 0;
+    check(mi_fft64_pbs_key_info(raw_, nullptr, &k, nullptr, &level));
+    size_t len = 0;
+    check(mi_fft64_bsk_serialized_size(n_lwe_, k, level, fmt, &len));
+    std::vector<uint8_t> out(len);
+    check(mi_fft64_pbs_key_write(raw_, fmt, out.data(), out.size(), stream));
+    return out;
+  }
+
  private:
+  FourierBootstrapKey(mi_fft64_pbs_key* raw, size_t n_lwe) : raw_(raw), n_lwe_(n_lwe) {}
   mi_fft64_pbs_key* raw_ = nullptr;
   size_t n_lwe_;
 };

@@ -201,6 +201,23 @@ int main() {
         worst = std::max(worst, d < 0 ? -d : d);
       }
     EXPECT(worst < (int64_t(1) << 48));
+    {  // the reference's FourierLweBootstrapKey bytes: write, load (a key owning its copy), write again: same bytes
+      tfhe_ntt_amd::fft64::FourierBootstrapKey key(fft, fg, 1, bl, 1);
+      for (const bool ver : {false, true}) {
+        const auto bytes = key.serialize(ver);
+        EXPECT(bytes.size() == (ver ? 8u : 0u) + 24 + 4 * (8 + 16 * (N / 2)) + 32 + (ver ? 16u : 0u));
+        const auto loaded = tfhe_ntt_amd::fft64::FourierBootstrapKey::load(fft, bytes.data(), bytes.size(), ver);
+        EXPECT(loaded.input_lwe_dimension() == 1);
+        EXPECT(loaded.serialize(ver) == bytes);
+        bool threw = false;
+        try {
+          (void)tfhe_ntt_amd::fft64::FourierBootstrapKey::load(fft, bytes.data(), bytes.size() - 1, ver);
+        } catch (const tfhe_ntt_amd::Error& e) {
+          threw = e.status() == MI_ERR_INVALID_ARG;
+        }
+        EXPECT(threw);
+      }
+    }
     (void)hipFree(fg);
   }
 

@@ -315,21 +315,30 @@ def test_fourier_key_bytes_round_trip_and_reference_key(engine, fft, versioned):
     fbsk = torch.zeros((n_lwe, level, 2, 2, M, 2), dtype=torch.float64, device="cuda")
     engine.fft64.convert_standard_lwe_bootstrap_key_to_fourier(dev(bsk), fbsk, fft)
     key = engine.fft64.FourierLweBootstrapKey(fbsk, base_log, level, fft)
-    buf = key.serialize(versioned)
+    buf = key.serialize(versioned)                                  # the library's writer
     assert len(buf) == 24 + n_lwe * 4 * (8 + 16 * M) + 32 + (24 if versioned else 0)
+    nat = torch.empty_like(fbsk)
+    fft.to_standard_order(nat, fbsk)
+    assert buf == FB.serialize_fourier_bsk(nat.cpu().numpy(), N, 2, level, base_log, versioned)  # == Python mirror
     key2 = engine.fft64.FourierLweBootstrapKey.deserialize(buf, versioned, device=0, fft=fft)
     assert torch.equal(key2.fbsk, fbsk)
     assert (key2.input_lwe_dimension, key2.base_log, key2.level) == (n_lwe, base_log, level)
+    key4 = engine.fft64.FourierLweBootstrapKey.load(buf, versioned, fft=fft)  # the library's loader (owns its copy)
+    assert (key4.input_lwe_dimension, key4.glwe_dimension, key4.base_log, key4.level) == (n_lwe, 1, base_log, level)
+    assert key4.serialize(versioned) == buf
+    for bad in (buf[:-1], buf + b"\0", buf[: len(buf) - 8] + bytes(8)):  # truncated, trailing, level 0
+        with pytest.raises(engine.MiError):
+            engine.fft64.FourierLweBootstrapKey.load(bad, versioned, fft=fft)
     f = lambda x: (x + 1) % msg_mod
     lut = dev(H.pbs_lut(N, 1, msg_mod, delta, f))
     msgs = np.arange(8) % msg_mod
     lwe = dev(H.lwe_encrypt_batch(g, msgs.astype(np.uint64) * np.uint64(delta), lwe_sk, 30))
     outs = []
-    for k_ in (key, key2):
+    for k_ in (key, key2, key4):
         out = dev(np.zeros((len(msgs), N + 1), np.uint64))
         engine.fft64.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, k_)
         outs.append(host(out))
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     # the reference's way: natural-order Fourier polynomials (numpy), the reference's bytes, loaded here
     zn = F.forward_as_torus(bsk)                                   # (n_lwe, 1, 2, 2, M) complex, natural order
     ref_bytes = FB.serialize_fourier_bsk(zn, N, 2, level, base_log, versioned)

@@ -6,6 +6,7 @@
 //   external product / CMUX   algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330, 510-560
 //   PBS                       algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:924-1060
 #include <cmath>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <new>
@@ -27,7 +28,8 @@ struct mi_fft64_plan {
 
 struct mi_fft64_pbs_key {
   const mi_fft64_plan* plan = nullptr;
-  const double* fbsk = nullptr;  // caller-owned Fourier key
+  const double* fbsk = nullptr;  // caller-owned Fourier key, or `owned`
+  double* owned = nullptr;       // device copy made by mi_fft64_pbs_key_load
   size_t n_lwe = 0;
   int k = 1, base_log = 0, level = 0;
 };
@@ -254,8 +256,175 @@ int mi_fft64_pbs_key_create(const mi_fft64_plan* plan, const double* fbsk, size_
 }
 
 int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key* key) {
+  if (key && key->owned) {
+    DeviceGuard g(key->plan->device);
+    (void)hipFree(key->owned);
+  }
   delete key;
   return MI_OK;
+}
+
+// ---- the reference's FourierLweBootstrapKey bytes (bincode 1.3 defaults: fixint, little-endian, u64 sequence
+// lengths, u32 variant indices).  Field order fft_impl/fft64/crypto/bootstrap.rs:30-39; the list's custom
+// Serialize fft_impl/fft64/math/fft/mod.rs:642-690: u64 (2 + chunks), u64 polynomial_size, u64 chunks, then per
+// polynomial u64 (N/2) and N/2 (re, im) f64 pairs in the natural order (tfhe-fft unordered.rs:943-964); then
+// input_lwe_dimension, glwe_size, decomposition_base_log, decomposition_level_count as u64.  Versioned
+// (key.versionize()): u32 1 (FourierLweBootstrapKeyVersions::V1), u32 0 (FourierPolynomialListVersioned::V0) in
+// front, a u32 0 (...Versions::V0) before each scalar field (backward_compatibility/fft_impl/mod.rs:14-70).
+namespace {
+struct FourierLayout {
+  uint64_t n_lwe, glwe, base_log, level, chunks;
+  size_t head, chunk_bytes, total;  // bytes before the first polynomial's length prefix, per polynomial, all
+};
+
+bool fourier_layout(uint64_t n_lwe, uint64_t glwe, uint64_t level, uint64_t base_log, bool ver, FourierLayout* L) {
+  uint64_t c;
+  if (__builtin_mul_overflow(glwe, glwe, &c) || __builtin_mul_overflow(c, level, &c) ||
+      __builtin_mul_overflow(c, n_lwe, &c))
+    return false;
+  L->n_lwe = n_lwe, L->glwe = glwe, L->base_log = base_log, L->level = level, L->chunks = c;
+  L->head = (ver ? 8 : 0) + 24;
+  L->chunk_bytes = 8 + 16 * FFT_M;
+  size_t body;
+  return !__builtin_mul_overflow((size_t)c, L->chunk_bytes, &body) &&
+         !__builtin_add_overflow(body, L->head + 32 + (ver ? 16 : 0), &L->total);
+}
+
+uint32_t rd32(const uint8_t* p) {
+  uint32_t v;
+  std::memcpy(&v, p, sizeof v);  // little-endian host
+  return v;
+}
+uint64_t rd64(const uint8_t* p) {
+  uint64_t v;
+  std::memcpy(&v, p, sizeof v);
+  return v;
+}
+uint8_t* wr32(uint8_t* p, uint32_t v) {
+  std::memcpy(p, &v, sizeof v);
+  return p + sizeof v;
+}
+uint8_t* wr64(uint8_t* p, uint64_t v) {
+  std::memcpy(p, &v, sizeof v);
+  return p + sizeof v;
+}
+}  // namespace
+
+int mi_fft64_bsk_serialized_size(size_t n_lwe, int k, int level, int format, size_t* out_len) {
+  if (!out_len) return fail(MI_ERR_INVALID_ARG, "out_len is NULL");
+  if (format != MI_NTT_BSK_PLAIN && format != MI_NTT_BSK_VERSIONED) return fail(MI_ERR_INVALID_ARG, "unknown format");
+  FourierLayout L;
+  if (k < 1 || level < 1 || !fourier_layout(n_lwe, (uint64_t)k + 1, (uint64_t)level, 0, format == MI_NTT_BSK_VERSIONED, &L))
+    return fail(MI_ERR_INVALID_ARG, "Fourier BSK: bad sizes");
+  *out_len = L.total;
+  return MI_OK;
+}
+
+int mi_fft64_pbs_key_load(const mi_fft64_plan* plan, const uint8_t* bytes, size_t len, int format, void* stream,
+                          mi_fft64_pbs_key** out_key) {
+  if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
+  *out_key = nullptr;
+  if (!plan || !bytes) return fail(MI_ERR_INVALID_ARG, "NULL argument");
+  if (format != MI_NTT_BSK_PLAIN && format != MI_NTT_BSK_VERSIONED) return fail(MI_ERR_INVALID_ARG, "unknown format");
+  const bool ver = format == MI_NTT_BSK_VERSIONED;
+  size_t off = 0;
+  if (ver) {
+    if (len < 8) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: truncated");
+    const uint32_t kt = rd32(bytes), lt = rd32(bytes + 4);
+    if (kt == 0) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: deprecated V0 version (TFHE-rs < v0.10)");
+    if (kt != 1 || lt != 0) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: unknown version tags");
+    off = 8;
+  }
+  if (len - off < 24) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: truncated");
+  const uint64_t seq = rd64(bytes + off), n = rd64(bytes + off + 8), chunks = rd64(bytes + off + 16);
+  if (n != plan->n) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: polynomial size differs from the plan's");
+  if (chunks > ((uint64_t)1 << 40) || seq != chunks + 2)
+    return fail(MI_ERR_INVALID_ARG, "Fourier BSK: sequence length is not 2 + the polynomial count");
+  // the scalar fields sit after the polynomials
+  const size_t chunk_bytes = 8 + 16 * FFT_M, tail = 32 + (ver ? 16 : 0);
+  if (len < off + 24 + tail || (len - off - 24 - tail) % chunk_bytes || (len - off - 24 - tail) / chunk_bytes != chunks)
+    return fail(MI_ERR_INVALID_ARG, "Fourier BSK: length does not match the polynomial count");
+  const uint8_t* t = bytes + off + 24 + chunks * chunk_bytes;
+  uint64_t f[4];
+  for (int i = 0; i < 4; ++i) {
+    if (ver) {
+      if (rd32(t) != 0) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: unknown parameter version tag");
+      t += 4;
+    }
+    f[i] = rd64(t);
+    t += 8;
+  }
+  const uint64_t n_lwe = f[0], glwe = f[1], base_log = f[2], level = f[3];
+  FourierLayout L;
+  if (glwe < 2 || glwe > 3 || level < 1 || level > 63 || base_log < 1 || base_log > 63 ||
+      !fourier_layout(n_lwe, glwe, level, base_log, ver, &L) || L.chunks != chunks)
+    return fail(MI_ERR_INVALID_ARG, "Fourier BSK: the polynomial count does not match n_lwe x level x glwe_size^2");
+  int st = check_shape(plan, (int)glwe - 1, (int)base_log, (int)level);
+  if (st != MI_OK) return st;
+  if (n_lwe == 0 || n_lwe > 0xFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: n_lwe out of range");
+  for (uint64_t c = 0; c < chunks; ++c)
+    if (rd64(bytes + off + 24 + c * chunk_bytes) != FFT_M)
+      return fail(MI_ERR_INVALID_ARG, "Fourier BSK: a polynomial does not hold N/2 values");
+  auto* key = new (std::nothrow) mi_fft64_pbs_key;
+  if (!key) return fail(MI_ERR_OOM, "host allocation failed");
+  key->plan = plan;
+  key->n_lwe = n_lwe;
+  key->k = (int)glwe - 1;
+  key->base_log = (int)base_log;
+  key->level = (int)level;
+  DeviceGuard g(plan->device);
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipMalloc(&key->owned, chunks * 16 * FFT_M) != hipSuccess) {
+    delete key;
+    return fail(MI_ERR_OOM, "Fourier key allocation failed");
+  }
+  // one strided upload skips the per-polynomial length prefixes, then the natural order becomes the engine's
+  hipError_t e = hipMemcpy2DAsync(key->owned, 16 * FFT_M, bytes + off + 24 + 8, chunk_bytes, 16 * FFT_M, chunks,
+                                  hipMemcpyHostToDevice, s);
+  st = e == hipSuccess ? MI_OK : hip_fail(e, "Fourier key upload");
+  if (st == MI_OK) {
+    e = mi::launch_fft64_reorder(key->owned, key->owned, chunks, false, s);
+    st = e == hipSuccess ? MI_OK : hip_fail(e, "fft64 reorder launch");
+  }
+  if (st == MI_OK && (e = hipStreamSynchronize(s)) != hipSuccess) st = hip_fail(e, "Fourier key upload");
+  if (st != MI_OK) {
+    (void)hipFree(key->owned);
+    delete key;
+    return st;
+  }
+  key->fbsk = key->owned;
+  *out_key = key;
+  return MI_OK;
+}
+
+int mi_fft64_pbs_key_write(const mi_fft64_pbs_key* key, int format, uint8_t* out, size_t out_len, void* stream) {
+  if (!key || !out) return fail(MI_ERR_INVALID_ARG, "NULL argument");
+  size_t need = 0;
+  int st = mi_fft64_bsk_serialized_size(key->n_lwe, key->k, key->level, format, &need);
+  if (st != MI_OK) return st;
+  if (out_len != need) return fail(MI_ERR_INVALID_ARG, "output length is not the serialized size");
+  const bool ver = format == MI_NTT_BSK_VERSIONED;
+  FourierLayout L;
+  (void)fourier_layout(key->n_lwe, (uint64_t)key->k + 1, (uint64_t)key->level, (uint64_t)key->base_log, ver, &L);
+  uint8_t* p = out;
+  if (ver) p = wr32(wr32(p, 1), 0);
+  p = wr64(wr64(wr64(p, L.chunks + 2), key->plan->n), L.chunks);
+  for (uint64_t c = 0; c < L.chunks; ++c) wr64(p + c * L.chunk_bytes, FFT_M);
+  uint8_t* t = p + L.chunks * L.chunk_bytes;
+  for (const uint64_t v : {L.n_lwe, L.glwe, L.base_log, L.level}) {
+    if (ver) t = wr32(t, 0);
+    t = wr64(t, v);
+  }
+  DeviceGuard g(key->plan->device);
+  const hipStream_t s = (hipStream_t)stream;
+  double* tmp = nullptr;
+  if (hipMalloc(&tmp, L.chunks * 16 * FFT_M) != hipSuccess) return fail(MI_ERR_OOM, "scratch allocation failed");
+  hipError_t e = mi::launch_fft64_reorder(tmp, key->fbsk, L.chunks, true, s);
+  if (e == hipSuccess)
+    e = hipMemcpy2DAsync(p + 8, L.chunk_bytes, tmp, 16 * FFT_M, 16 * FFT_M, L.chunks, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "Fourier key download");
 }
 
 int mi_fft64_pbs_key_info(const mi_fft64_pbs_key* key, size_t* n_lwe, int* k, int* base_log, int* level) {

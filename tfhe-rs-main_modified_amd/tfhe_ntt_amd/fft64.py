@@ -168,21 +168,42 @@ class FourierLweBootstrapKey:
 
     def serialize(self, versioned: bool = False) -> bytes:
         """The reference's bytes of this key (``bincode::serialize(&FourierLweBootstrapKey)``, or of its
-        ``versionize()`` form): the Fourier polynomials in the natural order, see ``fourier_bsk_format``."""
-        from .fourier_bsk_format import serialize_fourier_bsk
+        ``versionize()`` form), written by the library (``mi_fft64_pbs_key_write``: natural Fourier order, see
+        ``fourier_bsk_format``)."""
+        size = ctypes.c_size_t()
+        check(lib().mi_fft64_bsk_serialized_size(self.input_lwe_dimension, self.glwe_dimension, self.level,
+                                                 int(bool(versioned)), ctypes.byref(size)))
+        out = ctypes.create_string_buffer(size.value)
+        check(lib().mi_fft64_pbs_key_write(self._h, int(bool(versioned)), out, size.value, self._stream()))
+        return out.raw
 
+    def _stream(self):
         import torch
 
-        std = torch.empty_like(self.fbsk)
-        self.fft.to_standard_order(std, self.fbsk)
-        host = std.cpu().numpy()
-        return serialize_fourier_bsk(host, self.polynomial_size, self.glwe_dimension + 1, self.level, self.base_log,
-                                     versioned)
+        return ctypes.c_void_p(torch.cuda.current_stream(torch.device("cuda", self.fft.device)).cuda_stream)
+
+    @classmethod
+    def load(cls, buf: bytes, versioned: bool = False, fft: Fft | None = None, device: int = 0):
+        """A key from the reference's bytes through the library (``mi_fft64_pbs_key_load``: validated, one strided
+        upload, reordered into this engine's order on the device; the key owns that copy, ``fbsk`` is None)."""
+        fft = fft or Fft(2048, device)
+        self = cls.__new__(cls)
+        self.fft, self.fbsk = fft, None
+        h = ctypes.c_void_p()
+        check(lib().mi_fft64_pbs_key_load(fft.handle, buf, len(buf), int(bool(versioned)), self._stream(),
+                                          ctypes.byref(h)))
+        self._h = h
+        n_lwe, k, bl, lv = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().mi_fft64_pbs_key_info(h, ctypes.byref(n_lwe), ctypes.byref(k), ctypes.byref(bl), ctypes.byref(lv)))
+        self.input_lwe_dimension, self.glwe_dimension = n_lwe.value, k.value
+        self.base_log, self.level, self.polynomial_size = bl.value, lv.value, fft.n
+        return self
 
     @classmethod
     def deserialize(cls, buf: bytes, versioned: bool = False, device=None, fft: Fft | None = None):
-        """A key from the reference's bytes: parsed on the host, copied to ``device`` once, reordered into this
-        engine's order in place on the device."""
+        """A key from the reference's bytes parsed on the host by ``fourier_bsk_format`` (the Python mirror of the
+        layout), copied to ``device`` as a tensor the key references, reordered into this engine's order in
+        place on the device."""
         from .fourier_bsk_format import deserialize_fourier_bsk
 
         import torch
