@@ -131,6 +131,16 @@ int mi_ext_product_ntt64_batch(const mi_ntt64_plan *plan, uint64_t *out_glwe, co
  * / cmux_ntt64_bnf_assign (ntt64_bnf_pbs.rs:683-705); like the reference, ct1 is left holding ct1 - ct0. */
 int mi_cmux_ntt64_batch(const mi_ntt64_plan *plan, uint64_t *ct0, uint64_t *ct1, const uint64_t *ggsw_ntt, int k,
                         int base_log, int level, size_t batch, int variant, void *stream);
+/* The same with one GGSW per item ("one shared GGSW or a per-item GGSW index array"): item b uses
+ * GGSW ggsw_index[b] of the n_ggsw GGSWs stored back to back in ggsw_list (device u32 array of `batch` entries);
+ * an item whose index is >= n_ggsw is left untouched (both its GLWEs), so a bad index never reads outside the
+ * list.  Useful for batched CMUX trees and per-ciphertext selectors. */
+int mi_ext_product_ntt64_batch_indexed(const mi_ntt64_plan *plan, uint64_t *out_glwe, const uint64_t *in_glwe,
+                                       const uint64_t *ggsw_list, const uint32_t *ggsw_index, size_t n_ggsw, int k,
+                                       int base_log, int level, size_t batch, int variant, void *stream);
+int mi_cmux_ntt64_batch_indexed(const mi_ntt64_plan *plan, uint64_t *ct0, uint64_t *ct1, const uint64_t *ggsw_list,
+                                const uint32_t *ggsw_index, size_t n_ggsw, int k, int base_log, int level,
+                                size_t batch, int variant, void *stream);
 
 /* A bootstrap key made ready for mi_pbs_ntt64_batch on the plan's device.  MI_NTT64_BNF keys
  * (converted Raw, as ntt64_bnf_pbs.rs tests do) are copied once with N^{-1} folded in — the

@@ -435,3 +435,45 @@ def test_pbs_functional_k2_real_keys(engine, oracle):
     for i, m in enumerate(msgs):
         assert np.array_equal(got[i], c.pbs(lwe[i], lut.reshape(-1), nbsk.reshape(-1), k, base_log, level))
         assert H.decode(H.lwe_decrypt(got[i], out_sk, 0), delta, msg_mod, 0) % msg_mod == f(m)
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+@pytest.mark.parametrize("n,k,base_log,level", [(2048, 1, 23, 1), (2048, 1, 12, 2), (1024, 2, 23, 1)])
+def test_indexed_ggsw_ext_product_and_cmux(engine, oracle, bnf, n, k, base_log, level):
+    """One GGSW per item ("one shared GGSW or a per-item GGSW index array"): item b uses
+    ggsw_list[index[b]], on the twisted kernel (BNF/Solinas level 1, N 2048, k 1) and the generic one; an index
+    past the list leaves the item (both GLWEs) untouched.  Oracle per item."""
+    import torch
+    q = 0 if bnf else P
+    g = H.rng(5000 + n + 10 * k + level + bnf)
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    n_ggsw, batch = 3, 7
+    ggsw = rand_q(g, (n_ggsw, level, k + 1, k + 1, n), P)
+    idx = np.array([2, 0, 1, 1, 7, 0, 2], np.int32)       # item 4: out of range
+    glwe = rand_q(g, (batch, k + 1, n), q)
+    out0 = rand_q(g, (batch, k + 1, n), q)
+    want = out0.copy()
+    want0, want1 = out0.copy(), glwe.copy()
+    for b in range(batch):
+        if idx[b] >= n_ggsw:
+            continue
+        gg = ggsw[idx[b]].reshape(-1)
+        want[b] = c.ext_product(out0[b].reshape(-1), gg, glwe[b].reshape(-1), k, base_log, level,
+                                bnf=bnf).reshape(k + 1, n)
+        want0[b] = c.cmux(out0[b].reshape(-1), glwe[b].reshape(-1), gg, k, base_log, level, bnf=bnf).reshape(k + 1, n)
+        want1[b] = H.sub_q(glwe[b], out0[b], q)
+    tidx = torch.from_numpy(idx).cuda()
+    out, tg = dev(out0), dev(glwe)
+    fn = M.add_external_product_ntt64_bnf_assign if bnf else M.add_external_product_ntt64_assign
+    fn(pl, out, dev(ggsw), tg, base_log, level, ggsw_index=tidx)
+    assert np.array_equal(host(out), want)
+    assert np.array_equal(host(tg), glwe)
+    t0, t1 = dev(out0), dev(glwe)
+    fn = M.cmux_ntt64_bnf_assign if bnf else M.cmux_ntt64_assign
+    fn(pl, t0, t1, dev(ggsw), base_log, level, ggsw_index=tidx)
+    assert np.array_equal(host(t0), want0)
+    assert np.array_equal(host(t1), want1)
+    with pytest.raises(ValueError):
+        fn(pl, t0, t1, dev(ggsw), base_log, level, ggsw_index=tidx[:3])

@@ -398,42 +398,52 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
   return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
 }
 
-int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
-                               const uint64_t* ggsw_ntt, int k, int base_log, int level, size_t batch, int variant,
-                               void* stream) {
+static int ext_common(const mi_ntt64_plan* plan, bool cmux, uint64_t* out, uint64_t* in, const uint64_t* ggsw,
+                      const uint32_t* gidx, size_t n_ggsw, int k, int base_log, int level, size_t batch, int variant,
+                      void* stream) {
   int st = check_pbs_shape(plan, k, base_log, level, variant);
   if (st != MI_OK) return st;
   if (batch == 0) return MI_OK;
-  if (!out_glwe || !in_glwe || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (!out || !in || !ggsw) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  if (n_ggsw == 0 || n_ggsw > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "GGSW count out of range");
   DeviceGuard g(plan->device);
-  if (twisted_ext_applies(plan, variant, k, base_log, level)) {
-    hipError_t e = mi::launch_ext_tw(false, variant == MI_NTT64_SOLINAS, out_glwe, const_cast<uint64_t*>(in_glwe),
-                                     ggsw_ntt, batch, base_log, plan->d_twist_f, (hipStream_t)stream);
-    return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
-  }
-  hipError_t e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, false, level, out_glwe, const_cast<uint64_t*>(in_glwe),
-                                        ggsw_ntt, batch, base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv,
-                                        (hipStream_t)stream);
-  return e == hipSuccess ? MI_OK : hip_fail(e, "external product launch");
+  hipError_t e;
+  if (twisted_ext_applies(plan, variant, k, base_log, level))
+    e = mi::launch_ext_tw(cmux, variant == MI_NTT64_SOLINAS, out, in, ggsw, batch, base_log, plan->d_twist_f,
+                          (hipStream_t)stream, gidx, (uint32_t)n_ggsw);
+  else
+    e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch, base_log,
+                               plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
+                               (uint32_t)n_ggsw);
+  return e == hipSuccess ? MI_OK : hip_fail(e, cmux ? "cmux launch" : "external product launch");
+}
+
+int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
+                               const uint64_t* ggsw_ntt, int k, int base_log, int level, size_t batch, int variant,
+                               void* stream) {
+  return ext_common(plan, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_ntt, nullptr, 1, k, base_log, level,
+                    batch, variant, stream);
 }
 
 int mi_cmux_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1, const uint64_t* ggsw_ntt, int k,
                         int base_log, int level, size_t batch, int variant, void* stream) {
-  int st = check_pbs_shape(plan, k, base_log, level, variant);
-  if (st != MI_OK) return st;
-  if (batch == 0) return MI_OK;
-  if (!ct0 || !ct1 || !ggsw_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
-  if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
-  DeviceGuard g(plan->device);
-  if (twisted_ext_applies(plan, variant, k, base_log, level)) {
-    hipError_t e = mi::launch_ext_tw(true, variant == MI_NTT64_SOLINAS, ct0, ct1, ggsw_ntt, batch, base_log,
-                                     plan->d_twist_f, (hipStream_t)stream);
-    return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
-  }
-  hipError_t e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, true, level, ct0, ct1, ggsw_ntt, batch, base_log,
-                                        plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream);
-  return e == hipSuccess ? MI_OK : hip_fail(e, "cmux launch");
+  return ext_common(plan, true, ct0, ct1, ggsw_ntt, nullptr, 1, k, base_log, level, batch, variant, stream);
+}
+
+int mi_ext_product_ntt64_batch_indexed(const mi_ntt64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
+                                       const uint64_t* ggsw_list, const uint32_t* ggsw_index, size_t n_ggsw, int k,
+                                       int base_log, int level, size_t batch, int variant, void* stream) {
+  if (!ggsw_index && batch) return fail(MI_ERR_INVALID_ARG, "ggsw_index is NULL");
+  return ext_common(plan, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_list, ggsw_index, n_ggsw, k, base_log,
+                    level, batch, variant, stream);
+}
+
+int mi_cmux_ntt64_batch_indexed(const mi_ntt64_plan* plan, uint64_t* ct0, uint64_t* ct1, const uint64_t* ggsw_list,
+                                const uint32_t* ggsw_index, size_t n_ggsw, int k, int base_log, int level,
+                                size_t batch, int variant, void* stream) {
+  if (!ggsw_index && batch) return fail(MI_ERR_INVALID_ARG, "ggsw_index is NULL");
+  return ext_common(plan, true, ct0, ct1, ggsw_list, ggsw_index, n_ggsw, k, base_log, level, batch, variant, stream);
 }
 
 }  // extern "C"

@@ -60,9 +60,12 @@ hipError_t launch_bsk_to_ntt(int logn, uint64_t* dst, const uint64_t* src, size_
                              int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s);
 hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64_t c, hipStream_t s);
 // cmux: glwe -= out first (written back), then out += GGSW (.) glwe
+// gidx (device, may be NULL): item b uses GGSW gidx[b] of the n_ggsw in `ggsw` (an index >= n_ggsw leaves the item
+// untouched); NULL: every item uses the one GGSW (n_ggsw must then be >= 1)
 hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
                               const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
-                              const uint64_t* itw, uint64_t n_inv, hipStream_t s);
+                              const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx = nullptr,
+                              uint32_t n_ggsw = 1);
 hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s);
@@ -70,7 +73,8 @@ hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const
 // BNF level-1 external product (cmux=false: out += GGSW . glwe) / CMUX (cmux=true: ct0 = out,
 // ct1 = glwe) on the twisted transform; the GGSW is the Raw NTT key (N^-1 via the third table)
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
-                         int base_log, const uint64_t* tab, hipStream_t s);
+                         int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx = nullptr,
+                         uint32_t n_ggsw = 1);
 // Solinas PBS on the twisted engine: switched = pre-switched mask + body values in [0, 2N)
 hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s);
 hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,

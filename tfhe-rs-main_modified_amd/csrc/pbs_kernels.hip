@@ -203,10 +203,12 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
 template <int LOGN, int K, bool BNF, bool CMUX>
 __global__ __launch_bounds__(Shape<LOGN>::T) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
-                                                                     const u64* __restrict__ ggsw, uint32_t batch,
+                                                                     const u64* __restrict__ ggsw_list, uint32_t batch,
                                                                      int base_log, int level,
                                                                      const u64* __restrict__ tw,
-                                                                     const u64* __restrict__ itw, u64 n_inv) {
+                                                                     const u64* __restrict__ itw, u64 n_inv,
+                                                                     const uint32_t* __restrict__ gidx,
+                                                                     uint32_t n_ggsw) {
   using S = Shape<LOGN>;
   using G = typename S::G;
   constexpr int E = S::E, N = S::N;
@@ -214,6 +216,10 @@ __global__ __launch_bounds__(Shape<LOGN>::T) void ext_product_kernel(u64* __rest
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;  // uniform per workgroup
+  // per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one shared GGSW
+  const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
+  if (gi >= n_ggsw) return;
+  const u64* ggsw = ggsw_list + (size_t)gi * level * (K + 1) * (K + 1) * N;
   u64* in = glwe + (size_t)b * (K + 1) * N;
   u64* o = out + (size_t)b * (K + 1) * N;
   u64 ct[K + 1][E], y[K + 1][E], acc[K + 1][E];
@@ -481,30 +487,32 @@ hipError_t launch_scale(uint64_t* dst, const uint64_t* src, size_t count, uint64
 
 template <int LOGN, int K, bool BNF, bool CMUX>
 static hipError_t ext_launch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
-                             int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
+                             int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s,
+                             const uint32_t* gidx, uint32_t n_ggsw) {
   hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX>), dim3((unsigned)batch), dim3(pbs::Shape<LOGN>::T), 0,
-                     s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw, n_inv);
+                     s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw, n_inv, gidx, n_ggsw);
   return hipGetLastError();
 }
 
 template <int LOGN, int K>
 static hipError_t ext_shape(bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw,
                             size_t batch, int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv,
-                            hipStream_t s) {
+                            hipStream_t s, const uint32_t* gi, uint32_t ng) {
   if (bnf)
-    return cmux ? ext_launch<LOGN, K, true, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
-                : ext_launch<LOGN, K, true, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
-  return cmux ? ext_launch<LOGN, K, false, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s)
-              : ext_launch<LOGN, K, false, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+    return cmux ? ext_launch<LOGN, K, true, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gi, ng)
+                : ext_launch<LOGN, K, true, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gi, ng);
+  return cmux ? ext_launch<LOGN, K, false, true>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gi, ng)
+              : ext_launch<LOGN, K, false, false>(level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gi, ng);
 }
 
 hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
                               const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
-                              const uint64_t* itw, uint64_t n_inv, hipStream_t s) {
+                              const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx,
+                              uint32_t n_ggsw) {
   if (batch == 0) return hipSuccess;
 #define MI_EXT_SHAPE(L, KK)                                                                      \
   if (logn == L && k == KK)                                                                      \
-    return ext_shape<L, KK>(bnf, cmux, level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s);
+    return ext_shape<L, KK>(bnf, cmux, level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gidx, n_ggsw);
   MI_EXT_SHAPE(10, 1) MI_EXT_SHAPE(10, 2) MI_EXT_SHAPE(11, 1) MI_EXT_SHAPE(11, 2) MI_EXT_SHAPE(12, 1)
   MI_EXT_SHAPE(12, 2)
 #undef MI_EXT_SHAPE

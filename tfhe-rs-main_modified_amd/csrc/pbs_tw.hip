@@ -195,14 +195,19 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
 // SOL: GLWEs modulo p with a Normalize GGSW (ntt64_pbs.rs:553-702), else BNF (native GLWEs, Raw GGSW)
 template <bool CMUX, bool SOL = false>
 __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
-                                                     const u64* __restrict__ ggsw, uint32_t batch, int base_log,
-                                                     const u64* __restrict__ tab) {
+                                                     const u64* __restrict__ ggsw_list, uint32_t batch, int base_log,
+                                                     const u64* __restrict__ tab, const uint32_t* __restrict__ gidx,
+                                                     uint32_t n_ggsw) {
   __shared__ u64 buf[2 * N];
   __shared__ u64 lwtab[64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;
+  // per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one shared GGSW
+  const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
+  if (gi >= n_ggsw) return;  // uniform per workgroup
+  const u64* ggsw = ggsw_list + (size_t)gi * 4 * N;
   load_lane_pair_tables(lwtab, tab, threadIdx.x);
   const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
   u64* o = out + ((size_t)b * 2 + w) * N;
@@ -239,18 +244,18 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
 }  // namespace pbstw
 
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
-                         int base_log, const uint64_t* tab, hipStream_t s) {
+                         int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
   const dim3 g((unsigned)batch), blk(128);
   if (sol && cmux)
-    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else if (sol)
-    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else if (cmux)
-    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else
-    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab);
+    hipLaunchKernelGGL((pbstw::ext_tw_kernel<false>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   return hipGetLastError();
 }
 

@@ -55,6 +55,8 @@ _SIGS = {
     "mi_bsk_to_ntt64": (_int, [_vp, _vp, _vp, _sz, ctypes.c_uint, _int, _vp]),
     "mi_ext_product_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _int, _vp]),
     "mi_cmux_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _int, _vp]),
+    "mi_ext_product_ntt64_batch_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _int, _int, _sz, _int, _vp]),
+    "mi_cmux_ntt64_batch_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _int, _int, _sz, _int, _vp]),
     "mi_pbs_ntt64_key_create": (_int, [_vp, _vp, _sz, _int, _int, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_key_destroy": (_int, [_vp]),
     "mi_pbs_ntt64_key_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int),

@@ -73,7 +73,7 @@ def convert_standard_lwe_bootstrap_key_to_ntt64(plan, input_bsk, output_bsk, nor
                                 _stream(output_bsk)))
 
 
-def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux):
+def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux, ggsw_index=None):
     n = plan.ntt_size()
     if out.dim() < 2:
         raise ValueError(f"assertion failed: out shape {tuple(out.shape)} != (..., k + 1, {n})")
@@ -81,29 +81,46 @@ def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux):
     b = _glwe_batch(out, k, n, "out")
     if glwe.shape != out.shape:
         raise ValueError(f"assertion failed: glwe shape {tuple(glwe.shape)} != out shape {tuple(out.shape)}")
-    _ggsw_shape(plan, ggsw, level, k)
-    fn = lib().mi_cmux_ntt64_batch if cmux else lib().mi_ext_product_ntt64_batch
-    check(fn(plan.handle, _dev(out, "out"), _dev(glwe, "glwe"), _dev(ggsw, "ggsw"), k, base_log, level, b, variant,
-             _stream(out)))
+    if ggsw_index is None:
+        _ggsw_shape(plan, ggsw, level, k)
+        fn = lib().mi_cmux_ntt64_batch if cmux else lib().mi_ext_product_ntt64_batch
+        check(fn(plan.handle, _dev(out, "out"), _dev(glwe, "glwe"), _dev(ggsw, "ggsw"), k, base_log, level, b,
+                 variant, _stream(out)))
+        return
+    # one GGSW per item: ggsw = (n_ggsw, level, k+1, k+1, N), ggsw_index = `b` int32 / uint32 device indices
+    want = (level, k + 1, k + 1, n)
+    if ggsw.dim() != 5 or tuple(ggsw.shape[1:]) != want:
+        raise ValueError(f"assertion failed: ggsw list shape {tuple(ggsw.shape)} != (n_ggsw, *{want})")
+    import torch
+
+    if (ggsw_index.dtype not in (torch.int32, torch.uint32) or ggsw_index.numel() != b or not ggsw_index.is_cuda
+            or not ggsw_index.is_contiguous()):
+        raise ValueError(f"assertion failed: ggsw_index must be {b} contiguous int32 device indices")
+    fn = lib().mi_cmux_ntt64_batch_indexed if cmux else lib().mi_ext_product_ntt64_batch_indexed
+    check(fn(plan.handle, _dev(out, "out"), _dev(glwe, "glwe"), _dev(ggsw, "ggsw"),
+             ctypes.c_void_p(ggsw_index.data_ptr()), int(ggsw.shape[0]), k, base_log, level, b, variant, _stream(out)))
 
 
-def add_external_product_ntt64_assign(plan, out, ggsw, glwe, base_log: int, level: int) -> None:
-    """out += ggsw (.) glwe modulo the Solinas prime; ``ggsw`` NTT-domain (converted Normalize)."""
-    _ext(plan, out, ggsw, glwe, base_log, level, SOLINAS, False)
+def add_external_product_ntt64_assign(plan, out, ggsw, glwe, base_log: int, level: int, ggsw_index=None) -> None:
+    """out += ggsw (.) glwe modulo the Solinas prime; ``ggsw`` NTT-domain (converted Normalize).  With
+    ``ggsw_index`` (int32 device tensor, one entry per item) ``ggsw`` is a list (n_ggsw, level, k+1, k+1, N) and
+    item b uses ``ggsw[ggsw_index[b]]`` (an out-of-range index leaves the item untouched)."""
+    _ext(plan, out, ggsw, glwe, base_log, level, SOLINAS, False, ggsw_index)
 
 
-def add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, base_log: int, level: int) -> None:
-    """out += ggsw (.) glwe on native 2^64 ciphertexts; ``ggsw`` NTT-domain (converted Raw)."""
-    _ext(plan, out, ggsw, glwe, base_log, level, BNF, False)
+def add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, base_log: int, level: int, ggsw_index=None) -> None:
+    """out += ggsw (.) glwe on native 2^64 ciphertexts; ``ggsw`` NTT-domain (converted Raw); ``ggsw_index`` as
+    ``add_external_product_ntt64_assign``."""
+    _ext(plan, out, ggsw, glwe, base_log, level, BNF, False, ggsw_index)
 
 
-def cmux_ntt64_assign(plan, ct0, ct1, ggsw, base_log: int, level: int) -> None:
+def cmux_ntt64_assign(plan, ct0, ct1, ggsw, base_log: int, level: int, ggsw_index=None) -> None:
     """ct0 = cmux(ggsw, ct0, ct1) mod p; like the reference, ct1 is left holding ct1 - ct0."""
-    _ext(plan, ct0, ggsw, ct1, base_log, level, SOLINAS, True)
+    _ext(plan, ct0, ggsw, ct1, base_log, level, SOLINAS, True, ggsw_index)
 
 
-def cmux_ntt64_bnf_assign(plan, ct0, ct1, ggsw, base_log: int, level: int) -> None:
-    _ext(plan, ct0, ggsw, ct1, base_log, level, BNF, True)
+def cmux_ntt64_bnf_assign(plan, ct0, ct1, ggsw, base_log: int, level: int, ggsw_index=None) -> None:
+    _ext(plan, ct0, ggsw, ct1, base_log, level, BNF, True, ggsw_index)
 
 
 class NttBootstrapKey:
