@@ -412,7 +412,11 @@ def gen_ext(tabs, cmux, sol=False):
         B.raw(f"s_add_u32 s{S_TWI}, %[tab_lo], {2 * 2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0")
     B.raw(f"s_mov_b32 s{S_GL}, %[glwe_lo]", f"s_mov_b32 s{S_GL + 1}, %[glwe_hi]",
           f"s_mov_b32 s{S_OUT}, %[out_lo]", f"s_mov_b32 s{S_OUT + 1}, %[out_hi]")
-    B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
+    if cmux:  # ct1 -= ct0 needs the out rows (ct0) first
+        B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
+    else:  # the out rows are only read by the final accumulate: issued last, waited for only by the MAC's waits
+        # (vmcnt waits for at most the count given, so the MAC's chunk waits over-cover them, which is safe)
+        B.raw(*load_rows(64, S_GL), *gload(0), *gload(1), *load_rows(ACC, S_OUT), "s_waitcnt vmcnt(48)")
     sg = Seg()
     sls = slots_at([8, 16, 24, 32, 40, 48, 56])
     for r in range(32):
@@ -441,7 +445,7 @@ def gen_ext(tabs, cmux, sol=False):
         add_acc_sol(B, dmap)
     else:
         modswitch_acc(B, dmap)
-    B.raw(*store_rows(ACC, S_OUT), "s_waitcnt vmcnt(0)")
+    B.raw(*store_rows(ACC, S_OUT))  # no final wait: the wave retires while its stores drain
     return B
 
 
