@@ -141,7 +141,7 @@ def slots_at(bases):
     return [T.Slot(b, SG0 + 6 * i) for i, b in enumerate(bases)]
 
 
-def decompose(sg, sl, xl, xh):
+def decompose(sg, sl, xl, xh, signed=False):
     """Level-1 signed decomposition of the native u64 (xl, xh) in place (closest representable +
     one balanced digit, decomposer.rs:156-185 + iter.rs:131-151), mapped into [0, p) (ntt64.rs:231-238).
     With t = the top B + 1 bits of x (rounding bit last) the reference's digit is
@@ -156,13 +156,15 @@ def decompose(sg, sl, xl, xh):
     sg.add(f"v_cmp_eq_u32_e64 {c[2]}, s{S_K1}, {t}", [t], [c[2]])
     sg.add(f"v_sub_u32 {nd}, 0, {xl}", [xl], [nd])
     sg.add(f"v_cndmask_b32_e64 {xl}, {xl}, {nd}, {c[2]}", [xl, nd, c[2]], [xl])
+    if signed:  # the signed digit in xl only: stage0_signed consumes it
+        return
     sg.add(f"v_ashrrev_i32 {xh}, 31, {xl}", [xl], [xh])
     sg.add(f"v_and_b32 {m}, -15, {xh}", [xh], [m])
     xp = pv(int(xl[1:]))
     sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
 
 
-def decompose_sol(sg, sl, xl, xh):
+def decompose_sol(sg, sl, xl, xh, signed=False):
     """Level-1 signed decomposition of x in [0, p] modulo the Solinas prime, in place, mapped into
     [0, p): TensorSignedDecompositionLendingIterNonNative (iter.rs:623-745) with one level.  The sign is
     s = x >= p / 2 + 1 (div_ceil), the magnitude |x| = s ? p - x : x < 2^63, the rounded state
@@ -180,11 +182,51 @@ def decompose_sol(sg, sl, xl, xh):
     sg.add(f"v_lshrrev_b32 {t}, 1, {t}", [t], [t])                                  # state = digit
     sg.add(f"v_sub_u32 {nl}, 0, {t}", [t], [nl])
     sg.add(f"v_cndmask_b32_e64 {xl}, {t}, {nl}, {c[2]}", [t, nl, c[2]], [xl])
+    if signed:
+        return
     sg.add(f"v_ashrrev_i32 {xh}, 31, {xl}", [xl], [xh])
     m = v[4]
     sg.add(f"v_and_b32 {m}, -15, {xh}", [xh], [m])
     xp = pv(int(xl[1:]))
     sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
+
+
+def stage0_signed(B, tabs, dmap):
+    """The forward's first stage (registers r, r + 16, twiddle 2^48) straight from the signed level-1 digits the
+    decomposition leaves in the low words (|d| < 2^31), instead of mapping each digit into [0, p) and running a
+    general shift-class butterfly.  With bh = d_b >> 16 (arithmetic) and T = (d_b mod 2^16) 2^48 (high word
+    d_b << 16, low word 0): d_b 2^48 = T + bh 2^64 = T + bh EPS (mod p), so a + d_b 2^48 = S0 + T and
+    a - d_b 2^48 = S1 - T with S0 = d_a + bh EPS = sext(d_a - bh) + bh 2^32 and S1 = d_a - bh EPS =
+    sext(d_a + bh) - bh 2^32 (|S| < 2^47), each made canonical (S < 0: S - EPS mod 2^64 = S + p).  T < p, so
+    a' = S0 + T (one carry fix) and b' = S1 - T (one borrow fix) need only high-word arithmetic: 16 VALU, 12 of
+    them single-rate 32-bit ops, per butterfly, and no digit is ever mapped into [0, p) on its own."""
+    assert all(e == 48 for e in tabs["G1_FWD"][0]), "stage 0 twiddle is not 2^48"
+    sg = Seg()
+    sls = B.slots(free_blocks_except(dmap))
+    for r in range(16):
+        sl = sls[r % len(sls)]
+        v, c = sl.v, sl.c
+        al, ah, ap = X(dmap, r)
+        bl, bh, bp = X(dmap, r + 16)
+        hb, th, m0, m1 = v[0], v[1], v[2], v[3]
+        sg.add(f"v_ashrrev_i32 {hb}, 16, {bl}", [bl], [hb])                      # bh = d_b >> 16
+        sg.add(f"v_lshlrev_b32 {th}, 16, {bl}", [bl], [th])                      # T high word
+        sg.add(f"v_add_u32 {bl}, {al}, {hb}", [al, hb], [bl])                    # S1 = sext(d_a + bh) - bh 2^32
+        sg.add(f"v_sub_u32 {al}, {al}, {hb}", [al, hb], [al])                    # S0 = sext(d_a - bh) + bh 2^32
+        sg.add(f"v_ashrrev_i32 {bh}, 31, {bl}", [bl], [bh])
+        sg.add(f"v_sub_u32 {bh}, {bh}, {hb}", [bh, hb], [bh])
+        sg.add(f"v_ashrrev_i32 {ah}, 31, {al}", [al], [ah])
+        sg.add(f"v_add_u32 {ah}, {ah}, {hb}", [ah, hb], [ah])
+        for (lo, hi, pair, m) in ((al, ah, ap, m0), (bl, bh, bp, m1)):            # S < 0: S + p
+            sg.add(f"v_ashrrev_i32 {m}, 31, {hi}", [hi], [m])
+            sg.add(f"v_and_b32 {m}, -15, {m}", [m], [m])
+            sg.add(f"v_mad_i64_i32 {pair}, {JUNK}, {m}, s{T.S_X15}, {pair}", [m, lo, hi], [lo, hi, JUNK])
+        sg.add(f"v_sub_co_u32_e64 {bh}, {c[0]}, {bh}, {th}", [bh, th], [bh, c[0]])   # b' = S1 - T
+        minus_eps(sg, v[4], c[0], bp)
+        sg.add(f"v_add_co_u32_e64 {ah}, {c[1]}, {ah}, {th}", [ah, th], [ah, c[1]])   # a' = S0 + T
+        sg.add(f"v_cndmask_b32_e64 {v[5]}, 0, -1, {c[1]}", [c[1]], [v[5]])
+        sg.add(f"v_mad_u64_u32 {ap}, {JUNK}, {v[5]}, 1, {ap}", [v[5], al, ah], [al, ah, JUNK])
+    sched(B, sg)
 
 
 def rotate_decompose(B, sol=False):
@@ -225,7 +267,7 @@ def rotate_decompose(B, sol=False):
                 sg.add(f"v_sub_co_u32_e64 {xl}, {c[0]}, {xl}, {al}", [xl, al], [xl, c[0]])
                 sg.add(f"v_subb_co_u32_e64 {xh}, {c[1]}, {xh}, {ah}, {c[0]}", [xh, ah, c[0]], [xh, c[1]])
                 minus_eps(sg, v[5], c[1], pv(int(xl[1:])))
-                decompose_sol(sg, sl, xl, xh)
+                decompose_sol(sg, sl, xl, xh, signed=True)
                 continue
             sg.add(f"v_xor_b32 {xl}, {m}, {xl}", [m, xl], [xl])
             sg.add(f"v_xor_b32 {xh}, {m}, {xh}", [m, xh], [xh])
@@ -233,7 +275,7 @@ def rotate_decompose(B, sol=False):
             sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {m}, {c[0]}", [xh, m, c[0]], [xh, JUNK])
             sg.add(f"v_sub_co_u32_e64 {xl}, {c[1]}, {xl}, {al}", [xl, al], [xl, c[1]])
             sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {c[1]}", [xh, ah, c[1]], [xh, JUNK])
-            decompose(sg, sl, xl, xh)
+            decompose(sg, sl, xl, xh, signed=True)
         sched(B, sg)
 
 
@@ -381,7 +423,8 @@ def gen_pbs(tabs, sol=False):
           "s_cbranch_scc1 Lpbs_skip_%=")
     B.raw(*gload(0), *gload(1))
     rotate_decompose(B, sol)
-    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
+    stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
+    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
     mac(B, dmap)
     dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
     if sol:
@@ -436,9 +479,10 @@ def gen_ext(tabs, cmux, sol=False):
         B.raw(*store_rows(64, S_GL))
     sg = Seg()
     for r in range(32):
-        (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}")
+        (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
     sched(B, sg)
-    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR)
+    stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
+    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
     mac(B, dmap)
     dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
     if sol:

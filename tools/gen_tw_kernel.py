@@ -842,7 +842,7 @@ def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None, first_loaded=F
         B.mulrows(dmap, list(range(8 * bt, 8 * bt + 8)), [buf(bt % 2, k) for k in range(8)], ms, zero_hi=False)
 
 
-def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False):
+def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=0):
     """Forward transform of the W0 data in dmap (must be v64..v127); returns the output dmap (W0,
     canonical).  With `stop`, returns early (debug bodies).  `prefetch` (the standalone kernel, whose
     waves run in lockstep so a wait on a table load is not covered by other waves): the first twist
@@ -852,7 +852,7 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False):
     if prefetch:
         B.raw(*[ad.tw_load(0, k, 8 + 2 * k) for k in range(8)])
     fb = free_blocks_except(dmap, busy)
-    for s in range(5):
+    for s in range(first_stage, 5):  # first_stage 1: the caller ran stage 0 (the PBS bodies' signed digits)
         gw = None
         if s == 0 and PROGRESSIVE and prefetch:  # rows issued as pairs (k, k + 16), then the 8 twist-row loads
             gw = [f"s_waitcnt vmcnt({40 - 8 * (g + 1)})" for g in range(4)]
