@@ -55,10 +55,10 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
   return total_half - (u64)(total_hed / 2) - (1ull << (64u - LOG_MOD - 1u));
 }
 
-// The lane-pair twiddles of the forward and inverse transforms (tab[N..N+31], tab[2N+32+..]: the
-// same for the plain and the N^-1-folded inverse tables) into LDS, read by the body's pair stage.
+// The forward's lane-pair twiddles (tab[N..N+31]) and the W1'' inverse's last-DIT-stage twiddles (tab[3 (N+32)..],
+// powers of two: the same for the plain and the N^-1-folded untwist) into LDS, read by the bodies' pair stages.
 __device__ __forceinline__ void load_lane_pair_tables(u64* lwtab, const u64* __restrict__ tab, int t) {
-  if (t < 64) lwtab[t] = t < 32 ? tab[N + t] : tab[2 * N + 32 + (t - 32)];
+  if (t < 64) lwtab[t] = t < 32 ? tab[N + t] : tab[3 * (N + 32) + (t - 32)];
   __syncthreads();
 }
 

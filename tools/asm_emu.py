@@ -408,12 +408,15 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False):
 
 
 def _lds_with_lane_pair_tables(tab, N):
-    """Workgroup LDS as pbs_tw.hip lays it out: 2 x N exchange buffers, then the 32 forward and 32
-    inverse lane-pair twiddles (tab[N:N+32], tab[N+32+N : N+32+N+32])."""
+    """Workgroup LDS as pbs_tw.hip lays it out: 2 x N exchange buffers, then the 32 forward lane-pair twiddles
+    (tab[N:N+32]) and the W1'' inverse's 32 last-DIT-stage twiddles, entry m + 16 par = 2^(-3 (2 m + par) mod 192)
+    (the plan's fourth table region, c_api.cpp)."""
+    P = 0xFFFFFFFF00000001
     lds = np.zeros(2 * N + 64, dtype=np.uint64)
     t = np.array(tab, dtype=np.uint64)
     lds[2 * N:2 * N + 32] = t[N:N + 32]
-    lds[2 * N + 32:2 * N + 64] = t[2 * N + 32:2 * N + 64]
+    lds[2 * N + 32:2 * N + 64] = [pow(2, (192 - 3 * (2 * m + par) % 192) % 192, P)
+                                  for par in range(2) for m in range(16)]
     return lds
 
 

@@ -55,15 +55,19 @@ def sp(b):
     return f"s[{b}:{b + 1}]"
 
 
+V_T1X = 249   # the W1'' inverse's transpose address S + 8 (lane + (lane >> 5)); its read address equals V_T2WL
+
+
 def addr_for(tab):
     return Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, v{VOFF + bt}, {sp(tab)} offset:{512 * k}",
                 t1w=f"v{V_T1W}", t1r=f"v{V_T1R}", t2wl=f"v{V_T2WL}", t2wh=f"v{V_T2WH}", t2r=f"v{V_T2R}",
-                t4w=f"v{V_T4W}", t4r=f"v{V_T4R}", lwo=f"v{V_LWO}", lw=sp(tab))
+                t4w=f"v{V_T4W}", t4r=f"v{V_T4R}", lwo=f"v{V_LWO}", lw=sp(tab), t1x=f"v{V_T1X}", t1y=f"v{V_T2WL}")
 
 
 FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
-# the lane-pair twiddles (32 forward + 32 inverse) live in the workgroup's LDS (copied by pbs_tw.hip at
-# kernel start): 4 lookups per step at LDS instead of L2 latency.  V_LWL = table base + 128 * (lane & 1).
+# the lane-pair twiddles (32 forward + the inverse's 32 last-DIT-stage twiddles of the W1'' layout) live in the
+# workgroup's LDS (copied by pbs_tw.hip at kernel start): lookups at LDS instead of L2 latency.
+# V_LWL = table base + 128 * (lane & 1).
 V_LWL = 248
 FWD_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
 INV_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
@@ -113,7 +117,9 @@ def prologue(B):
           f"v_add_u32 v{V_T2R}, %[S], v15",
           "v_add_u32 v16, v12, v9", "v_lshlrev_b32 v16, 3, v16", f"v_add_u32 v{V_T4W}, %[S], v16",
           f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}",
-          f"v_lshlrev_b32 v{V_LWL}, 7, v9", f"v_add_u32 v{V_LWL}, %[LW], v{V_LWL}")
+          f"v_lshlrev_b32 v{V_LWL}, 7, v9", f"v_add_u32 v{V_LWL}, %[LW], v{V_LWL}",
+          "v_lshrrev_b32 v17, 5, %[lane]", "v_add_u32 v17, %[lane], v17", "v_lshlrev_b32 v17, 3, v17",
+          f"v_add_u32 v{V_T1X}, %[S], v17")
 
 
 def load_rows(dst, base):
@@ -356,6 +362,14 @@ def mac(B, dmap):
     B.raw("s_barrier")
 
 
+def w1pp_regs(dmap):
+    """Register plan of the W1'' inverse after the MAC (dmap: rows 0..15 at v96.., rows 16..31 at v64..): the
+    transposed data in v8..v63 + the first four pairs of rows 0..15, the lane-pair twiddles in v64..v71 (rows
+    16.. are in LDS by then), the output's first half in v64.. and its second in v96.."""
+    assert dmap == [96 + 2 * r for r in range(16)] + [64 + 2 * r for r in range(16)], dmap
+    return dict(dst=[8 + 2 * r for r in range(28)] + [96 + 2 * r for r in range(4)], pre_base=64, ybase=64, newhi=96)
+
+
 def modswitch_acc(B, dmap):
     sg = Seg()
     sls = B.slots(free_blocks_except(dmap))
@@ -426,7 +440,7 @@ def gen_pbs(tabs, sol=False):
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
     dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
     mac(B, dmap)
-    dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
+    dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
     if sol:
         add_acc_sol(B, dmap)
     else:
@@ -484,7 +498,7 @@ def gen_ext(tabs, cmux, sol=False):
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
     dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
     mac(B, dmap)
-    dmap = T.inv_core(B, tabs, dmap, INV_ADDR)
+    dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
     if sol:
         add_acc_sol(B, dmap)
     else:

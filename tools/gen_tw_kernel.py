@@ -762,7 +762,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
     assert len(regs) >= (48 if busy else 49), len(regs)
     wb = regs[0:16]
     tmps = [regs[16:20], regs[20:24]]
-    msl = [MulSlot(regs[24], SG0), MulSlot(regs[36], SG0 + 6)]
+    msl = [MulSlot(0, SG0, regs[24:36]), MulSlot(0, SG0 + 6, regs[36:48])]
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
     # the lane-parity shift offset: the top register of the reserved block (its twiddles use the bottom)
     par3 = f"v{busy[-1]}" if busy else f"v{regs[48]}"
@@ -1067,7 +1067,7 @@ def pair_stage_dit(B, dmap, ad, pre, busy):
     assert len(regs) >= 40, len(regs)
     tmps = [regs[0:4], regs[4:8]]
     amts = [regs[8:10], regs[10:12]]
-    msl = [MulSlot(regs[16], SG0), MulSlot(regs[28], SG0 + 6)]
+    msl = [MulSlot(0, SG0, regs[16:28]), MulSlot(0, SG0 + 6, regs[28:40])]  # explicit lists: free blocks need not be contiguous
     c23 = [(f"s[{SG0 + 4}:{SG0 + 5}]",), (f"s[{SG0 + 10}:{SG0 + 11}]",)]
     par3 = f"v{regs[12]}"
     B.raw(f"v_cndmask_b32_e64 {par3}, 0, 3, s[{S_PAR}:{S_PAR + 1}]")
@@ -1097,30 +1097,34 @@ def pair_stage_dit(B, dmap, ad, pre, busy):
         B.out(sg.schedule())
 
 
-def inv_cyc_w1pp(B, dmap, ad):
-    """Standalone inverse: W0 data -> T1'' -> DIT stages 0..4 in registers -> the lane-pair DIT stage -> W0.
-    The lane-pair stage's table twiddles load right after T1'' (into v72..), five stages ahead of their use."""
-    dmap = t1_w1pp(B, dmap, [8 + 2 * r for r in range(32)], ad)
+def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64):
+    """W0 data -> T1'' -> DIT stages 0..4 in registers -> the lane-pair DIT stage -> W0.  The lane-pair stage's
+    table twiddles load right after T1'' (into pre_base..), five stages ahead of their use.  Register plan
+    (standalone defaults; the PBS bodies pass their own): `dst` (32 pairs) may reuse only rows 0..15 of `dmap`,
+    pre_base.. (8 registers) must be free of `dst`, and `ybase` (the first output half) must be free of `dst`."""
+    dmap = t1_w1pp(B, dmap, dst or [8 + 2 * r for r in range(32)], ad)
     ms = pair_stage_dit_gmul_ms()
-    pre = {m: 72 + 2 * i for i, m in enumerate(ms)}
+    pre = {m: pre_base + 2 * i for i, m in enumerate(ms)}
     assert len(ms) <= 4
-    busy = tuple(range(72, 80))
+    busy = tuple(range(pre_base, pre_base + 8))
+    assert not set(busy) & {r for b in dmap for r in (b, b + 1)}
     B.raw(*[ad.lw_load(r, m) for m, r in pre.items()])
     fb = free_blocks_except(dmap, busy)
     cf = [True] * 32  # loaded data is canonical
     for s in range(5):
         B.stage("ct", 1 << s, dit_exps_pp(s), dmap, fb, cf, by_reg=True)
     pair_stage_dit(B, dmap, ad, pre, busy)
-    return t_w1pp_w0(B, dmap, 96, 64, ad)
+    assert not set(range(ybase, ybase + 32)) & {r for b in dmap for r in (b, b + 1)}
+    return t_w1pp_w0(B, dmap, ybase, newhi, ad)
 
 
-def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False):
+def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False, w1pp_regs=None):
     """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  `prefetch`
     (standalone kernel, see fwd_core): the caller has loaded the lane-pair table twiddles into
     v40..v43 with the data; the first untwist batch is loaded into v40..v55 after the lane-pair stage
     and stays there through the cyclic stages and T4 (the one register range free in both layouts)."""
     if w1pp:
-        dmap = inv_cyc_w1pp(B, dmap, ad)
+        dmap = inv_cyc_w1pp(B, dmap, ad, **(w1pp_regs or {}))
         prefetch, busy = False, ()
     else:
         dmap = t1(B, dmap, 8, 64, ad, row_waits)
@@ -1151,7 +1155,7 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=Fa
         twist_rows(B, dmap, ad, None, ms, contiguous=False, regs=tregs, first_loaded=True)
     else:
         assert len(regs) >= 56, len(regs)
-        twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(regs[32 + 12 * i], SG0 + 6 * i) for i in range(2)],
+        twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(0, SG0 + 6 * i, regs[32 + 12 * i:44 + 12 * i]) for i in range(2)],
                    contiguous=False, regs=regs)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
