@@ -78,3 +78,23 @@ def test_single_hip_runtime_in_process(engine):
     torch.cuda.synchronize()
     paths = engine._lib.hip_runtimes()
     assert len(paths) == 1, paths
+
+
+def test_integration_rust_binding_covers_the_header():
+    """INTEGRATION.md's Rust extern block is tools/gen_rust_sys.py's output for the current header: every C-ABI
+    function is bound, with the translated signature."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gen = subprocess.run([sys.executable, os.path.join(root, "tools", "gen_rust_sys.py")], capture_output=True,
+                         text=True, check=True).stdout.strip()
+    assert gen in open(os.path.join(root, "INTEGRATION.md")).read()
+
+
+def test_integration_rust_binding_declares_every_opaque_type():
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "tfhe_ntt_amd.h")).read()
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    opaque = set(re.findall(r"typedef struct (mi_\w+) \1;", hdr))
+    assert opaque <= set(re.findall(r"pub struct (mi_\w+)", doc)), opaque - set(re.findall(r"pub struct (mi_\w+)", doc))
