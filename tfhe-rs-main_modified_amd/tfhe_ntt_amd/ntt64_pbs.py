@@ -94,8 +94,8 @@ def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux, ggsw_index=None)
     import torch
 
     if (ggsw_index.dtype not in (torch.int32, torch.uint32) or ggsw_index.numel() != b or not ggsw_index.is_cuda
-            or not ggsw_index.is_contiguous()):
-        raise ValueError(f"assertion failed: ggsw_index must be {b} contiguous int32 device indices")
+            or not ggsw_index.is_contiguous() or ggsw_index.device != out.device):
+        raise ValueError(f"assertion failed: ggsw_index must be {b} contiguous int32 indices on the GLWEs' device")
     fn = lib().mi_cmux_ntt64_batch_indexed if cmux else lib().mi_ext_product_ntt64_batch_indexed
     check(fn(plan.handle, _dev(out, "out"), _dev(glwe, "glwe"), _dev(ggsw, "ggsw"),
              ctypes.c_void_p(ggsw_index.data_ptr()), int(ggsw.shape[0]), k, base_log, level, b, variant, _stream(out)))
