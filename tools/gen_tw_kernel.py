@@ -515,10 +515,12 @@ def gen_bases(src, dst):
     return lines
 
 
-# cache-policy bits appended to the data row loads / stores (gfx950: "nt", "sc0", "sc1"); the product
-# bodies use the default policy unless tools/variant_probe measures another one faster
+# cache-policy bits appended to the data row loads / stores (gfx950: "nt", "sc0", "sc1").  Stores carry sc0 sc1
+# (system scope): tools/variant_probe measured the forward 2.0 % and the 4-wave inverse 3.9 % faster per launch
+# (back-to-back launches, so the dependent-launch gap is included: fewer dirty L2 lines to write back at the kernel
+# boundary), sc1 alone about half of that, nt sc1 10 % slower; loads keep the default policy (nt loads were slower)
 LOAD_POLICY = ""
-STORE_POLICY = ""
+STORE_POLICY = " sc0 sc1"
 INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
 PROGRESSIVE = True   # forward: start the first stage as the data rows arrive (4 waits) instead of one vmcnt(0):
                      # 0.6 % faster (tools/variant_probe); the same per row in the inverse's T1 was 0.8 % slower
