@@ -128,7 +128,7 @@ def load_rows(dst, base):
 
 
 def store_rows(src, base):
-    return [f"global_store_dwordx2 v{VOFF + r // 8}, {pv(src + 2 * r)}, {sp(base)} offset:{512 * (r % 8)}"
+    return [f"global_store_dwordx2 v{VOFF + r // 8}, {pv(src + 2 * r)}, {sp(base)} offset:{512 * (r % 8)}{T.STORE_POLICY}"
             for r in range(32)]
 
 
