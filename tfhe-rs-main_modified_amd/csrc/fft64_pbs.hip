@@ -10,8 +10,8 @@
 // values u[n] = x[n] + i x[n + M] (forward_with_conv's split), twisted by w^n = exp(i pi n / 2M)
 // (Twisties::new(M)), and transformed with an M-point complex DFT (exp(-2 pi i / M) kernel).  The reference
 // runs tfhe-fft's measured "unordered" plan, whose Fourier-domain order is implementation defined; here the
-// order is this engine's own (documented below, exported by mi_fft64_fourier_order), and keys converted by this
-// engine are read by this engine only.  Results are f64 computations, not bit-identical to the reference's
+// order is this engine's own (documented below, exported by mi_fft64_fourier_order); the reference serialises the
+// natural order, which fourier_reorder_kernel converts to and from.  Results are f64 computations, not bit-identical to the reference's
 // (parity is decryption + an error bound against a numpy restatement).
 //
 // MI355X mapping: one wave per polynomial, 16 complex values per lane in VGPRs (lane j holds u[j + 64 m],
