@@ -231,12 +231,22 @@ int mi_multi_gpu_scatter(mi_multi_gpu *m, const void *src, void *const *dsts, si
 /* multi_gpu_gather_lwe_async, trivial index: shard i of dst (devices[0]) <- srcs[i] */
 int mi_multi_gpu_gather(mi_multi_gpu *m, void *dst, const void *const *srcs, size_t total, size_t unit_bytes,
                         void *stream);
-/* Batched PBS over the device set: scatter lwe_in (devices[0]), mi_pbs_ntt64_batch on every device with
- * keys[i] / luts[i] (bound to devices[i], same shape), gather into lwe_out (devices[0]).  Shard 0 runs in
- * place on `stream`; the others use stream-ordered scratch on their device. */
+/* Batched PBS over the device set: scatter lwe_in (devices[0]), mi_pbs_ntt64_batch on every active device
+ * with keys[i] / luts[i] (bound to devices[i], same shape), gather into lwe_out (devices[0]).  Only the first
+ * get_active_gpu_count(batch, count) entries are active (helper_multi_gpu.cu:42-49, min(ceil(batch / 12),
+ * count), as the reference's CudaStreams::active_gpu_subset, helper_multi_gpu.h:74-79); the keys / LUTs of
+ * inactive entries are not read and may be NULL.  Shard 0 runs in place on `stream`; the others use
+ * stream-ordered scratch on their device.
+ * _ordered: producer_streams[i] is the stream of devices[i] that produced keys[i] / luts[i] (NULL array or
+ * entry: that device's legacy null stream).  Shard i starts after the work queued on it and it is ordered
+ * after shard i's last read, so the caller may release / reuse the LUT on that stream right away.
+ * mi_pbs_ntt64_multi_gpu is _ordered with producer_streams = NULL. */
 int mi_pbs_ntt64_multi_gpu(mi_multi_gpu *m, const mi_pbs_ntt64_key *const *keys, uint64_t *lwe_out,
                            const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
                            void *stream);
+int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu *m, const mi_pbs_ntt64_key *const *keys, uint64_t *lwe_out,
+                                   const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
+                                   void *stream, void *const *producer_streams);
 
 /* ---- f64-FFT PBS (the default shortint PBS path) ----------------------------
  * Reference paths relative to /root/reference/tfhe/src/core_crypto.  The negacyclic f64 FFT of

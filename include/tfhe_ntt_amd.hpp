@@ -206,9 +206,9 @@ class NttBootstrapKey {
                               int format = MI_NTT_BSK_PLAIN, void* stream = nullptr) {
     mi_pbs_ntt64_key* raw = nullptr;
     check(mi_pbs_ntt64_key_load(plan.raw(), bytes, len, format, variant, stream, &raw));
-    size_t n_lwe = 0;
-    check(mi_pbs_ntt64_key_info(raw, &n_lwe, nullptr, nullptr, nullptr, nullptr));
-    return NttBootstrapKey(raw, n_lwe, variant);
+    NttBootstrapKey key(raw, 0, variant);  // owns the upload before anything else can throw
+    check(mi_pbs_ntt64_key_info(raw, &key.n_lwe_, nullptr, nullptr, nullptr, nullptr));
+    return key;
   }
   NttBootstrapKey(NttBootstrapKey&& o) noexcept
       : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_), variant_(o.variant_) {}
@@ -364,9 +364,9 @@ class FourierBootstrapKey {
                                   void* stream = nullptr) {
     mi_fft64_pbs_key* k = nullptr;
     check(mi_fft64_pbs_key_load(fft.raw(), bytes, len, versioned ? MI_NTT_BSK_VERSIONED : MI_NTT_BSK_PLAIN, stream, &k));
-    size_t n = 0;
-    check(mi_fft64_pbs_key_info(k, &n, nullptr, nullptr, nullptr));
-    return FourierBootstrapKey(k, n);
+    FourierBootstrapKey key(k, 0);  // owns the upload before anything else can throw
+    check(mi_fft64_pbs_key_info(k, &key.n_lwe_, nullptr, nullptr, nullptr));
+    return key;
   }
   // this key as the reference's bytes
   std::vector<uint8_t> serialize(bool versioned = false, void* stream = nullptr) const {

@@ -223,6 +223,8 @@ _PBS_SIGS["ora_pbs_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.
 _PBS_SIGS["ora_pbs_bnf_ms"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, ctypes.c_int])
 _PBS_SIGS["ora_centered_ms_body_correction"] = (_u64, [_p64, _sz, ctypes.c_uint])
 _PBS_SIGS["ora_pbs_set_fast_ntt"] = (None, [ctypes.c_int])
+_PBS_SIGS["ora_pbs_solinas_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, _sz,
+                                         ctypes.c_int])
 _PBS_SIGS["ora_ext_product_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz, ctypes.c_int])
 _pbs_ready = False
 
@@ -301,6 +303,15 @@ class NttContext:
             out = np.zeros((batch, k * self.n + 1), np.uint64)
         _plib().ora_pbs_bnf_batch(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
                                   _ptr(_u(bsk)), n_lwe, batch, int(centered), threads)
+        return out
+
+    def pbs_batch_solinas(self, lwe_in, lut, bsk, k, base_log, level, threads=8, out=None):
+        lwe_in = _u(lwe_in)
+        batch, n_lwe = lwe_in.shape[0], lwe_in.shape[1] - 1
+        if out is None:
+            out = np.zeros((batch, k * self.n + 1), np.uint64)
+        _plib().ora_pbs_solinas_batch(self.tables, k, base_log, level, _ptr(out), _ptr(lwe_in), _ptr(_u(lut)),
+                                      _ptr(_u(bsk)), n_lwe, batch, threads)
         return out
 
     def bsk_to_ntt(self, bsk_std, in_width=64, normalize=False):

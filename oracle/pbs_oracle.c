@@ -320,6 +320,19 @@ void ora_pbs_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, 
                        n_lwe, centered);
 }
 
+/* programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized (ntt64_pbs.rs:482-538) over a batch, one PBS per
+ * thread as the reference's rayon throughput harness (pbs_bench.rs:865-886) */
+void ora_pbs_solinas_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
+                           const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe,
+                           size_t batch, int threads) {
+    const size_t out_len = (size_t)k * t->n + 1, in_len = n_lwe + 1;
+    long long b;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
+    for (b = 0; b < (long long)batch; ++b)
+        ora_pbs_solinas(t, k, base_log, level, lwe_out + (size_t)b * out_len, lwe_in + (size_t)b * in_len, lut, bsk,
+                        n_lwe);
+}
+
 void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
                                const uint64_t *ggsw, const uint64_t *glwe, size_t batch, int threads) {
     const size_t len = ((size_t)k + 1) * t->n;

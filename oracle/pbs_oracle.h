@@ -98,6 +98,9 @@ void ora_bsk_to_ntt(const ora_ntt_tables *t, const uint64_t *bsk_std, uint64_t *
 void ora_pbs_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
                        const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe,
                        size_t batch, int centered, int threads);
+void ora_pbs_solinas_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
+                           const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe,
+                           size_t batch, int threads);
 void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
                                const uint64_t *ggsw, const uint64_t *glwe, size_t batch, int threads);
 

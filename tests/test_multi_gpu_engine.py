@@ -209,3 +209,163 @@ def test_two_rank_real_engine(oracle, tmp_path):
     assert np.array_equal(out, want)
     polys = np.load(base + "_polys.npy").view(np.uint64)
     assert np.array_equal(np.load(base + "_fwd.npy").view(np.uint64), oracle.Plan.try_new(N, P).fwd(polys))
+
+
+@pytest.mark.gpu
+def test_device_set_active_count_13_on_8(engine, oracle):
+    """get_active_gpu_count inside mi_pbs_ntt64_multi_gpu (helper_multi_gpu.cu:42-49): 13 bootstraps on an
+    8-entry set run on the first ceil(13 / 12) = 2 entries (7 + 6).  The other six entries get no key and no
+    LUT (None): the call succeeds only if they are never read.  Output == one launch == the oracle."""
+    import torch
+    M = engine.ntt64_pbs
+    g = H.rng(1308)
+    n_lwe, batch = 20, 13
+    plan = engine.Plan.try_new(N, P)
+    bsk = g.integers(0, P, size=(n_lwe, 1, 2, 2, N), dtype=np.uint64)
+    lut = H.uniform_u64(g, (2, N))
+    lwe = H.uniform_u64(g, (batch, n_lwe + 1))
+    key = M.NttBootstrapKey(plan, _dev(bsk), 23, 1, M.BNF)
+    ds = engine.multi_gpu.DeviceSet([0] * 8)
+    assert ds.active_count(batch) == 2
+    lt = _dev(lut)
+    out_multi = torch.zeros((batch, N + 1), dtype=torch.int64, device="cuda")
+    ds.programmable_bootstrap([key, key] + [None] * 6, _dev(lwe), out_multi, [lt, lt] + [None] * 6)
+    with pytest.raises(ValueError):  # an active entry without a LUT is refused before the ABI
+        ds.programmable_bootstrap([key] * 8, _dev(lwe), out_multi, [lt] + [None] * 7)
+    out_one = torch.zeros_like(out_multi)
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(_dev(lwe), out_one, lt, key)
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(out_multi), _host(out_one))
+    want = oracle.NttContext(N).pbs_batch_bnf(lwe[[0, 6, 7, 12]], lut.reshape(-1), bsk.reshape(-1), 1, 23, 1, threads=8)
+    assert np.array_equal(_host(out_multi)[[0, 6, 7, 12]], want)
+
+
+@pytest.mark.gpu
+def test_device_set_producer_stream_ordering(engine):
+    """Every shard is ordered after the stream that produced its LUT, not only after the caller's
+    stream: the LUT copies are queued on a producer stream behind ~2 ms of transforms, and the PBS is queued on
+    another stream (torch's default stream) with that producer passed through mi_pbs_ntt64_multi_gpu_ordered.  An
+    unordered read would bootstrap with the zero LUTs.  The producer stream is then ordered after the PBS: work
+    queued on it next (zeroing the LUTs) must not reach the bootstrap."""
+    import ctypes
+
+    import torch
+    from tfhe_ntt_amd._lib import check, lib
+    M = engine.ntt64_pbs
+    g = H.rng(77)
+    n_lwe, batch, entries = 16, 48, 4
+    plan = engine.Plan.try_new(N, P)
+    bsk = g.integers(0, P, size=(n_lwe, 1, 2, 2, N), dtype=np.uint64)
+    lut = H.uniform_u64(g, (2, N))
+    lwe = H.uniform_u64(g, (batch, n_lwe + 1))
+    key = M.NttBootstrapKey(plan, _dev(bsk), 23, 1, M.BNF)
+    src_lut, src_lwe = _dev(lut), _dev(lwe)
+    ref = torch.zeros((batch, N + 1), dtype=torch.int64, device="cuda")
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(src_lwe, ref, src_lut, key)
+    busy = torch.zeros((4096, N), dtype=torch.int64, device="cuda")
+    luts = [torch.zeros((2, N), dtype=torch.int64, device="cuda") for _ in range(entries)]
+    out = torch.zeros_like(ref)
+    torch.cuda.synchronize()
+    ds = engine.multi_gpu.DeviceSet([0] * entries)
+    assert ds.active_count(batch) == entries
+    producer = torch.cuda.Stream()
+    caller = torch.cuda.default_stream()
+    with torch.cuda.stream(producer):
+        for _ in range(20):
+            plan.fwd(busy)
+            plan.inv(busy)
+        for t in luts:
+            t.copy_(src_lut)
+    kp = (ctypes.c_void_p * entries)(*[key._h.value] * entries)
+    lp = (ctypes.c_void_p * entries)(*[t.data_ptr() for t in luts])
+    ps = (ctypes.c_void_p * entries)(*[producer.cuda_stream] * entries)
+    check(lib().mi_pbs_ntt64_multi_gpu_ordered(ds._h, kp, ctypes.c_void_p(out.data_ptr()),
+                                               ctypes.c_void_p(src_lwe.data_ptr()), lp, batch, 0,
+                                               ctypes.c_void_p(caller.cuda_stream), ps))
+    with torch.cuda.stream(producer):
+        for t in luts:
+            t.zero_()
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(out), _host(ref))
+
+
+@pytest.mark.gpu
+def test_device_set_two_distinct_devices(engine):
+    """The cross-device path (peer copies, per-device keys, producer ordering on a second device); skipped on a
+    one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    M = engine.ntt64_pbs
+    g = H.rng(2002)
+    n_lwe, batch = 16, 40
+    bsk = g.integers(0, P, size=(n_lwe, 1, 2, 2, N), dtype=np.uint64)
+    lut = H.uniform_u64(g, (2, N))
+    lwe = H.uniform_u64(g, (batch, n_lwe + 1))
+    keys, luts = [], []
+    for d in (0, 1):
+        with torch.cuda.device(d):
+            plan = engine.Plan.try_new(N, P, device=d)
+            keys.append(M.NttBootstrapKey(plan, _dev(bsk).to(f"cuda:{d}"), 23, 1, M.BNF))
+            luts.append(_dev(lut).to(f"cuda:{d}"))
+    ds = engine.multi_gpu.DeviceSet([0, 1])
+    out = torch.zeros((batch, N + 1), dtype=torch.int64, device="cuda:0")
+    ds.programmable_bootstrap(keys, _dev(lwe), out, luts)
+    one = torch.zeros_like(out)
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(_dev(lwe), one, luts[0], keys[0])
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(out), _host(one))
+
+
+@pytest.mark.gpu
+def test_config5_device_set_65536_real_keys(engine, oracle):
+    """BASELINE config 5's workload on the HIP path: one global batch of 65,536 PBS at PARAM_MESSAGE_2_CARRY_2
+    (n = 918, N = 2048, B = 2^23, l = 1, TUniform 2^45 LWE / 2^17 GLWE noise bounds, ks_pbs.rs:29-47) under real
+    keys, split by mi_pbs_ntt64_multi_gpu over an 8-entry DeviceSet (one card stands in for the 8 GPUs: every
+    entry is device 0, so the split, the scatter / gather copies and the 8 shard launches all run).
+    * every one of the 65,536 outputs decrypts to f(m);
+    * the sharded output equals one single-launch run of the whole batch, bit for bit;
+    * 72 ciphertexts spread over all eight shards (every 1024th, plus each shard's first and last) equal the
+      oracle PBS bit for bit."""
+    import torch
+    n_lwe, base_log, level, msg_mod, batch, entries = 918, 23, 1, 16, 65536, 8
+    delta = (1 << 63) // msg_mod
+    g = H.rng(65536918)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (1, N))
+    bsk = H.bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, 17)
+    f = lambda x: (3 * x + 1) % msg_mod
+    lut = H.pbs_lut(N, 1, msg_mod, delta, f)
+    msgs = (np.arange(batch) * 7 + 3) % msg_mod
+    M = engine.ntt64_pbs
+    plan = engine.Plan.try_new(N, P)
+    gkey = _dev(np.zeros_like(bsk))
+    M.convert_standard_lwe_bootstrap_key_to_ntt64(plan, _dev(bsk), gkey, normalize=False, input_modulus_width=64)
+    nbsk = _host(gkey)
+    key = M.NttBootstrapKey(plan, gkey, base_log, level, M.BNF)
+    lwe = np.concatenate([H.lwe_encrypt_batch(g, msgs[i:i + 8192].astype(np.uint64) * np.uint64(delta), lwe_sk, 45)
+                          for i in range(0, batch, 8192)])
+    lt = _dev(lut)
+    src = _dev(lwe)
+    ds = engine.multi_gpu.DeviceSet([0] * entries)
+    assert ds.active_count(batch) == entries
+    out = torch.zeros((batch, N + 1), dtype=torch.int64, device="cuda")
+    ds.programmable_bootstrap([key] * entries, src, out, [lt] * entries)
+    one = torch.zeros_like(out)
+    M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(src, one, lt, key)
+    torch.cuda.synchronize()
+    assert torch.equal(out, one), "sharded PBS != single launch"
+    got = _host(out)
+    del one, src
+    out_sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    want_dec = np.array([f(int(m)) for m in range(msg_mod)], np.uint64)[msgs]
+    for i in range(0, batch, 8192):
+        pts = H.lwe_decrypt_batch(got[i:i + 8192], out_sk)
+        with np.errstate(over="ignore"):
+            dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
+        assert np.array_equal(dec, want_dec[i:i + 8192]), f"decryption mismatch in rows {i}..{i + 8191}"
+    edges = [b for i in range(entries) for b in (i * batch // entries, (i + 1) * batch // entries - 1)]
+    idx = np.unique(np.concatenate([np.arange(0, batch, 1024), edges]))
+    want = oracle.NttContext(N).pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), 1, base_log, level,
+                                              threads=16)
+    assert np.array_equal(got[idx], want)

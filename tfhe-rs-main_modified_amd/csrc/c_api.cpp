@@ -5,6 +5,7 @@
 // a status code plus a thread-local message.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -210,17 +211,17 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
   return MI_OK;
 }
 
-// Ntt64::new's PLANS map (ntt64.rs:27-79): a read-locked probe, then one slot per key built under its
-// own once-flag so concurrent first users of one (n, p, device) build it once and other keys are not
-// blocked behind that build.
+// Ntt64::new's PLANS map (ntt64.rs:27-79): a read-locked probe, then one slot per key whose plan is built under
+// that slot's own mutex, so concurrent first users of one (n, p, device) build it once and other keys are not
+// blocked behind that build.  A failed build is not cached (the reference's map only ever holds built plans):
+// the slot stays empty and the next caller retries, so a transient failure (e.g. an OOM while uploading the
+// tables) does not make the key unusable for the rest of the process.
 int mi_ntt64_plan_cached(size_t n, uint64_t p, int device, const mi_ntt64_plan** out_plan) {
   if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
   *out_plan = nullptr;
   struct Slot {
-    std::once_flag once;
-    mi_ntt64_plan* plan = nullptr;
-    int status = MI_OK;
-    std::string error;
+    std::mutex build;
+    std::atomic<mi_ntt64_plan*> plan{nullptr};
   };
   static std::shared_mutex mu;
   static std::map<std::tuple<size_t, uint64_t, int>, std::unique_ptr<Slot>>* plans =
@@ -238,15 +239,18 @@ int mi_ntt64_plan_cached(size_t n, uint64_t p, int device, const mi_ntt64_plan**
     if (!ent) ent.reset(new Slot);
     slot = ent.get();
   }
-  std::call_once(slot->once, [&] {
-    slot->status = mi_ntt64_plan_create(n, p, device, &slot->plan);
-    if (slot->status == MI_OK)
-      slot->plan->cached = true;
-    else
-      slot->error = last_error();
-  });
-  if (slot->status != MI_OK) return fail(slot->status, slot->error);
-  *out_plan = slot->plan;
+  mi_ntt64_plan* built = slot->plan.load(std::memory_order_acquire);
+  if (!built) {
+    std::lock_guard<std::mutex> lk(slot->build);
+    built = slot->plan.load(std::memory_order_acquire);
+    if (!built) {
+      const int st = mi_ntt64_plan_create(n, p, device, &built);
+      if (st != MI_OK) return st;  // last_error() already holds the reason; nothing is cached
+      built->cached = true;
+      slot->plan.store(built, std::memory_order_release);
+    }
+  }
+  *out_plan = built;
   return MI_OK;
 }
 
@@ -328,18 +332,97 @@ int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan* plan, uint64_t* acc, cons
   return run_pw(2, plan, acc, lhs, rhs, batch, stride, stream);
 }
 
+// The `&mut [u64]` host form (Plan::fwd / Plan::inv on a caller slice, as Ntt64View::forward / add_backward call
+// it per polynomial, ntt64.rs:89-137).  Each call borrows a staging slot of the plan's device from a process-wide
+// pool: a private non-blocking stream, a device buffer and a pinned host buffer, all grown on demand and reused.
+// A call is memcpy -> async H2D -> transform -> async D2H -> wait on that stream only -> memcpy: no allocation in
+// the steady state, and nothing else of the process is synchronised (no hipDeviceSynchronize), so concurrent
+// callers (rayon workers) each run on their own slot and stream.
+}  // extern "C"
+
+namespace {
+struct HostSlot {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  u64* dbuf = nullptr;
+  u64* hbuf = nullptr;  // pinned
+  size_t cap = 0;       // u64 elements of both buffers
+};
+
+struct HostSlotPool {
+  std::mutex mu;
+  std::vector<HostSlot*> free;  // slots are never destroyed: the pool lives until process exit, as PLANS does
+};
+
+HostSlotPool& host_pool() {
+  static HostSlotPool* p = new HostSlotPool;
+  return *p;
+}
+
+HostSlot* acquire_slot(int device) {
+  HostSlotPool& pool = host_pool();
+  {
+    std::lock_guard<std::mutex> lk(pool.mu);
+    for (size_t i = 0; i < pool.free.size(); ++i)
+      if (pool.free[i]->device == device) {
+        HostSlot* s = pool.free[i];
+        pool.free[i] = pool.free.back();
+        pool.free.pop_back();
+        return s;
+      }
+  }
+  HostSlot* s = new (std::nothrow) HostSlot;
+  if (!s) return nullptr;
+  s->device = device;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void release_slot(HostSlot* s) {
+  HostSlotPool& pool = host_pool();
+  std::lock_guard<std::mutex> lk(pool.mu);
+  pool.free.push_back(s);
+}
+
+hipError_t slot_reserve(HostSlot* s, size_t elems) {
+  if (elems <= s->cap) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(s->stream);
+  if (s->dbuf) (void)hipFree(s->dbuf);
+  if (s->hbuf) (void)hipHostFree(s->hbuf);
+  s->dbuf = s->hbuf = nullptr;
+  s->cap = 0;
+  if (e == hipSuccess) e = hipMalloc(&s->dbuf, elems * sizeof(u64));
+  if (e == hipSuccess) e = hipHostMalloc(&s->hbuf, elems * sizeof(u64), hipHostMallocDefault);
+  if (e == hipSuccess) s->cap = elems;
+  return e;
+}
+}  // namespace
+
+extern "C" {
+
 static int run_host(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch) {
   int st = check_batch(plan, buf, batch, plan ? plan->n : 0);
   if (st != MI_OK || batch == 0) return st;
   DeviceGuard g(plan->device);
-  const size_t bytes = batch * plan->n * sizeof(u64);
-  u64* d = nullptr;
-  if (hipMalloc(&d, bytes) != hipSuccess) return fail(MI_ERR_OOM, "device buffer allocation failed");
-  hipError_t e = hipMemcpy(d, buf, bytes, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = launch_transform(fwd, plan, d, batch, plan->n, nullptr);
-  if (e == hipSuccess) e = hipMemcpy(buf, d, bytes, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  (void)hipFree(d);
+  if (!g.ok) return fail(MI_ERR_HIP, "hipSetDevice failed");
+  HostSlot* slot = acquire_slot(plan->device);
+  if (!slot) return fail(MI_ERR_HIP, "staging stream creation failed");
+  const size_t elems = batch * plan->n, bytes = elems * sizeof(u64);
+  hipError_t e = slot_reserve(slot, elems);
+  if (e != hipSuccess) {
+    release_slot(slot);
+    return fail(MI_ERR_OOM, std::string("staging buffer allocation failed: ") + hipGetErrorString(e));
+  }
+  std::memcpy(slot->hbuf, buf, bytes);
+  e = hipMemcpyAsync(slot->dbuf, slot->hbuf, bytes, hipMemcpyHostToDevice, slot->stream);
+  if (e == hipSuccess) e = launch_transform(fwd, plan, slot->dbuf, batch, plan->n, slot->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(slot->hbuf, slot->dbuf, bytes, hipMemcpyDeviceToHost, slot->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(slot->stream);
+  if (e == hipSuccess) std::memcpy(buf, slot->hbuf, bytes);
+  release_slot(slot);
   return e == hipSuccess ? MI_OK : hip_fail(e, "host transform");
 }
 

@@ -210,23 +210,37 @@ int mi_multi_gpu_gather(mi_multi_gpu* m, void* dst, const void* const* srcs, siz
 }
 
 // The CUDA backend's multi-GPU bootstrap pattern: scatter the LWE batch from devices[0], one PBS launch per
-// device with that device's key and LUT copy, gather the outputs back.  keys[i] / luts[i] live on
-// devices[i]; lwe_in / lwe_out on devices[0]; `stream` (devices[0]) is ordered before and after.  Shard 0
-// runs in place on the caller's buffers; the other shards use stream-ordered scratch on their device.
-int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,
-                           const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode, void* stream) {
+// active device with that device's key and LUT copy, gather the outputs back.  Only the first
+// get_active_gpu_count(batch, G) entries take part (helper_multi_gpu.cu:42-49, CudaStreams::active_gpu_subset,
+// helper_multi_gpu.h:74-79): a batch of 13 on 8 entries runs on 2 devices (7 + 6), and the keys / LUTs of the
+// inactive entries are not read.  keys[i] / luts[i] live on devices[i]; lwe_in / lwe_out on devices[0].
+//
+// Ordering: `stream` (devices[0]) is ordered before the whole call and after it.  producer_streams[i] (a stream of
+// devices[i], NULL entry or NULL array = that device's legacy null stream) is the stream that produced luts[i] /
+// keys[i]: shard i starts after the work queued on it so far, and it is ordered after shard i's last use of them,
+// so the caller's allocator may free or reuse them on that stream as soon as the call returns.  Shard 0 runs in
+// place on `stream`; the other shards use stream-ordered scratch on their device.
+int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,
+                                   const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode,
+                                   void* stream, void* const* producer_streams) {
   if (!m || !keys || !luts) return fail(MI_ERR_INVALID_ARG, "NULL argument");
   if (batch == 0) return MI_OK;
   if (!lwe_out || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
-  const size_t G = m->devices.size();
+  if (batch > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  uint32_t active = 0;
+  mi_multi_gpu_active_count((uint32_t)batch, (uint32_t)m->devices.size(), &active);
+  const size_t G = active;
   for (size_t i = 0; i < G; ++i) {
-    if (!keys[i] || !luts[i]) return fail(MI_ERR_INVALID_ARG, "key / lut is NULL");
+    if (!keys[i] || !luts[i]) return fail(MI_ERR_INVALID_ARG, "key / lut of an active entry is NULL");
     if (keys[i]->plan->device != m->devices[i]) return fail(MI_ERR_INVALID_ARG, "keys[i] is not on devices[i]");
     if (keys[i]->n_lwe != keys[0]->n_lwe || keys[i]->k != keys[0]->k || keys[i]->variant != keys[0]->variant ||
         keys[i]->plan->n != keys[0]->plan->n)
       return fail(MI_ERR_INVALID_ARG, "keys differ in shape");
   }
   const size_t in_w = keys[0]->n_lwe + 1, out_w = (size_t)keys[0]->k * keys[0]->plan->n + 1;
+  auto producer = [&](size_t i) -> hipStream_t {
+    return producer_streams ? (hipStream_t)producer_streams[i] : nullptr;
+  };
   std::vector<uint64_t*> ins(G, nullptr), outs(G, nullptr), scratch(G, nullptr);
   int st = MI_OK;
   for (size_t i = 0; i < G && st == MI_OK; ++i) {
@@ -238,13 +252,35 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys,
       continue;
     }
     DeviceGuard g(m->devices[i]);
+    // shard i's work on the set's stream follows its producer stream (the key / LUT of devices[i])
+    hipError_t e = after(m->streams[i], producer(i), m->events[i], m->devices[i]);
+    if (e != hipSuccess) {
+      st = hip_fail(e, "producer-stream ordering");
+      break;
+    }
     uint64_t* buf = nullptr;
     if (hipMallocAsync((void**)&buf, n * (in_w + out_w) * sizeof(uint64_t), m->streams[i]) != hipSuccess)
       st = fail(MI_ERR_OOM, "shard scratch allocation failed");
     scratch[i] = ins[i] = buf;
     outs[i] = buf ? buf + n * in_w : nullptr;
   }
-  if (st == MI_OK) st = mi_multi_gpu_scatter(m, lwe_in, (void* const*)ins.data(), batch, in_w * 8, stream);
+  // shard 0 follows its producer stream too, when that is not the caller's stream itself
+  if (st == MI_OK && producer(0) != (hipStream_t)stream) {
+    hipError_t e = after((hipStream_t)stream, producer(0), m->events[0], m->devices[0]);
+    if (e != hipSuccess) st = hip_fail(e, "producer-stream ordering");
+  }
+  // scatter / gather over the active prefix of the set only
+  std::vector<void*> dsts(m->devices.size(), nullptr);
+  std::vector<const void*> srcs(m->devices.size(), nullptr);
+  for (size_t i = 0; i < G; ++i) {
+    dsts[i] = ins[i];
+    srcs[i] = outs[i];
+  }
+  mi_multi_gpu sub;
+  sub.devices.assign(m->devices.begin(), m->devices.begin() + G);
+  sub.streams.assign(m->streams.begin(), m->streams.begin() + G);
+  sub.events.assign(m->events.begin(), m->events.begin() + G);
+  if (st == MI_OK) st = mi_multi_gpu_scatter(&sub, lwe_in, dsts.data(), batch, in_w * 8, stream);
   // shard 0 runs on the caller's stream directly; the others on their device streams
   for (size_t i = 0; i < G && st == MI_OK; ++i) {
     size_t off = 0, n = 0;
@@ -252,13 +288,25 @@ int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys,
     if (n == 0) continue;
     st = mi_pbs_ntt64_batch(keys[i], outs[i], ins[i], luts[i], n, ms_mode, i == 0 ? stream : m->streams[i]);
   }
-  if (st == MI_OK) st = mi_multi_gpu_gather(m, lwe_out, (const void* const*)outs.data(), batch, out_w * 8, stream);
+  if (st == MI_OK) st = mi_multi_gpu_gather(&sub, lwe_out, srcs.data(), batch, out_w * 8, stream);
   for (size_t i = 1; i < G; ++i)
     if (scratch[i]) {
       DeviceGuard g(m->devices[i]);
       (void)hipFreeAsync(scratch[i], m->streams[i]);
     }
+  // the producer streams follow the last use of their key / LUT (shard 0's is `stream`, which the gather ordered)
+  for (size_t i = 0; i < G && st == MI_OK; ++i) {
+    hipStream_t ps = producer(i);
+    if (i == 0 && ps == (hipStream_t)stream) continue;
+    hipError_t e = after(ps, i == 0 ? (hipStream_t)stream : m->streams[i], m->events[i], m->devices[i]);
+    if (e != hipSuccess) st = hip_fail(e, "producer-stream ordering");
+  }
   return st;
+}
+
+int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,
+                           const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode, void* stream) {
+  return mi_pbs_ntt64_multi_gpu_ordered(m, keys, lwe_out, lwe_in, luts, batch, ms_mode, stream, nullptr);
 }
 
 }  // extern "C"

@@ -10,7 +10,7 @@ namespace mi {
 //   t1  [16][64]  w^j omega^(j k1), w = exp(i pi / 2M), omega = exp(-2 pi i / M), M = 1024
 //   t2  [3][16]   W64^(jl q1) = exp(-2 pi i jl q1 / 64), q1 = 1..3
 //   cm  [16]      exp(i pi m / 32)
-//   cmi [16]      exp(-i pi m / 32) 2^64 / M
+//   cmi [16]      exp(-i pi m / 32) / M  (torus units; the API backward applies the 2^64)
 struct FftTables {
   const double* t1;
   const double* t2;

@@ -172,23 +172,40 @@ class DeviceSet:
         check(lib().mi_multi_gpu_gather(self._h, ctypes.c_void_p(dst.data_ptr()), self._ptrs(srcs), dst.shape[0],
                                         unit, self._stream(dst)))
 
+    def active_count(self, batch: int) -> int:
+        """How many leading entries a batch of ``batch`` bootstraps runs on (``get_active_gpu_count``)."""
+        return lib_active_count(batch, len(self.devices))
+
     def programmable_bootstrap(self, keys, lwe_in, lwe_out, luts, ms_mode: int = 0):
-        """Batched PBS over the set (``mi_pbs_ntt64_multi_gpu``): ``keys[i]`` / ``luts[i]`` on ``devices[i]``,
-        ``lwe_in`` / ``lwe_out`` on ``devices[0]``; results land in ``lwe_out`` as one launch would."""
+        """Batched PBS over the set (``mi_pbs_ntt64_multi_gpu_ordered``): ``keys[i]`` / ``luts[i]`` on
+        ``devices[i]``, ``lwe_in`` / ``lwe_out`` on ``devices[0]``; results land in ``lwe_out`` as one launch
+        would.  Only the first ``active_count(batch)`` entries run (their keys / LUTs are the only ones read;
+        the others may be None).  Each device's current torch stream is passed as the producer of its key and
+        LUT: shard i starts after it, and it waits for shard i's last read, so torch's caching allocator may
+        reuse a LUT's memory on that stream as soon as this returns (no ``record_stream`` needed)."""
         import ctypes
+
+        import torch
 
         from ._lib import check, lib
         if len(keys) != len(self.devices) or len(luts) != len(self.devices):
-            raise ValueError("one key and one LUT per device of the set")
+            raise ValueError("one key (or None) and one LUT (or None) per device of the set")
         k0 = keys[0]
         n_in, n_out = k0.input_lwe_dimension + 1, k0.output_lwe_size()
         batch = lwe_in.numel() // n_in
         if lwe_in.shape[-1] != n_in or lwe_out.shape[-1] != n_out or lwe_out.numel() // n_out != batch:
             raise ValueError("assertion failed: lwe shapes do not match the key")
-        kp = (ctypes.c_void_p * len(keys))(*[k._h.value for k in keys])
-        check(lib().mi_pbs_ntt64_multi_gpu(self._h, kp, ctypes.c_void_p(lwe_out.data_ptr()),
-                                           ctypes.c_void_p(lwe_in.data_ptr()), self._ptrs(luts), batch, ms_mode,
-                                           self._stream(lwe_out)))
+        active = self.active_count(batch) if batch else 0
+        for i in range(active):
+            if keys[i] is None or luts[i] is None:
+                raise ValueError(f"entry {i} is active for a batch of {batch}: it needs a key and a LUT")
+        kp = (ctypes.c_void_p * len(keys))(*[k._h.value if k is not None else None for k in keys])
+        lp = (ctypes.c_void_p * len(luts))(*[t.data_ptr() if t is not None else None for t in luts])
+        prod = (ctypes.c_void_p * len(self.devices))(
+            *[torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream for d in self.devices])
+        check(lib().mi_pbs_ntt64_multi_gpu_ordered(self._h, kp, ctypes.c_void_p(lwe_out.data_ptr()),
+                                                   ctypes.c_void_p(lwe_in.data_ptr()), lp, batch, ms_mode,
+                                                   self._stream(lwe_out), prod))
 
 
 def lib_shard(total: int, index: int, count: int):

@@ -5,7 +5,8 @@ Costs are the MI355X measurements of tools/valu_probe.hip (cycles per wave-instr
 8 waves/SIMD of independent instructions).  The model is what bench.py's
 "valu_bound" reports against: cycles per polynomial pass (transform) or per CMUX step (PBS body).
 
-  python tools/valu_cost.py        -> JSON {"fwd": cycles, "inv": cycles, "pbs_step": cycles}
+  python tools/valu_cost.py        -> JSON {"fwd", "inv": cycles per polynomial pass; "pbs_step", "pbs_sol_step": per wave
+                                      per CMUX step; "ext_bnf": per wave per external product}
 """
 import json
 import os
@@ -20,7 +21,7 @@ COST = {  # cycles per wave-instruction (tools/valu_probe.hip on MI355X)
     "v_add3_u32": 4.26, "v_alignbit_b32": 4.30, "v_cndmask_b32_e64": 4.31, "v_mad_u64_u32": 4.56,
     "v_mad_i64_i32": 4.56, "v_lshl_add_u64": 4.22, "v_mov_b64": 4.21, "v_lshrrev_b64": 4.24,
     "v_lshlrev_b64": 4.24, "v_mul_hi_u32": 4.29, "v_mul_lo_u32": 4.31, "v_mul_u32_u24": 4.27,
-    "v_bfe_u32": 4.28, "v_bfe_i32": 4.28, "v_cmp_eq_u32_e64": 4.52, "v_bfi_b32": 4.28, "v_perm_b32": 4.27, "v_cmp_le_u32_e64": 4.52,
+    "v_bfe_u32": 4.28, "v_bfe_i32": 4.28, "v_cmp_eq_u32_e64": 4.52, "v_cmp_ge_u64_e64": 4.56, "v_bfi_b32": 4.28, "v_perm_b32": 4.27, "v_cmp_le_u32_e64": 4.52,
     "v_add_co_u32_e64": 4.56, "v_addc_co_u32_e64": 4.57, "v_sub_co_u32_e64": 4.57, "v_subb_co_u32_e64": 4.57,
     "v_mov_b32_dpp": 4.3,
 }
@@ -50,11 +51,12 @@ def main():
         out[name + "_valu"] = body.nvalu
         if unk:
             out[name + "_unpriced"] = unk
-    b = P.gen_pbs(tabs)
-    out["pbs_step"], unk = cycles(b.lines)
-    out["pbs_step_valu"] = b.nvalu
-    if unk:
-        out["pbs_step_unpriced"] = unk
+    for name, body in (("pbs_step", P.gen_pbs(tabs)), ("pbs_sol_step", P.gen_pbs(tabs, sol=True)),
+                       ("ext_bnf", P.gen_ext(tabs, False))):
+        out[name], unk = cycles(body.lines)
+        out[name + "_valu"] = body.nvalu
+        if unk:
+            out[name + "_unpriced"] = unk
     print(json.dumps({k: (round(v, 1) if isinstance(v, float) else v) for k, v in out.items()}))
 
 
