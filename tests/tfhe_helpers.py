@@ -203,3 +203,59 @@ def bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, noise_log2):
     bsk[:, 0, :, 0] = masks.reshape(n_lwe, 2, n)
     bsk[:, 0, :, 1] = body
     return bsk
+
+
+def polymul_binary_fast(oracle, a, s, q=0, threads=16):
+    """(a * s) mod (X^N + 1) for every polynomial of `a` (..., N) and one binary polynomial s (N,), coefficients
+    mod q (q = 0: mod 2^64), through the oracle's Solinas-prime transform (test infrastructure: the large-N key
+    generation of the shape tests).  q = p: one exact product mod p.  Native: a = sum_t a_t 2^(16 t) with 16-bit limbs
+    a_t, each limb product's coefficients are in (-N 2^16, N 2^16), far inside (-p/2, p/2), so the prime product
+    lifted to a signed integer is exact; the limbs recombine mod 2^64."""
+    P = 0xFFFFFFFF00000001
+    n = a.shape[-1]
+    plan = oracle.Plan.try_new(n, P)
+    flat = np.ascontiguousarray(a.reshape(-1, n), dtype=np.uint64)
+    s_hat = np.broadcast_to(plan.fwd(np.asarray(s, dtype=np.uint64)), flat.shape).copy()
+
+    def prime_product(x):
+        return plan.inv(plan.mul_assign_normalize(plan.fwd(x, threads=threads), s_hat), threads=threads)
+
+    if q:
+        assert q == P
+        return prime_product(flat).reshape(a.shape)
+    out = np.zeros_like(flat)
+    with np.errstate(over="ignore"):
+        for t in range(4):
+            v = prime_product((flat >> np.uint64(16 * t)) & np.uint64(0xFFFF))
+            v = np.where(v > np.uint64(P // 2), v - np.uint64(P), v)  # signed lift, as u64 mod 2^64
+            out += v << np.uint64(16 * t)
+    return out.reshape(a.shape)
+
+
+def bsk_gen_fast(g, oracle, lwe_sk, glwe_sk, base_log, level, noise_log2, q=0):
+    """Standard-domain bootstrap key (n_lwe, level, k+1, k+1, N) with the semantics of ggsw_encrypt / bsk_gen
+    (ggsw_encryption.rs:20-45, 318-375; highest level first), every mask product computed in one batched pass
+    (polymul_binary_fast) so N = 8192 / 65536 keys generate in seconds.  Test infrastructure only."""
+    n_lwe = lwe_sk.size
+    k, n = glwe_sk.shape
+    mod = q if q else 2**64
+    masks = uniform_q(g, (n_lwe, level, k + 1, k, n), q)
+    body = noise_q(g, (n_lwe, level, k + 1, n), noise_log2, q)
+    for i in range(k):
+        body = add_q(body, polymul_binary_fast(oracle, np.ascontiguousarray(masks[..., i, :]), glwe_sk[i], q), q)
+    for b in range(n_lwe):
+        for li in range(level):
+            j = level - li
+            factor = (-(int(lwe_sk[b])) * (1 << (64 - base_log * j))) % mod
+            for r in range(k + 1):
+                if r < k:
+                    pt = np.array([(int(v) * factor) % mod for v in glwe_sk[r]], dtype=np.uint64) if factor else \
+                        np.zeros(n, np.uint64)
+                else:
+                    pt = np.zeros(n, np.uint64)
+                    pt[0] = np.uint64((-factor) % mod)
+                body[b, li, r] = add_q(body[b, li, r], pt, q)
+    bsk = np.zeros((n_lwe, level, k + 1, k + 1, n), np.uint64)
+    bsk[..., :k, :] = masks
+    bsk[..., k, :] = body
+    return bsk

@@ -447,8 +447,15 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   if (variant != MI_NTT64_SOLINAS && variant != MI_NTT64_BNF) return fail(MI_ERR_INVALID_ARG, "unknown variant");
   if (level < 1 || base_log < 1 || base_log * level > 63)
     return fail(MI_ERR_INVALID_ARG, "decomposition must satisfy level >= 1, base_log >= 1, base_log*level < 64");
-  if (!plan->goldilocks || plan->logn < 10 || plan->logn > 12 || k < 1 || k > 2)
-    return fail(MI_ERR_UNSUPPORTED, "external product / PBS run for the Solinas plan at N in {1024, 2048, 4096}, k in {1, 2}");
+  // the compiled shapes (pbs_kernels.hip): N in {1024, 2048, 4096} with k in {1, 2}, N = 512 with k in {1, 4}
+  // (PARAM_MESSAGE_1_CARRY_1), N = 8192 with k = 1 (PARAM_MESSAGE_3_CARRY_3)
+  const int ln = plan->logn;
+  const bool shape_ok = plan->goldilocks && ((ln >= 10 && ln <= 12 && (k == 1 || k == 2)) ||
+                                             (ln == 9 && (k == 1 || k == 4)) || (ln == 13 && k == 1));
+  if (!shape_ok)
+    return fail(MI_ERR_UNSUPPORTED,
+                "external product / PBS run for the Solinas plan at N in {1024, 2048, 4096} with k in {1, 2}, "
+                "N = 512 with k in {1, 4}, N = 8192 with k = 1");
   return MI_OK;
 }
 
@@ -467,8 +474,8 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
   if (n_polys == 0) return MI_OK;
   if (!bsk_std || !bsk_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (in_modulus_width > 64) return fail(MI_ERR_INVALID_ARG, "in_modulus_width > 64");
-  if (!plan->goldilocks || plan->logn < 10 || plan->logn > 12)
-    return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {1024, 2048, 4096}");
+  if (!plan->goldilocks || plan->logn < 9 || plan->logn > 13)
+    return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {512, ..., 8192}");
   if (n_polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "too many polynomials");
   DeviceGuard g(plan->device);
   if (plan->twisted && in_modulus_width == 64) {  // the fused twisted-body conversion (ntt64_tw.hip)

@@ -30,10 +30,16 @@ namespace mi {
 namespace pbs {
 
 static constexpr u64 P = GL_P;
-static constexpr int LOGE = 3;  // 8 coefficients per lane
 
-template <int LOGN>
+// Coefficients per lane: 8, or 4 for the wide GLWEs (k >= 3, e.g. N = 512, k = 4 of PARAM_MESSAGE_1_CARRY_1,
+// shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/ks_pbs.rs:8-27), whose (k + 1) polynomials of
+// accumulator, digits and products must stay in the registers of one lane.
+template <int K>
+constexpr int loge_for() { return K >= 3 ? 2 : 3; }
+
+template <int LOGN, int K>
 struct Shape {
+  static constexpr int LOGE = loge_for<K>();
   using G = Geo<LOGN, LOGE>;
   static constexpr int N = G::N;
   static constexpr int T = G::T;  // lanes per polynomial = workgroup size
@@ -117,12 +123,12 @@ __device__ __forceinline__ u64 neg_q(u64 a) { return BNF ? (u64)0 - a : neg_cust
 // domain, highest level first; row r = the decomposition of GLWE polynomial r); BNF keys are expected
 // pre-normalised unless `normalize`.  The decomposition levels are a runtime loop.
 template <int LOGN, int K, bool BNF>
-__device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<LOGN>::E],
-                                                 u64 (&y)[K + 1][Shape<LOGN>::E], const u64* __restrict__ ggsw,
+__device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<LOGN, K>::E],
+                                                 u64 (&y)[K + 1][Shape<LOGN, K>::E], const u64* __restrict__ ggsw,
                                                  int base_log, int level, int t, u64* sh,
                                                  const u64* __restrict__ tw, const u64* __restrict__ itw,
                                                  bool normalize, u64 n_inv) {
-  using S = Shape<LOGN>;
+  using S = Shape<LOGN, K>;
   using G = typename S::G;
   constexpr int E = S::E, N = S::N;
   const Goldilocks gl;
@@ -202,14 +208,14 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
 // EXT : out[b] += GGSW (.) glwe[b]                          (add_external_product_ntt64[_bnf]_assign)
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
 template <int LOGN, int K, bool BNF, bool CMUX>
-__global__ __launch_bounds__(Shape<LOGN>::T) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                                      const u64* __restrict__ ggsw_list, uint32_t batch,
                                                                      int base_log, int level,
                                                                      const u64* __restrict__ tw,
                                                                      const u64* __restrict__ itw, u64 n_inv,
                                                                      const uint32_t* __restrict__ gidx,
                                                                      uint32_t n_ggsw) {
-  using S = Shape<LOGN>;
+  using S = Shape<LOGN, K>;
   using G = typename S::G;
   constexpr int E = S::E, N = S::N;
   __shared__ u64 sh[(K + 1) * G::PADDED];
@@ -280,12 +286,12 @@ __device__ u64 centered_body_correction(const u64* __restrict__ lwe, uint32_t n_
 // lwe_in: batch x (n+1); lut: (K+1) x N shared; bsk: n x level x (K+1) x (K+1) x N (BNF: pre-normalised
 // copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
 template <int LOGN, int K, bool BNF>
-__global__ __launch_bounds__(Shape<LOGN>::T) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                                              const u64* __restrict__ lut, const u64* __restrict__ bsk,
                                                              uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                              const u64* __restrict__ tw, const u64* __restrict__ itw,
                                                              int centered) {
-  using S = Shape<LOGN>;
+  using S = Shape<LOGN, K>;
   using G = typename S::G;
   constexpr int E = S::E, N = S::N, T = S::T;
   __shared__ u64 sh[(K + 1) * G::PADDED];
@@ -395,10 +401,10 @@ __global__ __launch_bounds__(Shape<LOGN>::T) void pbs_kernel(u64* __restrict__ l
 // ---- key conversion (lwe_bootstrap_key_conversion.rs:294-365) + normalisation ---------------------
 // bsk_ntt[pi] = fwd(modswitch_{2^w -> p}(bsk_std[pi])) [* N^-1]; also used to prepare the BNF copy.
 template <int LOGN>
-__global__ __launch_bounds__(Shape<LOGN>::T) void bsk_to_ntt_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
+__global__ __launch_bounds__((Shape<LOGN, 1>::T)) void bsk_to_ntt_kernel(u64* __restrict__ dst, const u64* __restrict__ src,
                                                                     uint64_t n_polys, unsigned in_width, int normalize,
                                                                     u64 n_inv, const u64* __restrict__ tw) {
-  using S = Shape<LOGN>;
+  using S = Shape<LOGN, 1>;
   using G = typename S::G;
   constexpr int E = S::E, N = S::N;
   __shared__ u64 sh[G::PADDED];
@@ -447,7 +453,9 @@ __global__ __launch_bounds__(256) void lift_switched_kernel(u64* __restrict__ ds
 }  // namespace pbs
 
 // ---- dispatch ------------------------------------------------------------------------------------
-// Shapes compiled: N = 2^LOGN for LOGN in {10, 11, 12}, K in {1, 2}; callers validate (c_api.cpp).
+// Shapes compiled (callers validate, c_api.cpp mi::capi::check_pbs_shape): N = 1024 / 2048 / 4096 with K in {1, 2};
+// N = 512 with K in {1, 4} (PARAM_MESSAGE_1_CARRY_1); N = 8192 with K = 1 (PARAM_MESSAGE_3_CARRY_3).  N = 65536
+// (PARAM_MESSAGE_4_CARRY_4) runs the multi-workgroup blind rotation of pbs_large.hip.
 
 hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s) {
   if (count == 0) return hipSuccess;
@@ -461,7 +469,7 @@ hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count
 template <int LOGN>
 static hipError_t bsk_launch(uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width, int normalize,
                              uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
-  hipLaunchKernelGGL((pbs::bsk_to_ntt_kernel<LOGN>), dim3((unsigned)n_polys), dim3(pbs::Shape<LOGN>::T), 0, s, dst, src,
+  hipLaunchKernelGGL((pbs::bsk_to_ntt_kernel<LOGN>), dim3((unsigned)n_polys), dim3(pbs::Shape<LOGN, 1>::T), 0, s, dst, src,
                      (uint64_t)n_polys, in_width, normalize, n_inv, tw);
   return hipGetLastError();
 }
@@ -470,9 +478,11 @@ hipError_t launch_bsk_to_ntt(int logn, uint64_t* dst, const uint64_t* src, size_
                              int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
   if (n_polys == 0) return hipSuccess;
   switch (logn) {
+    case 9: return bsk_launch<9>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
     case 10: return bsk_launch<10>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
     case 11: return bsk_launch<11>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
     case 12: return bsk_launch<12>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
+    case 13: return bsk_launch<13>(dst, src, n_polys, in_width, normalize, n_inv, tw, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -489,7 +499,7 @@ template <int LOGN, int K, bool BNF, bool CMUX>
 static hipError_t ext_launch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                              int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s,
                              const uint32_t* gidx, uint32_t n_ggsw) {
-  hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX>), dim3((unsigned)batch), dim3(pbs::Shape<LOGN>::T), 0,
+  hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX>), dim3((unsigned)batch), dim3(pbs::Shape<LOGN, K>::T), 0,
                      s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw, n_inv, gidx, n_ggsw);
   return hipGetLastError();
 }
@@ -513,8 +523,8 @@ hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, u
 #define MI_EXT_SHAPE(L, KK)                                                                      \
   if (logn == L && k == KK)                                                                      \
     return ext_shape<L, KK>(bnf, cmux, level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gidx, n_ggsw);
-  MI_EXT_SHAPE(10, 1) MI_EXT_SHAPE(10, 2) MI_EXT_SHAPE(11, 1) MI_EXT_SHAPE(11, 2) MI_EXT_SHAPE(12, 1)
-  MI_EXT_SHAPE(12, 2)
+  MI_EXT_SHAPE(9, 1) MI_EXT_SHAPE(9, 4) MI_EXT_SHAPE(10, 1) MI_EXT_SHAPE(10, 2) MI_EXT_SHAPE(11, 1) MI_EXT_SHAPE(11, 2)
+  MI_EXT_SHAPE(12, 1) MI_EXT_SHAPE(12, 2) MI_EXT_SHAPE(13, 1)
 #undef MI_EXT_SHAPE
   return hipErrorInvalidValue;
 }
@@ -523,7 +533,7 @@ template <int LOGN, int K>
 static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                             const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                             const uint64_t* itw, int centered, hipStream_t s) {
-  const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN>::T);
+  const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN, K>::T);
   if (bnf)
     hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, true>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe,
                        (uint32_t)batch, base_log, level, tw, itw, centered);
@@ -540,8 +550,8 @@ hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const
 #define MI_PBS_SHAPE(L, KK)                                                                                     \
   if (logn == L && k == KK)                                                                                     \
     return pbs_shape<L, KK>(bnf, level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s);
-  MI_PBS_SHAPE(10, 1) MI_PBS_SHAPE(10, 2) MI_PBS_SHAPE(11, 1) MI_PBS_SHAPE(11, 2) MI_PBS_SHAPE(12, 1)
-  MI_PBS_SHAPE(12, 2)
+  MI_PBS_SHAPE(9, 1) MI_PBS_SHAPE(9, 4) MI_PBS_SHAPE(10, 1) MI_PBS_SHAPE(10, 2) MI_PBS_SHAPE(11, 1) MI_PBS_SHAPE(11, 2)
+  MI_PBS_SHAPE(12, 1) MI_PBS_SHAPE(12, 2) MI_PBS_SHAPE(13, 1)
 #undef MI_PBS_SHAPE
   return hipErrorInvalidValue;
 }
