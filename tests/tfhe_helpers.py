@@ -208,9 +208,9 @@ def bsk_gen_native_l1(g, lwe_sk, glwe_sk, base_log, noise_log2):
 def polymul_binary_fast(oracle, a, s, q=0, threads=16):
     """(a * s) mod (X^N + 1) for every polynomial of `a` (..., N) and one binary polynomial s (N,), coefficients
     mod q (q = 0: mod 2^64), through the oracle's Solinas-prime transform (test infrastructure: the large-N key
-    generation of the shape tests).  q = p: one exact product mod p.  Native: a = sum_t a_t 2^(16 t) with 16-bit limbs
-    a_t, each limb product's coefficients are in (-N 2^16, N 2^16), far inside (-p/2, p/2), so the prime product
-    lifted to a signed integer is exact; the limbs recombine mod 2^64."""
+    generation of the shape tests).  q = p: one exact product mod p.  Native: a = a_0 + a_1 2^32 with 32-bit limbs;
+    each limb product's coefficients are in (-N 2^32, N 2^32), inside (-p/2, p/2) for N <= 2^30, so the prime
+    product lifted to a signed integer is exact; the limbs recombine mod 2^64."""
     P = 0xFFFFFFFF00000001
     n = a.shape[-1]
     plan = oracle.Plan.try_new(n, P)
@@ -225,10 +225,10 @@ def polymul_binary_fast(oracle, a, s, q=0, threads=16):
         return prime_product(flat).reshape(a.shape)
     out = np.zeros_like(flat)
     with np.errstate(over="ignore"):
-        for t in range(4):
-            v = prime_product((flat >> np.uint64(16 * t)) & np.uint64(0xFFFF))
+        for t in range(2):
+            v = prime_product((flat >> np.uint64(32 * t)) & np.uint64(0xFFFFFFFF))
             v = np.where(v > np.uint64(P // 2), v - np.uint64(P), v)  # signed lift, as u64 mod 2^64
-            out += v << np.uint64(16 * t)
+            out += v << np.uint64(32 * t)
     return out.reshape(a.shape)
 
 
@@ -243,18 +243,17 @@ def bsk_gen_fast(g, oracle, lwe_sk, glwe_sk, base_log, level, noise_log2, q=0):
     body = noise_q(g, (n_lwe, level, k + 1, n), noise_log2, q)
     for i in range(k):
         body = add_q(body, polymul_binary_fast(oracle, np.ascontiguousarray(masks[..., i, :]), glwe_sk[i], q), q)
-    for b in range(n_lwe):
-        for li in range(level):
-            j = level - li
-            factor = (-(int(lwe_sk[b])) * (1 << (64 - base_log * j))) % mod
-            for r in range(k + 1):
-                if r < k:
-                    pt = np.array([(int(v) * factor) % mod for v in glwe_sk[r]], dtype=np.uint64) if factor else \
-                        np.zeros(n, np.uint64)
-                else:
-                    pt = np.zeros(n, np.uint64)
-                    pt[0] = np.uint64((-factor) % mod)
-                body[b, li, r] = add_q(body[b, li, r], pt, q)
+    # plaintexts: factor = -b 2^(64 - B j) (mod q); row r < k: s_r * factor (s_r binary: factor where s_r = 1),
+    # row k: -factor at X^0
+    for li in range(level):
+        j = level - li
+        f1 = (-(1 << (64 - base_log * j))) % mod                       # the factor of a key bit b = 1
+        fac = np.where(lwe_sk.astype(bool), np.uint64(f1), np.uint64(0))  # (n_lwe,)
+        for r in range(k):
+            pt = np.where(glwe_sk[r].astype(bool)[None, :], fac[:, None], np.uint64(0))
+            body[:, li, r] = add_q(body[:, li, r], pt, q)
+        nf = np.where(lwe_sk.astype(bool), np.uint64((-f1) % mod), np.uint64(0))
+        body[:, li, k, 0] = add_q(body[:, li, k, 0], nf, q)
     bsk = np.zeros((n_lwe, level, k + 1, k + 1, n), np.uint64)
     bsk[..., :k, :] = masks
     bsk[..., k, :] = body

@@ -450,12 +450,15 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   // the compiled shapes (pbs_kernels.hip): N in {1024, 2048, 4096} with k in {1, 2}, N = 512 with k in {1, 4}
   // (PARAM_MESSAGE_1_CARRY_1), N = 8192 with k = 1 (PARAM_MESSAGE_3_CARRY_3)
   const int ln = plan->logn;
+  // (PARAM_MESSAGE_1_CARRY_1), N = 8192 with k = 1 (PARAM_MESSAGE_3_CARRY_3); and N = 2^14 ... 2^17 with k in
+  // {1, 2} on the multi-kernel path of pbs_large.hip (PARAM_MESSAGE_4_CARRY_4: N = 65536)
   const bool shape_ok = plan->goldilocks && ((ln >= 10 && ln <= 12 && (k == 1 || k == 2)) ||
-                                             (ln == 9 && (k == 1 || k == 4)) || (ln == 13 && k == 1));
+                                             (ln == 9 && (k == 1 || k == 4)) || (ln == 13 && k == 1) ||
+                                             (ln >= 14 && ln <= 17 && (k == 1 || k == 2)));
   if (!shape_ok)
     return fail(MI_ERR_UNSUPPORTED,
                 "external product / PBS run for the Solinas plan at N in {1024, 2048, 4096} with k in {1, 2}, "
-                "N = 512 with k in {1, 4}, N = 8192 with k = 1");
+                "N = 512 with k in {1, 4}, N = 8192 with k = 1, N in {16384, ..., 131072} with k in {1, 2}");
   return MI_OK;
 }
 
@@ -474,8 +477,8 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
   if (n_polys == 0) return MI_OK;
   if (!bsk_std || !bsk_ntt) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (in_modulus_width > 64) return fail(MI_ERR_INVALID_ARG, "in_modulus_width > 64");
-  if (!plan->goldilocks || plan->logn < 9 || plan->logn > 13)
-    return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {512, ..., 8192}");
+  if (!plan->goldilocks || plan->logn < 9 || plan->logn > 17)
+    return fail(MI_ERR_UNSUPPORTED, "key conversion runs for the Solinas plan at N in {512, ..., 131072}");
   if (n_polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "too many polynomials");
   DeviceGuard g(plan->device);
   if (plan->twisted && in_modulus_width == 64) {  // the fused twisted-body conversion (ntt64_tw.hip)
@@ -483,8 +486,11 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
                                           (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
   }
-  hipError_t e = mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0, plan->n_inv,
-                                       plan->d_twid, (hipStream_t)stream);
+  hipError_t e = plan->logn > 13
+                     ? mi::launch_bsk_to_ntt_large(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width,
+                                                   normalize ? 1 : 0, plan->n_inv, plan->d_twid, (hipStream_t)stream)
+                     : mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0,
+                                             plan->n_inv, plan->d_twid, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
 }
 
@@ -502,6 +508,10 @@ static int ext_common(const mi_ntt64_plan* plan, bool cmux, uint64_t* out, uint6
   if (twisted_ext_applies(plan, variant, k, base_log, level))
     e = mi::launch_ext_tw(cmux, variant == MI_NTT64_SOLINAS, out, in, ggsw, batch, base_log, plan->d_twist_f,
                           (hipStream_t)stream, gidx, (uint32_t)n_ggsw);
+  else if (plan->logn > 13)
+    e = mi::launch_ext_product_large(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch,
+                                     base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
+                                     (uint32_t)n_ggsw);
   else
     e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch, base_log,
                                plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
@@ -642,6 +652,10 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   if (twisted_ext_applies(plan, key->variant, key->k, key->base_log, key->level))
     e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
                           ms_mode == MI_MS_CENTERED, s);
+  else if (plan->logn > 13)
+    e = mi::launch_pbs_large(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut,
+                             key->bsk, key->n_lwe, batch, key->base_log, plan->d_twid, plan->d_inv_twid,
+                             ms_mode == MI_MS_CENTERED, s);
   else
     e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
                        key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);

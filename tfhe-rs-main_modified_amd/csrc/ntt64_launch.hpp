@@ -53,8 +53,8 @@ hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint6
 
 namespace mi {
 
-// pbs_kernels.hip — Goldilocks, N = 2^logn for logn in {10, 11, 12}, GLWE dimension k in {1, 2}, any level
-// count (callers validate the shape; other shapes return hipErrorInvalidValue).
+// pbs_kernels.hip — Goldilocks, the shapes of mi::capi::check_pbs_shape up to N = 8192, any level count (callers
+// validate the shape; other shapes return hipErrorInvalidValue).
 hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s);
 hipError_t launch_bsk_to_ntt(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
                              int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s);
@@ -69,6 +69,17 @@ hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, u
 hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s);
+// pbs_large.hip — N = 2^14 ... 2^17 (beyond one workgroup): the blind rotation / external product as device-wide
+// passes per CMUX step over chunks of ciphertexts whose accumulators live in HBM; same arguments as above
+hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
+                            const uint64_t* lut, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
+                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s);
+hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
+                                    const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
+                                    const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx,
+                                    uint32_t n_ggsw);
+hipError_t launch_bsk_to_ntt_large(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
+                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s);
 // BNF, level 1, base_log <= 31, on the twisted transform; tab = plan twist tables [fwd | inverse]
 // BNF level-1 external product (cmux=false: out += GGSW . glwe) / CMUX (cmux=true: ct0 = out,
 // ct1 = glwe) on the twisted transform; the GGSW is the Raw NTT key (N^-1 via the third table)

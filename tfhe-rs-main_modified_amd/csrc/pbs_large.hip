@@ -1,0 +1,358 @@
+// pbs_large.hip — blind rotation, PBS, external product and CMUX for polynomial sizes beyond one workgroup
+// (N = 2^14 ... 2^17; the shortint PARAM_MESSAGE_4_CARRY_4 shape is N = 65536, k = 1, n = 1117, B = 2^11, l = 3,
+// shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/ks_pbs.rs:71-90), both NTT variants (reference paths
+// relative to /root/reference/tfhe/src/core_crypto):
+//   BNF     : algorithms/lwe_programmable_bootstrapping/ntt64_bnf_pbs.rs:208-726
+//   SOLINAS : algorithms/lwe_programmable_bootstrapping/ntt64_pbs.rs:213-702
+//
+// MI355X design.  An N = 65536 GLWE accumulator (k + 1 polynomials, 1 MiB at k = 1) cannot live in one workgroup, so
+// the accumulators of a chunk of ciphertexts live in HBM and every CMUX step is a short sequence of device-wide
+// kernels over the whole chunk, each one a streaming pass:
+//   decompose : ct1 = X^a acc - acc (the monomial rotation read straight from acc), signed decomposition into `level`
+//               digit polynomials per GLWE polynomial (mod p)           -> digits [b][level][k+1][N]
+//   forward   : the plan's large-N transform over all chunk x level x (k+1) digit polynomials (ntt64_kernels.hip:
+//               top stages on strided columns + 2^14 register-window blocks, the reference's depth-first split)
+//   mac       : y[b][c] = sum_{li, r} digits[b][li][r] . GGSW_i[li][r][c]   (the step's GGSW is shared by the whole
+//               chunk: read once per chunk, L2/MALL-resident across the ciphertexts)
+//   inverse   : large-N inverse transform of the chunk x (k+1) products
+//   accumulate: acc += modswitch_{p -> 2^64}(y) (BNF) / acc += y mod p (Solinas)
+// Masks that switch to 0 give ct1 = 0 and an exactly-zero contribution (decomposition of 0 is 0 at every level), so
+// every ciphertext runs every step and no per-ciphertext control flow reaches the kernels; the reference's skip
+// (ntt64_bnf_pbs.rs:241, ntt64_pbs.rs:257) changes no value.  The elementwise kernels are HBM-bound (coalesced,
+// grid-stride); the transforms are the engine's large-N kernels.  Bit-exact: every pass restates the reference
+// arithmetic exactly (canonical residues), as the fused kernels of pbs_kernels.hip do.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "mi_arith.hpp"
+#include "ntt64_launch.hpp"
+#include "pbs_device.hpp"
+
+namespace mi {
+namespace pbs {
+
+struct LargeShape {
+  uint32_t logn, n, k, level;
+  int base_log;
+};
+
+__device__ __forceinline__ uint64_t grid_stride_start() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t grid_stride() { return (uint64_t)gridDim.x * blockDim.x; }
+
+// signed decomposition of one GLWE coefficient into `level` digits mod p, least significant level first (the
+// order the reference's iterator yields them and the GGSW stores its blocks): BNF = decomposer.rs:156-185 +
+// iter.rs:131-151 (digits mapped into [0, p) as ntt64.rs:231-238); Solinas = iter.rs:623-745 (sign-magnitude)
+template <bool BNF>
+__device__ __forceinline__ void decompose_store(u64 x, u64* __restrict__ dst, uint64_t level_stride, int base_log,
+                                                int level) {
+  u64 state;
+  bool sign = false;
+  if (BNF) {
+    state = decomp_init_native(x, base_log, level);
+  } else {
+    const unsigned shift = 64u - (unsigned)(base_log * level);
+    sign = x >= P / 2 + 1;
+    state = closest_abs_nonnative(sign ? P - x : x, base_log, level) >> shift;
+  }
+  for (int li = 0; li < level; ++li) {
+    u64 term = decompose_one_level(base_log, state);
+    if (!BNF && sign) term = (u64)0 - term;
+    dst[(uint64_t)li * level_stride] = ((int64_t)term < 0) ? term + P : term;
+  }
+}
+
+// acc[b] = the LUT (BNF), or the LUT rotated by -ms(body) (Solinas, ntt64_pbs.rs:237-249)
+template <bool BNF>
+__global__ __launch_bounds__(256) void large_init_acc(u64* __restrict__ acc, const u64* __restrict__ lut,
+                                                      const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t batch,
+                                                      LargeShape sh) {
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    const uint64_t b = i / per, ce = i % per;
+    const uint32_t c = (uint32_t)(ce >> sh.logn), m = (uint32_t)(ce & (sh.n - 1));
+    if (BNF) {
+      acc[i] = lut[ce];
+    } else {
+      const u64 body = ms_non_native(lwe_in[b * (n_lwe + 1) + n_lwe], sh.logn + 1);
+      const uint32_t full = (uint32_t)(body >> sh.logn) & 1u, rem = (uint32_t)(body & (sh.n - 1));
+      u64 v = lut[(uint64_t)c * sh.n + ((m + rem) & (sh.n - 1))];  // div_assign by X^body
+      if (full ^ (m >= sh.n - rem)) v = neg_custom(v);
+      acc[i] = v;
+    }
+  }
+}
+
+// step i of the blind rotation: ct1 = X^a acc - acc (polynomial_wrapping_monic_monomial_mul_assign[_custom_mod],
+// then the CMUX difference), decomposed into digits[b][li][c][N]
+template <bool BNF>
+__global__ __launch_bounds__(256) void large_rotate_decompose(u64* __restrict__ digits, const u64* __restrict__ acc,
+                                                              const u64* __restrict__ lwe_in, uint32_t n_lwe,
+                                                              uint32_t step, uint32_t batch, LargeShape sh) {
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
+  const unsigned log_mod = sh.logn + 1;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    const uint64_t b = i / per, ce = i % per;
+    const uint32_t c = (uint32_t)(ce >> sh.logn), e = (uint32_t)(ce & (sh.n - 1));
+    const u64 a_raw = lwe_in[b * (n_lwe + 1) + step];
+    u64 a = 0;
+    if (BNF) a = modulus_switch(a_raw, log_mod);
+    else if (a_raw != 0) a = ms_non_native(a_raw, log_mod);
+    const uint32_t full = (uint32_t)(a >> sh.logn) & 1u, rem = (uint32_t)(a & (sh.n - 1));
+    const u64* ap = acc + b * per + (uint64_t)c * sh.n;
+    u64 v = ap[(e - rem) & (sh.n - 1)];  // mul_assign by X^a: new[e] = old[(e - rem) % N], negated for e < rem
+    if (full ^ (e < rem)) v = neg_q<BNF>(v);
+    const u64 ct1 = BNF ? v - ap[e] : sub_custom(v, ap[e]);
+    decompose_store<BNF>(ct1, digits + b * sh.level * per + (uint64_t)c * sh.n + e, per, sh.base_log, (int)sh.level);
+  }
+}
+
+// external product / CMUX input: CMUX first writes glwe -= out back (ct1 = ct1 - ct0), then both decompose glwe.
+// gidx: item b is skipped (nothing written anywhere) when gidx[b] >= n_ggsw
+template <bool BNF, bool CMUX>
+__global__ __launch_bounds__(256) void large_glwe_decompose(u64* __restrict__ digits, u64* __restrict__ glwe,
+                                                            const u64* __restrict__ out, uint32_t batch, LargeShape sh,
+                                                            const uint32_t* __restrict__ gidx, uint32_t n_ggsw) {
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    const uint64_t b = i / per, ce = i % per;
+    if (gidx && gidx[b] >= n_ggsw) continue;
+    u64 x = glwe[i];
+    if (CMUX) {
+      x = BNF ? x - out[i] : sub_custom(x, out[i]);
+      glwe[i] = x;
+    }
+    decompose_store<BNF>(x, digits + b * sh.level * per + ce, per, sh.base_log, (int)sh.level);
+  }
+}
+
+// y[b][c][e] = sum over levels li and rows r of digits[b][li][r][e] * G[li][r][c][e] (update_with_fmadd,
+// ntt64_pbs.rs:683-702 / ntt64_bnf_pbs.rs:707-726), times N^-1 when `n_inv` != 0 (the external product on a Raw
+// BNF GGSW; the PBS's BNF key copy has N^-1 folded in already).  ggsw = the GGSW of item b: ggsw_list + gidx[b] (or
+// the one GGSW when gidx is NULL)
+__global__ __launch_bounds__(256) void large_mac(u64* __restrict__ y, const u64* __restrict__ digits,
+                                                 const u64* __restrict__ ggsw_list, uint32_t batch, LargeShape sh,
+                                                 u64 n_inv, const uint32_t* __restrict__ gidx, uint32_t n_ggsw) {
+  const Goldilocks gl;
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
+  const uint64_t ggsw_len = (uint64_t)sh.level * (sh.k + 1) * per;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    const uint64_t b = i / per, ce = i % per;
+    const uint32_t c = (uint32_t)(ce >> sh.logn), e = (uint32_t)(ce & (sh.n - 1));
+    uint32_t g = 0;
+    if (gidx) {
+      g = gidx[b];
+      if (g >= n_ggsw) continue;
+    }
+    const u64* G = ggsw_list + (uint64_t)g * ggsw_len;
+    const u64* d = digits + b * sh.level * per + e;
+    u64 acc = 0;
+    for (uint32_t li = 0; li < sh.level; ++li)
+      for (uint32_t r = 0; r <= sh.k; ++r)
+        acc = gl.add(acc, gl.mul(d[(uint64_t)li * per + (uint64_t)r * sh.n],
+                                 G[((uint64_t)li * (sh.k + 1) * (sh.k + 1) + (uint64_t)r * (sh.k + 1) + c) * sh.n + e]));
+    y[i] = n_inv ? gl.mul(acc, n_inv) : acc;
+  }
+}
+
+// acc += modswitch_{p -> 2^64}(y) (ntt64.rs:184-197 + wrapping add) / acc += y mod p (ntt64.rs:244-266)
+template <bool BNF>
+__global__ __launch_bounds__(256) void large_accumulate(u64* __restrict__ acc, const u64* __restrict__ y, uint32_t batch,
+                                                        LargeShape sh, const uint32_t* __restrict__ gidx,
+                                                        uint32_t n_ggsw) {
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    if (gidx && gidx[i / per] >= n_ggsw) continue;
+    acc[i] = BNF ? acc[i] + modswitch_prime_to_native(y[i]) : add_custom(acc[i], y[i]);
+  }
+}
+
+// centered_binary_ms_body_correction_to_add (algorithms/modulus_switch.rs:60-104), one workgroup per ciphertext
+__global__ __launch_bounds__(256) void large_body_correction(u64* __restrict__ corr, const u64* __restrict__ lwe_in,
+                                                             uint32_t n_lwe, unsigned log_mod) {
+  __shared__ u64 sh[512];
+  const u64 v = centered_body_correction<256>(lwe_in + (uint64_t)blockIdx.x * (n_lwe + 1), n_lwe, log_mod,
+                                              (int)threadIdx.x, sh);
+  if (threadIdx.x == 0) corr[blockIdx.x] = v;
+}
+
+// BNF: rotate by -ms(body [+ centered correction]) (ntt64_bnf_pbs.rs:262-270); Solinas: the LUT was pre-rotated;
+// then sample extraction of coefficient 0 (glwe_sample_extraction.rs:89-160): out[c N] = A_c[0],
+// out[c N + j] = -A_c[N - j], out[k N] = B[0]
+template <bool BNF>
+__global__ __launch_bounds__(256) void large_extract(u64* __restrict__ lwe_out, const u64* __restrict__ acc,
+                                                     const u64* __restrict__ lwe_in, const u64* __restrict__ corr,
+                                                     uint32_t n_lwe, uint32_t batch, LargeShape sh) {
+  const uint64_t per_out = (uint64_t)sh.k * sh.n + 1, total = per_out * batch;
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
+  for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
+    const uint64_t b = i / per_out, o = i % per_out;
+    uint32_t full = 0, rem = 0;
+    if (BNF) {
+      const u64 body = modulus_switch(lwe_in[b * (n_lwe + 1) + n_lwe] + (corr ? corr[b] : 0), sh.logn + 1);
+      full = (uint32_t)(body >> sh.logn) & 1u;
+      rem = (uint32_t)(body & (sh.n - 1));
+    }
+    const uint32_t c = (uint32_t)(o >> sh.logn), j = (uint32_t)(o & (sh.n - 1));  // o = k N gives c = k, j = 0
+    const uint32_t m = (j == 0) ? 0 : sh.n - j;
+    u64 v = acc[b * per + (uint64_t)c * sh.n + ((m + rem) & (sh.n - 1))];
+    if (full ^ (m >= sh.n - rem)) v = neg_q<BNF>(v);
+    lwe_out[i] = (c == sh.k || j == 0) ? v : neg_q<BNF>(v);
+  }
+}
+
+// forward_from_power_of_two_modulus (ntt64.rs:166-178): x -> round(x p / 2^w) of the key conversion
+__global__ __launch_bounds__(256) void large_modswitch_to_prime(u64* __restrict__ dst, const u64* __restrict__ src,
+                                                                uint64_t count, unsigned in_width) {
+  for (uint64_t i = grid_stride_start(); i < count; i += grid_stride()) {
+    u64 v = src[i];
+    if (in_width) {
+      const unsigned __int128 w =
+          ((unsigned __int128)(v >> (64u - in_width))) * P + ((unsigned __int128)1 << (in_width - 1));
+      v = (u64)(w >> in_width);
+    }
+    dst[i] = v;
+  }
+}
+
+inline unsigned blocks_for(uint64_t total) {
+  const uint64_t b = (total + 255) / 256;
+  return (unsigned)std::min<uint64_t>(b, 65536);
+}
+
+// ciphertexts per chunk: the digits, products and accumulators of one chunk stay below ~1 GiB of scratch
+inline size_t chunk_for(const LargeShape& sh, size_t batch) {
+  const size_t per_item = ((size_t)sh.level + 2) * (sh.k + 1) * sh.n * sizeof(u64);
+  return std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per_item));
+}
+
+}  // namespace pbs
+
+hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
+                            const uint64_t* lut, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
+                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s) {
+  using namespace pbs;
+  if (batch == 0) return hipSuccess;
+  const LargeShape sh{(uint32_t)logn, 1u << logn, (uint32_t)k, (uint32_t)level, base_log};
+  const size_t per = (size_t)(k + 1) * sh.n, chunk = chunk_for(sh, batch);
+  const size_t ggsw_len = (size_t)level * (k + 1) * per;
+  u64 *scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, (chunk * ((size_t)level + 2) * per + chunk) * sizeof(u64), s);
+  if (e != hipSuccess) return e;
+  u64* digits = scratch;
+  u64* y = digits + chunk * level * per;
+  u64* acc = y + chunk * per;
+  u64* corr = acc + chunk * per;
+  const MontParams mp{};
+  for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
+    const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
+    const u64* in = lwe_in + b0 * (n_lwe + 1);
+    const uint64_t elems = (uint64_t)nb * per;
+    if (bnf)
+      hipLaunchKernelGGL(large_init_acc<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, lut, in, (uint32_t)n_lwe,
+                         nb, sh);
+    else
+      hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, lut, in, (uint32_t)n_lwe,
+                         nb, sh);
+    for (uint32_t i = 0; i < n_lwe && e == hipSuccess; ++i) {
+      if (bnf)
+        hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
+                           (uint32_t)n_lwe, i, nb, sh);
+      else
+        hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
+                           (uint32_t)n_lwe, i, nb, sh);
+      e = launch_ntt(true, logn, true, mp, digits, (size_t)nb * level * (k + 1), sh.n, tw, s);
+      if (e != hipSuccess) break;
+      hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, bsk + (size_t)i * ggsw_len, nb,
+                         sh, (u64)0, (const uint32_t*)nullptr, 1u);
+      e = launch_ntt(false, logn, true, mp, y, (size_t)nb * (k + 1), sh.n, itw, s);
+      if (e != hipSuccess) break;
+      if (bnf)
+        hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, y, nb, sh,
+                           (const uint32_t*)nullptr, 1u);
+      else
+        hipLaunchKernelGGL(large_accumulate<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, y, nb, sh,
+                           (const uint32_t*)nullptr, 1u);
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) break;
+    const bool corr_on = bnf && centered;
+    if (corr_on)
+      hipLaunchKernelGGL(large_body_correction, dim3(nb), dim3(256), 0, s, corr, in, (uint32_t)n_lwe,
+                         (unsigned)(logn + 1));
+    const uint64_t outs = (uint64_t)nb * ((uint64_t)k * sh.n + 1);
+    u64* o = out + b0 * ((size_t)k * sh.n + 1);
+    if (bnf)
+      hipLaunchKernelGGL(large_extract<true>, dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in,
+                         corr_on ? corr : (const u64*)nullptr, (uint32_t)n_lwe, nb, sh);
+    else
+      hipLaunchKernelGGL(large_extract<false>, dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in,
+                         (const u64*)nullptr, (uint32_t)n_lwe, nb, sh);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = hipFreeAsync(scratch, s);
+  return e != hipSuccess ? e : ef;
+}
+
+// convert_standard_lwe_bootstrap_key_to_ntt64 (lwe_bootstrap_key_conversion.rs:294-365) at large N: modulus switch
+// into dst, the large-N forward transform in place, optional normalisation (NttLweBootstrapKeyOption::Normalize)
+hipError_t launch_bsk_to_ntt_large(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
+                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
+  using namespace pbs;
+  if (n_polys == 0) return hipSuccess;
+  const uint64_t count = (uint64_t)n_polys << logn;
+  hipLaunchKernelGGL(large_modswitch_to_prime, dim3(blocks_for(count)), dim3(256), 0, s, dst, src, count, in_width);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = launch_ntt(true, logn, true, MontParams{}, dst, n_polys, (size_t)1 << logn, tw, s);
+  if (e == hipSuccess && normalize) e = launch_scale(dst, dst, count, n_inv, s);
+  return e;
+}
+
+hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
+                                    const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
+                                    const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx,
+                                    uint32_t n_ggsw) {
+  using namespace pbs;
+  if (batch == 0) return hipSuccess;
+  const LargeShape sh{(uint32_t)logn, 1u << logn, (uint32_t)k, (uint32_t)level, base_log};
+  const size_t per = (size_t)(k + 1) * sh.n, chunk = chunk_for(sh, batch);
+  u64* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, chunk * ((size_t)level + 1) * per * sizeof(u64), s);
+  if (e != hipSuccess) return e;
+  u64* digits = scratch;
+  u64* y = digits + chunk * level * per;
+  const MontParams mp{};
+  for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
+    const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
+    const uint64_t elems = (uint64_t)nb * per;
+    u64* o = out + b0 * per;
+    u64* g = glwe + b0 * per;
+    const uint32_t* gi = gidx ? gidx + b0 : nullptr;
+#define MI_LARGE_DEC(B, C)                                                                                          \
+  hipLaunchKernelGGL((large_glwe_decompose<B, C>), dim3(blocks_for(elems)), dim3(256), 0, s, digits, g, o, nb, sh, gi, \
+                     n_ggsw)
+    if (bnf) {
+      if (cmux) MI_LARGE_DEC(true, true); else MI_LARGE_DEC(true, false);
+    } else {
+      if (cmux) MI_LARGE_DEC(false, true); else MI_LARGE_DEC(false, false);
+    }
+#undef MI_LARGE_DEC
+    e = launch_ntt(true, logn, true, mp, digits, (size_t)nb * level * (k + 1), sh.n, tw, s);
+    if (e != hipSuccess) break;
+    // BNF GGSWs are the reference's Raw NTT keys: the product is normalised here (ntt64_bnf_pbs.rs:670)
+    hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, ggsw, nb, sh,
+                       bnf ? (u64)n_inv : (u64)0, gi, gi ? n_ggsw : 1u);
+    e = launch_ntt(false, logn, true, mp, y, (size_t)nb * (k + 1), sh.n, itw, s);
+    if (e != hipSuccess) break;
+    if (bnf)
+      hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, s, o, y, nb, sh, gi, n_ggsw);
+    else
+      hipLaunchKernelGGL(large_accumulate<false>, dim3(blocks_for(elems)), dim3(256), 0, s, o, y, nb, sh, gi, n_ggsw);
+    e = hipGetLastError();
+  }
+  const hipError_t ef = hipFreeAsync(scratch, s);
+  return e != hipSuccess ? e : ef;
+}
+
+}  // namespace mi
