@@ -273,6 +273,12 @@ class Wave:
         self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
         self.scc = int(word != 0)
 
+    def op_s_andn2_b64(self, a):
+        word = _word(self.mask(a[1]) & ~self.mask(a[2]))
+        b = self.spair(a[0])
+        self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
+        self.scc = int(word != 0)
+
     def op_s_add_u32(self, a):
         x = self.s_src(a[1]) + self.s_src(a[2])
         self.s_set(a[0], x)

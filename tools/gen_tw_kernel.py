@@ -215,11 +215,7 @@ def tmul(sg, S, xlo, xhi, xp, sl, tlo, thi):
             sg.add(f"v_lshrrev_b32 {h}, {32 - r}, {xhi}", [xhi], [h])
         sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {h}, -1, {P[0]}", [h, P[0]], [P[1], c[0]])
         if e > 32:
-            sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[0]}", [c[0]], [v[4]])
-            sg.add(f"v_mad_u64_u32 {P[0]}, {JUNK}, {v[4]}, 1, {P[1]}", [v[4], P[1]], [P[0], JUNK])
-            sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
-            sg.add(f"v_mov_b32 {v[7]}, {v[0]}", [v[0]], [v[7]])
-            sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[1]}, -1, {P[3]}", [v[1], P[3]], [P[1], c[0]])
+            times_2_32(sg, sl)
         sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {P[1]}", [P[1]], [P[0], c[1]])
         sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
         sg.add(f"v_cndmask_b32_e64 {tlo}, {v[2]}, {v[0]}, {c[1]}", [v[2], v[0], c[1]], [tlo])
@@ -238,6 +234,21 @@ def tmul(sg, S, xlo, xhi, xp, sl, tlo, thi):
     tp = pair_of(tlo, thi)
     sg.add(f"v_mad_i64_i32 {tp}, {JUNK}, {v[5]}, s{S_X15}, {P[1]}", [v[5], P[1]], [tp, tlo, thi, JUNK])
     return neg
+
+
+def times_2_32(sg, sl):
+    """P1 <- y 2^32 mod p (not canonical, carry in c0) for y = P1 + c0 2^64 (the unfolded result of a shift, carry
+    in c0): y 2^32 = P1_lo 2^32 + P1_hi 2^64 + c0 2^96 = (P1_lo : 0) + P1_hi EPS - c0.  The -c0 goes into the high
+    word: (P1_lo - c0 : 0) + (P1_hi + c0') EPS with the borrow b of P1_lo - c0 and c0' = c0 & ~b, since EPS - 2^32 = -1
+    (and when P1_lo = 0 the word wraps to 2^32 - 1 with b set: (2^32 - 1) 2^32 = -1 + p).  P1_hi + c0' never wraps
+    (y < 2^63 whenever c0 is set).  5 VALU + 1 SALU instead of folding the carry first (cndmask + mad) and moving
+    y_lo into a (y_lo : 0) pair."""
+    v, P, c = sl.v, sl.P, sl.c
+    sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
+    sg.add(f"v_subb_co_u32_e64 {v[7]}, {c[1]}, {v[2]}, 0, {c[0]}", [v[2], c[0]], [v[7], c[1]])
+    sg.add(f"s_andn2_b64 {c[0]}, {c[0]}, {c[1]}", [c[0], c[1]], [c[0], "scc"], "salu")
+    sg.add(f"v_addc_co_u32_e64 {v[4]}, {JUNK}, {v[3]}, 0, {c[0]}", [v[3], c[0]], [v[4], JUNK])
+    sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[4]}, -1, {P[3]}", [v[4], P[3]], [P[1], c[0]])
 
 
 def add_part1(sg, sl, alo, ahi, tlo, thi):
@@ -277,10 +288,9 @@ def ct_core(sg, sl, a, b, neg, tsrc=None):
     alo, ahi, ap = a
     blo, bhi, bp = b
     tlo, thi = tsrc if tsrc else (sl.v[2], sl.v[3])
-    if tsrc:  # t aliases b, which the subtraction overwrites: keep a copy
-        sg.add(f"v_mov_b32 {sl.v[2]}, {tlo}", [tlo], [sl.v[2]])
-        sg.add(f"v_mov_b32 {sl.v[3]}, {thi}", [thi], [sl.v[3]])
-        tlo, thi = sl.v[2], sl.v[3]
+    # t may alias b (tsrc: twiddle +-1 on a canonical b): the sum reads it first, and the subtraction that overwrites
+    # b reads each word of it in the instruction that writes that word, so no copy is needed (the list scheduler
+    # keeps the sum's reads ahead of the overwrite: a write waits for every earlier reader of its register)
     add_part1(sg, sl, alo, ahi, tlo, thi)
     if not neg:
         sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
@@ -720,11 +730,7 @@ def tmul_lane(sg, S_even, S_odd, x, sl, tlo, thi, par3, amt):
         sg.add(f"v_lshlrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
         sg.add(f"v_lshrrev_b32 {v[4]}, {A1}, {xhi}", [A1, xhi], [v[4]])
         sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[4]}, -1, {P[0]}", [v[4], P[0]], [P[1], c[0]])
-        sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[0]}", [c[0]], [v[4]])
-        sg.add(f"v_mad_u64_u32 {P[0]}, {JUNK}, {v[4]}, 1, {P[1]}", [v[4], P[1]], [P[0], JUNK])
-        sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
-        sg.add(f"v_mov_b32 {v[7]}, {v[0]}", [v[0]], [v[7]])
-        sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[1]}, -1, {P[3]}", [v[1], P[3]], [P[1], c[0]])
+        times_2_32(sg, sl)
         sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {P[1]}", [P[1]], [P[0], c[1]])
         sg.add(f"s_or_b64 {c[1]}, {c[1]}, {c[0]}", [c[1], c[0]], [c[1], "scc"], "salu")
         sg.add(f"v_cndmask_b32_e64 {tlo}, {v[2]}, {v[0]}, {c[1]}", [v[2], v[0], c[1]], [tlo])
