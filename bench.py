@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Integer-VALU issue model of the generated bodies (tools/valu_cost.py: instruction mix x the issue
 # costs measured by tools/valu_probe.hip; tests/test_bench_contract.py keeps these in sync), and the
 # MI355X peak engine clock it is priced at.
-VALU_CYCLES = {"fwd": 14341.4, "inv": 14447.5, "pbs_step": 35467.6, "pbs_sol_step": 35788.9, "ext_bnf": 34278.7}
+VALU_CYCLES = {"fwd": 14136.3, "inv": 14242.4, "pbs_step": 35090.9, "pbs_sol_step": 35412.1, "ext_bnf": 33902.0}
 SIMDS, PEAK_CLOCK_HZ = 256 * 4, 2.4e9
 # PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
 PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
@@ -295,6 +295,76 @@ def cpu_baseline_pbs_solinas(seconds: float):
             "sample": (f"{reps} x {sample} Solinas-modulus PBS (n=918, N=2048, l=1) in {el:.1f}s, restatement of "
                        f"ntt64_pbs.rs with {'AVX-512' if O.have_avx512() else 'scalar'} transforms, "
                        f"OpenMP {threads} threads")}
+
+
+# the other shortint parameter sets' PBS shapes (shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/
+# ks_pbs.rs:8-90): name -> (N, k, n, base_log, level, batch per step)
+SHAPE_LEGS = {
+    "message_1_carry_1": (512, 4, 879, 23, 1, 4096),
+    "message_3_carry_3": (8192, 1, 1077, 15, 2, 1024),
+    "message_4_carry_4": (65536, 1, 1117, 11, 3, 192),
+}
+
+
+def bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist):
+    """BNF PBS at another shortint shape (synthetic NTT-domain key and inputs, resident): N = 512 / 8192 run the fused
+    one-workgroup-per-ciphertext kernels (pbs_kernels.hip), N = 65536 the multi-kernel blind rotation
+    (pbs_large.hip, accumulators in HBM).  Same time-based timing as the other legs."""
+    M = eng.ntt64_pbs
+    n, k, n_lwe, base_log, level, batch = SHAPE_LEGS[name]
+    plan = eng.Plan.try_new(n, SOLINAS_P, device=dev.index)
+    bsk = torch.empty((n_lwe, level, k + 1, k + 1, n), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 90, SOLINAS_P)
+    key = M.NttBootstrapKey(plan, bsk, base_log, level, M.BNF)
+    del bsk
+    lut = torch.empty((k + 1, n), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 91, 0)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 92, 0)
+    out = torch.empty((batch, k * n + 1), dtype=torch.int64, device=dev)
+    run = lambda: M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe, out, lut, key)
+    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=1)
+    del key
+    ntts = n_lwe * (level + 1) * (k + 1)  # forward (level x (k+1)) + inverse (k+1) transforms per CMUX step
+    return {"metric": f"PBS/sec, BNF NTT PBS at the {name.upper()} shape", "value": world * batch * K / el,
+            "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms,
+            "ntt_per_s": world * batch * K / el * ntts,
+            "config": {"workload": f"programmable_bootstrap_ntt64_bnf, N={n} k={k} n={n_lwe} base_log={base_log} "
+                                   f"level={level} (shortint {name.upper()} shape), synthetic key",
+                       "batch_per_gpu": batch,
+                       "engine": "multi-kernel blind rotation (pbs_large.hip)" if n > 8192 else
+                                 "fused one-workgroup-per-ciphertext kernel (pbs_kernels.hip)"},
+            "cpu_baseline": None}
+
+
+def cpu_baseline_pbs_shape(name, seconds: float):
+    """Oracle restatement of the BNF PBS at the shape (OpenMP, one PBS per thread), bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    n, k, n_lwe, base_log, level, _ = SHAPE_LEGS[name]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    ctx = O.NttContext(n)
+    bsk = O.fill_uniform(SEED + 90, SOLINAS_P, n_lwe * level * (k + 1) ** 2 * n)
+    lut = O.fill_uniform(SEED + 91, 0, (k + 1) * n)
+    sample = threads
+    lwe = O.fill_uniform(SEED + 92, 0, sample * (n_lwe + 1)).reshape(sample, n_lwe + 1)
+    out = np.zeros((sample, k * n + 1), np.uint64)
+    O.pbs_set_fast_ntt(True)
+    try:
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ctx.pbs_batch_bnf(lwe, lut, bsk, k, base_log, level, threads=threads, out=out)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        O.pbs_set_fast_ntt(False)
+    return {"value": reps * sample / el, "unit": "PBS/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {sample} BNF PBS (N={n}, k={k}, n={n_lwe}, l={level}) in {el:.1f}s, restatement of "
+                      f"ntt64_bnf_pbs.rs, OpenMP {threads} threads"}
 
 
 def bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist):
@@ -790,6 +860,8 @@ def main():
         legs["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
         legs["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier, dist)
+        legs["pbs_shapes"] = {name: bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist)
+                              for name in SHAPE_LEGS}
 
     elapsed, launch_ms = headline(K, args.warmup)
 
@@ -891,6 +963,8 @@ def main():
             out["pbs_solinas"]["cpu_baseline"] = cpu_baseline_pbs_solinas(min(args.cpu_seconds, 6.0))
             out["keyswitch"]["cpu_baseline"] = cpu_baseline_ks(min(args.cpu_seconds, 4.0))
             out["bsk_conversion"]["cpu_baseline"] = cpu_baseline_bsk(min(args.cpu_seconds, 3.0))
+            for name in ("message_1_carry_1", "message_3_carry_3"):  # 4_4: ~0.1 s per CMUX step per core, unbounded
+                out["pbs_shapes"][name]["cpu_baseline"] = cpu_baseline_pbs_shape(name, min(args.cpu_seconds, 4.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -66,19 +66,22 @@ def test_host_concurrent_threads(engine, oracle):
 
 def test_host_call_does_not_wait_for_other_streams(engine):
     """A host call returns while a long transform loop queued on another stream is still running (the old path
-    called hipDeviceSynchronize, which waited for it)."""
+    called hipDeviceSynchronize, which waited for it).  The loop is 80 launches over a 1 GiB batch (~35 ms of GPU
+    work, few enough launches that queueing them never blocks the host), and the host path is warmed first so
+    its staging slot exists."""
     import torch
     plan = engine.Plan.try_new(2048, P)
-    busy = torch.zeros((8192, 2048), dtype=torch.int64, device="cuda")
+    x = np.arange(2048, dtype=np.uint64)
+    plan.fwd(x)  # warm: the staging slot of this device exists and is large enough
+    busy = torch.zeros((65536, 2048), dtype=torch.int64, device="cuda")
     s = torch.cuda.Stream()
     done = torch.cuda.Event()
     torch.cuda.synchronize()
     with torch.cuda.stream(s):
-        for _ in range(400):  # ~50 ms of queued work
+        for _ in range(40):
             plan.fwd(busy)
             plan.inv(busy)
         done.record(s)
-    x = np.arange(2048, dtype=np.uint64)
     plan.fwd(x)
     assert not done.query(), "the host call waited for an unrelated stream"
     torch.cuda.synchronize()
