@@ -94,3 +94,83 @@ def test_gloo_world2_scatter_compute_gather(total):
         if p.is_alive():
             p.kill()
     assert results == [(0, "ok"), (1, "ok")], results
+
+
+class _FakeDist:
+    """Records the point-to-point ops scatter_batch / gather_batch build (the RCCL path's op construction, checked
+    without a process group or a GPU)."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank, self.posted = world, rank, []
+        self.isend, self.irecv = "isend", "irecv"
+
+    def get_world_size(self):
+        return self.world
+
+    def get_rank(self):
+        return self.rank
+
+    def P2POp(self, op, tensor, peer):  # noqa: N802 (torch.distributed's name)
+        return (op, tensor, peer)
+
+    def batch_isend_irecv(self, ops):
+        assert ops, "an empty op list must not be posted"
+        self.posted.append(list(ops))
+
+        class W:
+            def wait(self):
+                pass
+        return [W() for _ in ops]
+
+
+@pytest.mark.parametrize("total,world", [(13, 8), (5, 8), (65536, 8), (7, 2)])
+@pytest.mark.parametrize("device", ["cpu", "meta"])
+def test_p2p_op_construction(monkeypatch, total, world, device):
+    """scatter_batch / gather_batch on every rank of an 8-rank job: the root posts one send (scatter) / receive
+    (gather) per non-empty peer shard, on a contiguous slice of the right rows, on the batch's own device (meta
+    tensors stand in for device tensors: nothing is moved to the host); an empty shard posts nothing on either side;
+    the root's own shard is a local copy."""
+    mg = _multi_gpu()
+    width = 919
+    glob = torch.arange(total * width, dtype=torch.int64).reshape(total, width).to(device)
+    for rank in range(world):
+        fd = _FakeDist(world, rank)
+        monkeypatch.setattr(mg, "_dist", lambda fd=fd: fd)
+        a, b = mg.shard_bounds(total, world, rank)
+        shard = torch.empty((b - a, width), dtype=torch.int64, device=device)
+        mg.scatter_batch(glob if rank == 0 else None, shard, src=0)
+        if rank == 0:
+            ops = fd.posted[0] if fd.posted else []
+            peers = [p for _, _, p in ops]
+            want = [r for r in range(1, world) if mg.shard_bounds(total, world, r)[1] > mg.shard_bounds(total, world, r)[0]]
+            assert peers == want
+            for op, t, p in ops:
+                pa, pb = mg.shard_bounds(total, world, p)
+                assert op == "isend" and tuple(t.shape) == (pb - pa, width) and t.is_contiguous()
+                assert t.device.type == device and t.dtype == torch.int64
+                if device == "cpu":
+                    assert torch.equal(t, glob[pa:pb])
+            if device == "cpu":
+                assert torch.equal(shard, glob[a:b])
+        else:
+            if b == a:
+                assert fd.posted == []
+            else:
+                (op, t, p), = fd.posted[0]
+                assert op == "irecv" and p == 0 and t.data_ptr() == shard.data_ptr()
+        # gather back into a column-sliced (non-contiguous) global buffer on the root
+        fd.posted.clear()
+        out = torch.zeros((total, width + 1), dtype=torch.int64, device=device)[:, :width] if rank == 0 else None
+        mg.gather_batch(shard, out, dst=0)
+        if rank == 0:
+            ops = fd.posted[0] if fd.posted else []
+            for op, t, p in ops:
+                pa, pb = mg.shard_bounds(total, world, p)
+                assert op == "irecv" and tuple(t.shape) == (pb - pa, width) and t.is_contiguous()
+                assert t.device.type == device
+            assert len(ops) == len(want)
+        elif b == a:
+            assert fd.posted == []
+        else:
+            (op, t, p), = fd.posted[0]
+            assert op == "isend" and p == 0 and tuple(t.shape) == (b - a, width)
