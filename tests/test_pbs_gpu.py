@@ -181,11 +181,11 @@ def test_pbs_functional_real_keys(engine, plan, ctx, bnf):
 def test_pbs_errors(engine, plan):
     import torch
     M = engine.ntt64_pbs
-    small = engine.Plan.try_new(512, P)
-    bsk = torch.zeros((4, 1, 2, 2, 512), dtype=torch.int64, device="cuda")
+    small = engine.Plan.try_new(256, P)
+    bsk = torch.zeros((4, 1, 2, 2, 256), dtype=torch.int64, device="cuda")
     with pytest.raises(engine.MiError) as e:
         M.NttBootstrapKey(small, bsk, 23, 1, M.BNF)
-    assert e.value.status == 6  # MI_ERR_UNSUPPORTED (N outside {1024, 2048, 4096})
+    assert e.value.status == 6  # MI_ERR_UNSUPPORTED (N = 256: below the compiled shapes)
     with pytest.raises(engine.MiError) as e:
         M.NttBootstrapKey(plan, torch.zeros((2, 1, 4, 4, N), dtype=torch.int64, device="cuda"), 10, 1, M.BNF)
     assert e.value.status == 6  # k = 3
