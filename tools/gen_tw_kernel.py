@@ -236,6 +236,16 @@ def tmul(sg, S, xlo, xhi, xp, sl, tlo, thi):
     return neg
 
 
+def times_2_32_r2(sg, sl):
+    """The r2 form of times_2_32 (carry folded first, then the (y_lo : 0) pair by two moves), kept for A/B runs."""
+    v, P, c = sl.v, sl.P, sl.c
+    sg.add(f"v_cndmask_b32_e64 {v[4]}, 0, -1, {c[0]}", [c[0]], [v[4]])
+    sg.add(f"v_mad_u64_u32 {P[0]}, {JUNK}, {v[4]}, 1, {P[1]}", [v[4], P[1]], [P[0], JUNK])
+    sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
+    sg.add(f"v_mov_b32 {v[7]}, {v[0]}", [v[0]], [v[7]])
+    sg.add(f"v_mad_u64_u32 {P[1]}, {c[0]}, {v[1]}, -1, {P[3]}", [v[1], P[3]], [P[1], c[0]])
+
+
 def times_2_32(sg, sl):
     """P1 <- y 2^32 mod p (not canonical, carry in c0) for y = P1 + c0 2^64 (the unfolded result of a shift, carry
     in c0): y 2^32 = P1_lo 2^32 + P1_hi 2^64 + c0 2^96 = (P1_lo : 0) + P1_hi EPS - c0.  The -c0 goes into the high
@@ -243,6 +253,8 @@ def times_2_32(sg, sl):
     (and when P1_lo = 0 the word wraps to 2^32 - 1 with b set: (2^32 - 1) 2^32 = -1 + p).  P1_hi + c0' never wraps
     (y < 2^63 whenever c0 is set).  5 VALU + 1 SALU instead of folding the carry first (cndmask + mad) and moving
     y_lo into a (y_lo : 0) pair."""
+    if not CLASS1_FOLD:
+        return times_2_32_r2(sg, sl)
     v, P, c = sl.v, sl.P, sl.c
     sg.add(f"v_mov_b32 {v[6]}, 0", [], [v[6]])
     sg.add(f"v_subb_co_u32_e64 {v[7]}, {c[1]}, {v[2]}, 0, {c[0]}", [v[2], c[0]], [v[7], c[1]])
@@ -291,6 +303,10 @@ def ct_core(sg, sl, a, b, neg, tsrc=None):
     # t may alias b (tsrc: twiddle +-1 on a canonical b): the sum reads it first, and the subtraction that overwrites
     # b reads each word of it in the instruction that writes that word, so no copy is needed (the list scheduler
     # keeps the sum's reads ahead of the overwrite: a write waits for every earlier reader of its register)
+    if tsrc and ALIAS_COPY:  # r2 form (tools/variant_probe A/B)
+        sg.add(f"v_mov_b32 {sl.v[2]}, {tlo}", [tlo], [sl.v[2]])
+        sg.add(f"v_mov_b32 {sl.v[3]}, {thi}", [thi], [sl.v[3]])
+        tlo, thi = sl.v[2], sl.v[3]
     add_part1(sg, sl, alo, ahi, tlo, thi)
     if not neg:
         sub_seq(sg, sl, blo, bhi, alo, ahi, tlo, thi)
@@ -531,6 +547,8 @@ def gen_bases(src, dst):
 # boundary), sc1 alone about half of that, nt sc1 10 % slower; loads keep the default policy (nt loads were slower)
 LOAD_POLICY = ""
 STORE_POLICY = " sc0 sc1"
+ALIAS_COPY = False   # r2: copy a +-1-twiddle operand before the subtraction overwrites it (2 moves)
+CLASS1_FOLD = True   # class-1 shifts: fold the first carry into the 2^32 step (times_2_32); False: the r2 sequence
 INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
 PROGRESSIVE = True   # forward: start the first stage as the data rows arrive (4 waits) instead of one vmcnt(0):
                      # 0.6 % faster (tools/variant_probe); the same per row in the inverse's T1 was 0.8 % slower

@@ -68,6 +68,13 @@
 #define I_ADDPAIR(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n s_nop 1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
 #define I_ADDPAIR_NONOP(x, k) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %1\n v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(x) : "v"(b) : "vcc");
 
+// cross-lane moves (pair stages): gfx950 half-swaps and a DPP quad_perm move
+#define I_PL32(x, k) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(c));
+#define I_PL16(x, k) asm volatile("v_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(c));
+#define I_DPPQ(x, k) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(x) : "v"(b));
+#define I_LSHL64(x, k) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(x));
+#define I_MADI64(x, k) { uint64_t cc; asm volatile("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(x), "=s"(cc) : "v"(b), "v"(c)); }
+
 // f64 (FFT PBS path)
 #define I_FADD(x, k) asm volatile("v_add_f64 %0, %0, %1" : "+v"(x) : "v"(fb));
 #define I_FMUL(x, k) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(x) : "v"(fb));
@@ -131,6 +138,11 @@ KERNEL(k_perm, uint32_t, I_PERM)
 KERNEL(k_nop1, uint32_t, I_NOP1)
 KERNEL(k_addpair, uint32_t, I_ADDPAIR)
 KERNEL(k_addpair_nonop, uint32_t, I_ADDPAIR_NONOP)
+KERNEL(k_pl32, uint32_t, I_PL32)
+KERNEL(k_pl16, uint32_t, I_PL16)
+KERNEL(k_dppq, uint32_t, I_DPPQ)
+KERNEL(k_lshl64, uint64_t, I_LSHL64)
+KERNEL(k_madi64, uint64_t, I_MADI64)
 
 typedef void (*kfn)(uint64_t*, uint32_t, uint32_t, uint64_t*);
 
@@ -150,6 +162,8 @@ int main(int argc, char** argv) {
       {"v_perm_b32", k_perm}, {"s_nop 1", k_nop1}, {"addco+nop1+addc (3 ins)", k_addpair}, {"addco+addc no nop", k_addpair_nonop},
       {"v_add_f64", k_fadd}, {"v_mul_f64", k_fmul}, {"v_fma_f64", k_ffma}, {"v_fmac_f64_e32", k_ffmac},
       {"v_rndne_f64", k_frnd}, {"v_cvt_f64_i32", k_fcvt}, {"v_pk_fma_f32", k_fpkfma},
+      {"v_permlane32_swap_b32", k_pl32}, {"v_permlane16_swap_b32", k_pl16}, {"v_mov_b32_dpp quad_perm", k_dppq},
+      {"v_lshlrev_b64", k_lshl64}, {"v_mad_i64_i32", k_madi64},
   };
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
