@@ -547,8 +547,13 @@ def gen_bases(src, dst):
 # boundary), sc1 alone about half of that, nt sc1 10 % slower; loads keep the default policy (nt loads were slower)
 LOAD_POLICY = ""
 STORE_POLICY = " sc0 sc1"
-ALIAS_COPY = False   # r2: copy a +-1-twiddle operand before the subtraction overwrites it (2 moves)
-CLASS1_FOLD = True   # class-1 shifts: fold the first carry into the 2^32 step (times_2_32); False: the r2 sequence
+# Two instruction cuts were tried in r3 and are OFF: tools/variant_probe timed them in one process against the r2 bodies
+# (profiles/r3/variant_probe_r3_changes.txt): the forward with both is 1.2 % slower (58.6 vs 57.9 us per 8192-poly
+# launch) although it issues 2.8 % fewer VALU cycles by the model; the inverse is unchanged.  Dropping the two moves puts
+# the subtraction right behind the add on the same registers, and the fold puts an SALU op inside the carry chain, so
+# both lengthen the dependent chains the 4 resident waves per SIMD must hide.
+ALIAS_COPY = True    # copy a +-1-twiddle operand before the subtraction overwrites it (2 moves; False saves them)
+CLASS1_FOLD = False  # class-1 shifts: True folds the first carry into the 2^32 step (times_2_32) instead
 INV_CYC_DIT = True   # inverse cyclic blocks by decimation in time (dit_exps); False: the GS form
 PROGRESSIVE = True   # forward: start the first stage as the data rows arrive (4 waits) instead of one vmcnt(0):
                      # 0.6 % faster (tools/variant_probe); the same per row in the inverse's T1 was 0.8 % slower
