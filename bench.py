@@ -307,8 +307,8 @@ SHAPE_LEGS = {
 
 
 def bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist):
-    """BNF PBS at another shortint shape (synthetic NTT-domain key and inputs, resident): N = 512 / 8192 run the fused
-    one-workgroup-per-ciphertext kernels (pbs_kernels.hip), N = 65536 the multi-kernel blind rotation
+    """BNF PBS at another shortint shape (synthetic NTT-domain key and inputs, resident): N = 512 runs the fused
+    one-workgroup-per-ciphertext kernel (pbs_kernels.hip), N = 8192 / 65536 the multi-kernel blind rotation
     (pbs_large.hip, accumulators in HBM).  Same time-based timing as the other legs."""
     M = eng.ntt64_pbs
     n, k, n_lwe, base_log, level, batch = SHAPE_LEGS[name]
@@ -332,7 +332,7 @@ def bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist):
             "config": {"workload": f"programmable_bootstrap_ntt64_bnf, N={n} k={k} n={n_lwe} base_log={base_log} "
                                    f"level={level} (shortint {name.upper()} shape), synthetic key",
                        "batch_per_gpu": batch,
-                       "engine": "multi-kernel blind rotation (pbs_large.hip)" if n > 8192 else
+                       "engine": "multi-kernel blind rotation (pbs_large.hip)" if n >= 8192 else
                                  "fused one-workgroup-per-ciphertext kernel (pbs_kernels.hip)"},
             "cpu_baseline": None}
 

@@ -94,11 +94,11 @@ int mi_fill_uniform(uint64_t *buf, size_t count, uint64_t seed, uint64_t p, int 
  * Solinas plan (p = 2^64 - 2^32 + 1), any decomposition with base_log * level < 64, at the shapes
  *   N in {1024, 2048, 4096} with GLWE dimension k in {1, 2};
  *   N = 512 with k in {1, 4}        (shortint PARAM_MESSAGE_1_CARRY_1: N 512, k 4);
- *   N = 8192 with k = 1             (PARAM_MESSAGE_3_CARRY_3);
- *   N in {16384, ..., 131072} with k in {1, 2} (PARAM_MESSAGE_4_CARRY_4: N 65536; the accumulators of a chunk of
- *                                    ciphertexts live in HBM and each CMUX step is a sequence of device-wide passes);
+ *   N in {8192, ..., 131072} with k in {1, 2} (PARAM_MESSAGE_3_CARRY_3: N 8192, 4_4: N 65536; the accumulators of
+ *                                    a chunk of ciphertexts live in HBM and each CMUX step is a sequence of
+ *                                    device-wide passes);
  * other plans / shapes return MI_ERR_UNSUPPORTED.  The N = 2048, k = 1, level-1 shapes run on the hand-scheduled
- * engine, N <= 8192 on the fused one-workgroup-per-ciphertext kernels.
+ * engine, N <= 4096 on the fused one-workgroup-per-ciphertext kernels.
  * Layouts are the reference's entity layouts, contiguous:
  *   GLWE       : (k+1) polynomials of N u64 (mask then body)
  *   GGSW (NTT) : level-major, highest level first; per level (k+1) rows x (k+1) columns of N u64,

@@ -442,6 +442,12 @@ int mi_fill_uniform(uint64_t* buf, size_t count, uint64_t seed, uint64_t p, int 
 
 }  // extern "C"
 
+// polynomial sizes from which the PBS / external product run as device-wide passes with the accumulators in HBM
+// (pbs_large.hip) instead of one fused workgroup per ciphertext (pbs_kernels.hip): at N = 8192 the fused kernel (1024
+// lanes, 128 VGPRs, spilling) takes 994.5 ms per 1024 PBS of the 3_3 shape, the passes 786.7 ms; below it the fused
+// kernels win (profiles/r3/fused_vs_large_pbs.txt)
+static constexpr int LARGE_PATH_MIN_LOGN = 13;
+
 int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant) {
   if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
   if (variant != MI_NTT64_SOLINAS && variant != MI_NTT64_BNF) return fail(MI_ERR_INVALID_ARG, "unknown variant");
@@ -450,15 +456,15 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   // the compiled shapes (pbs_kernels.hip): N in {1024, 2048, 4096} with k in {1, 2}, N = 512 with k in {1, 4}
   // (PARAM_MESSAGE_1_CARRY_1), N = 8192 with k = 1 (PARAM_MESSAGE_3_CARRY_3)
   const int ln = plan->logn;
-  // (PARAM_MESSAGE_1_CARRY_1), N = 8192 with k = 1 (PARAM_MESSAGE_3_CARRY_3); and N = 2^14 ... 2^17 with k in
-  // {1, 2} on the multi-kernel path of pbs_large.hip (PARAM_MESSAGE_4_CARRY_4: N = 65536)
+  // (PARAM_MESSAGE_1_CARRY_1); and N = 2^13 ... 2^17 with k in {1, 2} on the multi-kernel path of pbs_large.hip
+  // (PARAM_MESSAGE_3_CARRY_3: N = 8192, 4_4: N = 65536)
   const bool shape_ok = plan->goldilocks && ((ln >= 10 && ln <= 12 && (k == 1 || k == 2)) ||
-                                             (ln == 9 && (k == 1 || k == 4)) || (ln == 13 && k == 1) ||
-                                             (ln >= 14 && ln <= 17 && (k == 1 || k == 2)));
+                                             (ln == 9 && (k == 1 || k == 4)) ||
+                                             (ln >= LARGE_PATH_MIN_LOGN && ln <= 17 && (k == 1 || k == 2)));
   if (!shape_ok)
     return fail(MI_ERR_UNSUPPORTED,
                 "external product / PBS run for the Solinas plan at N in {1024, 2048, 4096} with k in {1, 2}, "
-                "N = 512 with k in {1, 4}, N = 8192 with k = 1, N in {16384, ..., 131072} with k in {1, 2}");
+                "N = 512 with k in {1, 4}, N in {8192, ..., 131072} with k in {1, 2}");
   return MI_OK;
 }
 
@@ -486,7 +492,7 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
                                           (hipStream_t)stream);
     return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
   }
-  hipError_t e = plan->logn > 13
+  hipError_t e = plan->logn > 13  // the fused conversion kernel covers N <= 8192
                      ? mi::launch_bsk_to_ntt_large(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width,
                                                    normalize ? 1 : 0, plan->n_inv, plan->d_twid, (hipStream_t)stream)
                      : mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0,
@@ -508,7 +514,7 @@ static int ext_common(const mi_ntt64_plan* plan, bool cmux, uint64_t* out, uint6
   if (twisted_ext_applies(plan, variant, k, base_log, level))
     e = mi::launch_ext_tw(cmux, variant == MI_NTT64_SOLINAS, out, in, ggsw, batch, base_log, plan->d_twist_f,
                           (hipStream_t)stream, gidx, (uint32_t)n_ggsw);
-  else if (plan->logn > 13)
+  else if (plan->logn >= LARGE_PATH_MIN_LOGN)
     e = mi::launch_ext_product_large(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch,
                                      base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
                                      (uint32_t)n_ggsw);
@@ -652,7 +658,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   if (twisted_ext_applies(plan, key->variant, key->k, key->base_log, key->level))
     e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
                           ms_mode == MI_MS_CENTERED, s);
-  else if (plan->logn > 13)
+  else if (plan->logn >= LARGE_PATH_MIN_LOGN)
     e = mi::launch_pbs_large(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut,
                              key->bsk, key->n_lwe, batch, key->base_log, plan->d_twid, plan->d_inv_twid,
                              ms_mode == MI_MS_CENTERED, s);

@@ -354,8 +354,8 @@ __global__ __launch_bounds__(256) void lift_switched_kernel(u64* __restrict__ ds
 
 // ---- dispatch ------------------------------------------------------------------------------------
 // Shapes compiled (callers validate, c_api.cpp mi::capi::check_pbs_shape): N = 1024 / 2048 / 4096 with K in {1, 2};
-// N = 512 with K in {1, 4} (PARAM_MESSAGE_1_CARRY_1); N = 8192 with K = 1 (PARAM_MESSAGE_3_CARRY_3).  N = 65536
-// (PARAM_MESSAGE_4_CARRY_4) runs the multi-workgroup blind rotation of pbs_large.hip.
+// N = 512 with K in {1, 4} (PARAM_MESSAGE_1_CARRY_1).  N >= 8192 (PARAM_MESSAGE_3_CARRY_3, 4_4) runs the multi-kernel
+// blind rotation of pbs_large.hip (measured faster from N = 8192 on: profiles/r3/fused_vs_large_pbs.txt).
 
 hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s) {
   if (count == 0) return hipSuccess;
@@ -424,7 +424,7 @@ hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, u
   if (logn == L && k == KK)                                                                      \
     return ext_shape<L, KK>(bnf, cmux, level, out, glwe, ggsw, batch, base_log, tw, itw, n_inv, s, gidx, n_ggsw);
   MI_EXT_SHAPE(9, 1) MI_EXT_SHAPE(9, 4) MI_EXT_SHAPE(10, 1) MI_EXT_SHAPE(10, 2) MI_EXT_SHAPE(11, 1) MI_EXT_SHAPE(11, 2)
-  MI_EXT_SHAPE(12, 1) MI_EXT_SHAPE(12, 2) MI_EXT_SHAPE(13, 1)
+  MI_EXT_SHAPE(12, 1) MI_EXT_SHAPE(12, 2)
 #undef MI_EXT_SHAPE
   return hipErrorInvalidValue;
 }
@@ -451,7 +451,7 @@ hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const
   if (logn == L && k == KK)                                                                                     \
     return pbs_shape<L, KK>(bnf, level, out, lwe_in, lut, bsk, n_lwe, batch, base_log, tw, itw, centered, s);
   MI_PBS_SHAPE(9, 1) MI_PBS_SHAPE(9, 4) MI_PBS_SHAPE(10, 1) MI_PBS_SHAPE(10, 2) MI_PBS_SHAPE(11, 1) MI_PBS_SHAPE(11, 2)
-  MI_PBS_SHAPE(12, 1) MI_PBS_SHAPE(12, 2) MI_PBS_SHAPE(13, 1)
+  MI_PBS_SHAPE(12, 1) MI_PBS_SHAPE(12, 2)
 #undef MI_PBS_SHAPE
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Time bench.py's PBS legs at the other shortint shapes only (diagnostic; the numbers the bench reports come from
+bench.py itself).   python tools/shape_probe.py [message_1_carry_1 message_3_carry_3 message_4_carry_4]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tfhe-rs-main_modified_amd")]
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import tfhe_ntt_amd as eng  # noqa: E402
+
+names = sys.argv[1:] or list(bench.SHAPE_LEGS)
+for i, nm in enumerate(names):  # "N,k,n,base_log,level,batch" adds an ad-hoc shape
+    if "," in nm:
+        bench.SHAPE_LEGS[nm] = tuple(int(v) for v in nm.split(","))
+dev = torch.device("cuda", 0)
+bench.SIMDS = torch.cuda.get_device_properties(dev).multi_processor_count * 4
+torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+for name in names:
+    r = bench.bench_pbs_shape(name, None, eng, torch, dev, 1, lambda: None, None)
+    print(json.dumps({"shape": name, "value": r["value"], "kernel_ms": r["kernel_ms"], "steps": r["steps"],
+                      "engine": r["config"]["engine"]}), flush=True)
