@@ -261,8 +261,10 @@ int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu *m, const mi_pbs_ntt64_key *cons
  * (re, im) doubles, N/2 complex per polynomial, in this engine's order: position p holds frequency
  * freq[p] (mi_fft64_fourier_order).  The reference's tfhe-fft "unordered" in-memory order is implementation
  * defined, but its serialised order is the natural one: mi_fft64_to/from_standard_order convert to and from
- * it.  Results are f64 computations: parity with the reference is decryption-exact and within the FFT error bound, not bit-exact.  This build: N = 2048,
- * GLWE dimension k in {1, 2}, any decomposition with base_log * level < 64. */
+ * it.  Results are f64 computations: parity with the reference is decryption-exact and within the FFT error bound,
+ * not bit-exact.  This build: 32 <= N <= 2^18; N = 2048 runs the one-wave engine (GLWE dimension k in {1, 2}), every
+ * other N the shape-generic engine (1 <= k <= 16; multi-kernel, accumulators in HBM); any decomposition with
+ * base_log * level < 64. */
 typedef struct mi_fft64_plan mi_fft64_plan;
 /* Fft::new (fft_impl/fft64/math/fft/mod.rs:170-223): MI_ERR_INVALID_ARG if n is not a power of two,
  * MI_ERR_UNSUPPORTED for sizes this build does not compile.  _cached: one plan per (n, device), kept until
@@ -321,7 +323,8 @@ int mi_fft64_pbs_batch(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uin
  * P = n_lwe level glwe_size^2, the plan's polynomial size), uploads them with one strided copy and reorders them
  * into this engine's order on `stream` (synchronised before returning); the key owns that device copy.  _write
  * produces exactly mi_fft64_bsk_serialized_size bytes from any key (a loaded one or one over a caller tensor). */
-int mi_fft64_bsk_serialized_size(size_t n_lwe, int k, int level, int format, size_t *out_len);
+int mi_fft64_bsk_serialized_size(size_t polynomial_size, size_t n_lwe, int k, int level, int format,
+                                 size_t *out_len);
 int mi_fft64_pbs_key_load(const mi_fft64_plan *plan, const uint8_t *bytes, size_t len, int format, void *stream,
                           mi_fft64_pbs_key **out_key);
 int mi_fft64_pbs_key_write(const mi_fft64_pbs_key *key, int format, uint8_t *out, size_t out_len, void *stream);

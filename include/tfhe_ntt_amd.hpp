@@ -348,9 +348,11 @@ class FourierBootstrapKey {
   FourierBootstrapKey(const Fft& fft, const double* fbsk, size_t n_lwe, int base_log, int level,
                       int glwe_dimension = 1)
       : n_lwe_(n_lwe) {
+    check(mi_fft64_plan_info(fft.raw(), &n_, nullptr));
     check(mi_fft64_pbs_key_create(fft.raw(), fbsk, n_lwe, glwe_dimension, base_log, level, &raw_));
   }
-  FourierBootstrapKey(FourierBootstrapKey&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_) {}
+  FourierBootstrapKey(FourierBootstrapKey&& o) noexcept
+      : raw_(std::exchange(o.raw_, nullptr)), n_lwe_(o.n_lwe_), n_(o.n_) {}
   FourierBootstrapKey(const FourierBootstrapKey&) = delete;
   FourierBootstrapKey& operator=(const FourierBootstrapKey&) = delete;
   ~FourierBootstrapKey() {
@@ -366,6 +368,7 @@ class FourierBootstrapKey {
     check(mi_fft64_pbs_key_load(fft.raw(), bytes, len, versioned ? MI_NTT_BSK_VERSIONED : MI_NTT_BSK_PLAIN, stream, &k));
     FourierBootstrapKey key(k, 0);  // owns the upload before anything else can throw
     check(mi_fft64_pbs_key_info(k, &key.n_lwe_, nullptr, nullptr, nullptr));
+    check(mi_fft64_plan_info(fft.raw(), &key.n_, nullptr));
     return key;
   }
   // this key as the reference's bytes
@@ -374,7 +377,7 @@ class FourierBootstrapKey {
     int k = 0, level = 0;
     check(mi_fft64_pbs_key_info(raw_, nullptr, &k, nullptr, &level));
     size_t len = 0;
-    check(mi_fft64_bsk_serialized_size(n_lwe_, k, level, fmt, &len));
+    check(mi_fft64_bsk_serialized_size(n_, n_lwe_, k, level, fmt, &len));
     std::vector<uint8_t> out(len);
     check(mi_fft64_pbs_key_write(raw_, fmt, out.data(), out.size(), stream));
     return out;
@@ -384,6 +387,7 @@ class FourierBootstrapKey {
   FourierBootstrapKey(mi_fft64_pbs_key* raw, size_t n_lwe) : raw_(raw), n_lwe_(n_lwe) {}
   mi_fft64_pbs_key* raw_ = nullptr;
   size_t n_lwe_;
+  size_t n_ = 0;  // polynomial size of the plan
 };
 
 // programmable_bootstrap_lwe_ciphertext (fft64_pbs.rs:924-1060) over a batch

@@ -1,6 +1,8 @@
 // c_api_fft.cpp — C ABI of the f64-FFT PBS path (mi_fft64_*), the default shortint PBS of tfhe core_crypto
 // (SURVEY.md §8f rank 4).  Reference paths relative to /root/reference/tfhe/src/core_crypto:
-//   Fft::new + Twisties       fft_impl/fft64/math/fft/mod.rs:58-76, 104-224 (one plan per polynomial size)
+//   Fft::new + Twisties       fft_impl/fft64/math/fft/mod.rs:58-76, 104-224 (one plan per polynomial size; N = 2048
+//                             runs the one-wave engine of fft64_pbs.hip, every other 32 <= N <= 2^18 the generic
+//                             engine of fft64_generic.hip)
 //   forward/backward_as_torus fft_impl/fft64/math/fft/mod.rs:406-511
 //   key conversion            algorithms/lwe_bootstrap_key_conversion.rs:20-150
 //   external product / CMUX   algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330, 510-560
@@ -22,8 +24,11 @@ struct mi_fft64_plan {
   size_t n = 0;
   int device = 0;
   bool cached = false;
-  double* d_tables = nullptr;  // t1 (2048) | t2 (96, padded to 128) | cm (32) | cmi (32) doubles
+  bool generic = false;        // the shape-generic engine (N != 2048)
+  double* d_tables = nullptr;  // N = 2048: t1 (2048) | t2 (96, padded to 128) | cm (32) | cmi (32) doubles;
+                               // generic: tw | untw | wm (M complex each)
   mi::FftTables tables{};
+  mi::FftGenTables gtables{};
 };
 
 struct mi_fft64_pbs_key {
@@ -37,6 +42,7 @@ struct mi_fft64_pbs_key {
 namespace {
 
 constexpr size_t FFT_N = 2048, FFT_M = 1024;
+constexpr size_t GEN_MIN_N = 32, GEN_MAX_N = (size_t)1 << 18;
 constexpr size_t OFF_T2 = 2 * 1024, OFF_CM = OFF_T2 + 2 * 64, OFF_CMI = OFF_CM + 2 * 16, TABLE_DOUBLES = OFF_CMI + 2 * 16;
 
 // exp(i pi e / 2048) for an integer exponent (reduced exactly mod 4096 first), in long double
@@ -69,8 +75,32 @@ std::vector<double> host_tables() {
   return h;
 }
 
+// generic plan tables: tw[n] = exp(i pi n / 2M), untw[n] = exp(-i pi n / 2M) / M, wm[t] = exp(-2 pi i t / M), each an
+// exact root of unity exp(i pi e / 2M) (e reduced mod 4M) rounded from long double
+std::vector<double> generic_tables(size_t m) {
+  std::vector<double> h(6 * m);
+  const long four_m = 4 * (long)m;
+  auto root = [&](long e, double* re, double* im) {
+    e %= four_m;
+    if (e < 0) e += four_m;
+    const long double a = 3.14159265358979323846264338327950288L * (long double)e / (long double)(2 * m);
+    *re = (double)cosl(a);
+    *im = (double)sinl(a);
+  };
+  for (size_t n = 0; n < m; ++n) {
+    root((long)n, &h[2 * n], &h[2 * n + 1]);
+    double re, im;
+    root(-(long)n, &re, &im);
+    h[2 * (m + n)] = re / (double)m;  // exact scaling (a power of two)
+    h[2 * (m + n) + 1] = im / (double)m;
+    root(-4L * (long)n, &h[2 * (2 * m + n)], &h[2 * (2 * m + n) + 1]);
+  }
+  return h;
+}
+
 int make_plan(size_t n, int device, mi_fft64_plan** out) {
-  if (n != FFT_N) return fail(MI_ERR_UNSUPPORTED, "this build runs the f64-FFT path for N = 2048");
+  if (n != FFT_N && (n < GEN_MIN_N || n > GEN_MAX_N))
+    return fail(MI_ERR_UNSUPPORTED, "the f64-FFT engines run 32 <= N <= 2^18");
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
     return fail(MI_ERR_INVALID_ARG, "device index out of range");
@@ -80,7 +110,8 @@ int make_plan(size_t n, int device, mi_fft64_plan** out) {
   if (!p) return fail(MI_ERR_OOM, "host allocation failed");
   p->n = n;
   p->device = device;
-  const std::vector<double> h = host_tables();
+  p->generic = n != FFT_N;
+  const std::vector<double> h = p->generic ? generic_tables(n / 2) : host_tables();
   hipError_t e = hipMalloc(&p->d_tables, h.size() * sizeof(double));
   if (e != hipSuccess) {
     delete p;
@@ -92,17 +123,32 @@ int make_plan(size_t n, int device, mi_fft64_plan** out) {
     delete p;
     return hip_fail(e, "table upload");
   }
-  p->tables = {p->d_tables, p->d_tables + OFF_T2, p->d_tables + OFF_CM, p->d_tables + OFF_CMI};
+  if (p->generic) {
+    const size_t m = n / 2;
+    p->gtables = {p->d_tables, p->d_tables + 2 * m, p->d_tables + 4 * m, __builtin_ctzll((unsigned long long)n)};
+  } else {
+    p->tables = {p->d_tables, p->d_tables + OFF_T2, p->d_tables + OFF_CM, p->d_tables + OFF_CMI};
+  }
   *out = p;
   return MI_OK;
 }
+
+constexpr int MAX_GENERIC_K = 16;
 
 int check_shape(const mi_fft64_plan* plan, int k, int base_log, int level) {
   if (!plan) return fail(MI_ERR_INVALID_ARG, "plan is NULL");
   if (level < 1 || base_log < 1 || base_log * level > 63)
     return fail(MI_ERR_INVALID_ARG, "decomposition must satisfy level >= 1, base_log >= 1, base_log*level < 64");
-  if (k < 1 || k > 2) return fail(MI_ERR_UNSUPPORTED, "the f64-FFT external product / PBS run for k in {1, 2}");
+  if (plan->generic ? (k < 1 || k > MAX_GENERIC_K) : (k < 1 || k > 2))
+    return fail(MI_ERR_UNSUPPORTED, "the f64-FFT external product / PBS run for k in {1, 2} at N = 2048, 1 <= k <= 16 "
+                                    "at other N");
   return MI_OK;
+}
+
+hipError_t reorder_any(const mi_fft64_plan* plan, double* out, const double* in, size_t polys, bool to_std,
+                       hipStream_t s) {
+  return plan->generic ? mi::launch_fftg_reorder(out, in, polys, to_std, plan->gtables, s)
+                       : mi::launch_fft64_reorder(out, in, polys, to_std, s);
 }
 
 }  // namespace
@@ -153,6 +199,11 @@ int mi_fft64_plan_info(const mi_fft64_plan* plan, size_t* n, int* device) {
 
 int mi_fft64_fourier_order(const mi_fft64_plan* plan, uint32_t* freq) {
   if (!plan || !freq) return fail(MI_ERR_INVALID_ARG, "NULL argument");
+  if (plan->generic) {
+    const int logn = plan->gtables.logn;
+    for (uint32_t p = 0; p < (uint32_t)(plan->n / 2); ++p) freq[p] = mi::fftg_frequency(logn, p);
+    return MI_OK;
+  }
   for (int r = 0; r < 16; ++r)
     for (int l = 0; l < 64; ++l) freq[r * 64 + l] = mi::fft64_frequency(r, l);
   return MI_OK;
@@ -165,7 +216,9 @@ int mi_fft64_forward_torus_batch(const mi_fft64_plan* plan, double* fourier, con
   if (!fourier || !standard) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
-  const hipError_t e = mi::launch_fft64_fwd_torus(fourier, standard, batch, plan->tables, (hipStream_t)stream);
+  const hipError_t e = plan->generic
+                           ? mi::launch_fftg_fwd_torus(fourier, standard, batch, plan->gtables, (hipStream_t)stream)
+                           : mi::launch_fft64_fwd_torus(fourier, standard, batch, plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 forward launch");
 }
 
@@ -177,7 +230,8 @@ int mi_fft64_backward_torus_batch(const mi_fft64_plan* plan, uint64_t* standard,
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
   const hipError_t e =
-      mi::launch_fft64_bwd_torus(standard, fourier, batch, add != 0, plan->tables, (hipStream_t)stream);
+      plan->generic ? mi::launch_fftg_bwd_torus(standard, fourier, batch, add != 0, plan->gtables, (hipStream_t)stream)
+                    : mi::launch_fft64_bwd_torus(standard, fourier, batch, add != 0, plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 backward launch");
 }
 
@@ -187,10 +241,11 @@ static int reorder(const mi_fft64_plan* plan, double* out, const double* in, siz
   if (polys == 0) return MI_OK;
   if (!out || !in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (polys > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "polynomial count too large");
-  if (out != in && out < in + polys * 2 * FFT_M && in < out + polys * 2 * FFT_M)
+  const size_t doubles = polys * plan->n;  // N / 2 complex per polynomial
+  if (out != in && out < in + doubles && in < out + doubles)
     return fail(MI_ERR_INVALID_ARG, "buffers overlap partially (in place must be out == in)");
   DeviceGuard g(plan->device);
-  const hipError_t e = mi::launch_fft64_reorder(out, in, polys, to_std, (hipStream_t)stream);
+  const hipError_t e = reorder_any(plan, out, in, polys, to_std, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 reorder launch");
 }
 
@@ -217,8 +272,11 @@ int mi_fft64_ext_product_batch(const mi_fft64_plan* plan, uint64_t* out_glwe, co
   if (!out_glwe || !in_glwe || !ggsw_fourier) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
-  const hipError_t e = mi::launch_fft64_ext_product(k, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_fourier,
-                                                    batch, base_log, level, plan->tables, (hipStream_t)stream);
+  const hipError_t e =
+      plan->generic ? mi::launch_fftg_ext_product(k, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_fourier,
+                                                  batch, base_log, level, plan->gtables, (hipStream_t)stream)
+                    : mi::launch_fft64_ext_product(k, false, out_glwe, const_cast<uint64_t*>(in_glwe), ggsw_fourier,
+                                                   batch, base_log, level, plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 external product launch");
 }
 
@@ -230,8 +288,11 @@ int mi_fft64_cmux_batch(const mi_fft64_plan* plan, uint64_t* ct0, uint64_t* ct1,
   if (!ct0 || !ct1 || !ggsw_fourier) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(plan->device);
-  const hipError_t e = mi::launch_fft64_ext_product(k, true, ct0, ct1, ggsw_fourier, batch, base_log, level,
-                                                    plan->tables, (hipStream_t)stream);
+  const hipError_t e =
+      plan->generic ? mi::launch_fftg_ext_product(k, true, ct0, ct1, ggsw_fourier, batch, base_log, level,
+                                                  plan->gtables, (hipStream_t)stream)
+                    : mi::launch_fft64_ext_product(k, true, ct0, ct1, ggsw_fourier, batch, base_log, level,
+                                                   plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 cmux launch");
 }
 
@@ -277,14 +338,15 @@ struct FourierLayout {
   size_t head, chunk_bytes, total;  // bytes before the first polynomial's length prefix, per polynomial, all
 };
 
-bool fourier_layout(uint64_t n_lwe, uint64_t glwe, uint64_t level, uint64_t base_log, bool ver, FourierLayout* L) {
+bool fourier_layout(uint64_t m, uint64_t n_lwe, uint64_t glwe, uint64_t level, uint64_t base_log, bool ver,
+                    FourierLayout* L) {
   uint64_t c;
   if (__builtin_mul_overflow(glwe, glwe, &c) || __builtin_mul_overflow(c, level, &c) ||
       __builtin_mul_overflow(c, n_lwe, &c))
     return false;
   L->n_lwe = n_lwe, L->glwe = glwe, L->base_log = base_log, L->level = level, L->chunks = c;
   L->head = (ver ? 8 : 0) + 24;
-  L->chunk_bytes = 8 + 16 * FFT_M;
+  L->chunk_bytes = 8 + 16 * m;
   size_t body;
   return !__builtin_mul_overflow((size_t)c, L->chunk_bytes, &body) &&
          !__builtin_add_overflow(body, L->head + 32 + (ver ? 16 : 0), &L->total);
@@ -310,11 +372,15 @@ uint8_t* wr64(uint8_t* p, uint64_t v) {
 }
 }  // namespace
 
-int mi_fft64_bsk_serialized_size(size_t n_lwe, int k, int level, int format, size_t* out_len) {
+int mi_fft64_bsk_serialized_size(size_t polynomial_size, size_t n_lwe, int k, int level, int format,
+                                 size_t* out_len) {
   if (!out_len) return fail(MI_ERR_INVALID_ARG, "out_len is NULL");
+  if (polynomial_size < 2 || (polynomial_size & (polynomial_size - 1)) || polynomial_size > ((size_t)1 << 40))
+    return fail(MI_ERR_INVALID_ARG, "polynomial size must be a power of two");
   if (format != MI_NTT_BSK_PLAIN && format != MI_NTT_BSK_VERSIONED) return fail(MI_ERR_INVALID_ARG, "unknown format");
   FourierLayout L;
-  if (k < 1 || level < 1 || !fourier_layout(n_lwe, (uint64_t)k + 1, (uint64_t)level, 0, format == MI_NTT_BSK_VERSIONED, &L))
+  if (k < 1 || level < 1 ||
+      !fourier_layout(polynomial_size / 2, n_lwe, (uint64_t)k + 1, (uint64_t)level, 0, format == MI_NTT_BSK_VERSIONED, &L))
     return fail(MI_ERR_INVALID_ARG, "Fourier BSK: bad sizes");
   *out_len = L.total;
   return MI_OK;
@@ -341,7 +407,7 @@ int mi_fft64_pbs_key_load(const mi_fft64_plan* plan, const uint8_t* bytes, size_
   if (chunks > ((uint64_t)1 << 40) || seq != chunks + 2)
     return fail(MI_ERR_INVALID_ARG, "Fourier BSK: sequence length is not 2 + the polynomial count");
   // the scalar fields sit after the polynomials
-  const size_t chunk_bytes = 8 + 16 * FFT_M, tail = 32 + (ver ? 16 : 0);
+  const size_t m = plan->n / 2, chunk_bytes = 8 + 16 * m, tail = 32 + (ver ? 16 : 0);
   if (len < off + 24 + tail || (len - off - 24 - tail) % chunk_bytes || (len - off - 24 - tail) / chunk_bytes != chunks)
     return fail(MI_ERR_INVALID_ARG, "Fourier BSK: length does not match the polynomial count");
   const uint8_t* t = bytes + off + 24 + chunks * chunk_bytes;
@@ -356,14 +422,14 @@ int mi_fft64_pbs_key_load(const mi_fft64_plan* plan, const uint8_t* bytes, size_
   }
   const uint64_t n_lwe = f[0], glwe = f[1], base_log = f[2], level = f[3];
   FourierLayout L;
-  if (glwe < 2 || glwe > 3 || level < 1 || level > 63 || base_log < 1 || base_log > 63 ||
-      !fourier_layout(n_lwe, glwe, level, base_log, ver, &L) || L.chunks != chunks)
+  if (glwe < 2 || glwe > MAX_GENERIC_K + 1 || level < 1 || level > 63 || base_log < 1 || base_log > 63 ||
+      !fourier_layout(m, n_lwe, glwe, level, base_log, ver, &L) || L.chunks != chunks)
     return fail(MI_ERR_INVALID_ARG, "Fourier BSK: the polynomial count does not match n_lwe x level x glwe_size^2");
   int st = check_shape(plan, (int)glwe - 1, (int)base_log, (int)level);
   if (st != MI_OK) return st;
   if (n_lwe == 0 || n_lwe > 0xFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "Fourier BSK: n_lwe out of range");
   for (uint64_t c = 0; c < chunks; ++c)
-    if (rd64(bytes + off + 24 + c * chunk_bytes) != FFT_M)
+    if (rd64(bytes + off + 24 + c * chunk_bytes) != m)
       return fail(MI_ERR_INVALID_ARG, "Fourier BSK: a polynomial does not hold N/2 values");
   auto* key = new (std::nothrow) mi_fft64_pbs_key;
   if (!key) return fail(MI_ERR_OOM, "host allocation failed");
@@ -374,16 +440,16 @@ int mi_fft64_pbs_key_load(const mi_fft64_plan* plan, const uint8_t* bytes, size_
   key->level = (int)level;
   DeviceGuard g(plan->device);
   const hipStream_t s = (hipStream_t)stream;
-  if (hipMalloc(&key->owned, chunks * 16 * FFT_M) != hipSuccess) {
+  if (hipMalloc(&key->owned, chunks * 16 * m) != hipSuccess) {
     delete key;
     return fail(MI_ERR_OOM, "Fourier key allocation failed");
   }
   // one strided upload skips the per-polynomial length prefixes, then the natural order becomes the engine's
-  hipError_t e = hipMemcpy2DAsync(key->owned, 16 * FFT_M, bytes + off + 24 + 8, chunk_bytes, 16 * FFT_M, chunks,
+  hipError_t e = hipMemcpy2DAsync(key->owned, 16 * m, bytes + off + 24 + 8, chunk_bytes, 16 * m, chunks,
                                   hipMemcpyHostToDevice, s);
   st = e == hipSuccess ? MI_OK : hip_fail(e, "Fourier key upload");
   if (st == MI_OK) {
-    e = mi::launch_fft64_reorder(key->owned, key->owned, chunks, false, s);
+    e = reorder_any(plan, key->owned, key->owned, chunks, false, s);
     st = e == hipSuccess ? MI_OK : hip_fail(e, "fft64 reorder launch");
   }
   if (st == MI_OK && (e = hipStreamSynchronize(s)) != hipSuccess) st = hip_fail(e, "Fourier key upload");
@@ -400,16 +466,17 @@ int mi_fft64_pbs_key_load(const mi_fft64_plan* plan, const uint8_t* bytes, size_
 int mi_fft64_pbs_key_write(const mi_fft64_pbs_key* key, int format, uint8_t* out, size_t out_len, void* stream) {
   if (!key || !out) return fail(MI_ERR_INVALID_ARG, "NULL argument");
   size_t need = 0;
-  int st = mi_fft64_bsk_serialized_size(key->n_lwe, key->k, key->level, format, &need);
+  int st = mi_fft64_bsk_serialized_size(key->plan->n, key->n_lwe, key->k, key->level, format, &need);
   if (st != MI_OK) return st;
   if (out_len != need) return fail(MI_ERR_INVALID_ARG, "output length is not the serialized size");
   const bool ver = format == MI_NTT_BSK_VERSIONED;
   FourierLayout L;
-  (void)fourier_layout(key->n_lwe, (uint64_t)key->k + 1, (uint64_t)key->level, (uint64_t)key->base_log, ver, &L);
+  const size_t m = key->plan->n / 2;
+  (void)fourier_layout(m, key->n_lwe, (uint64_t)key->k + 1, (uint64_t)key->level, (uint64_t)key->base_log, ver, &L);
   uint8_t* p = out;
   if (ver) p = wr32(wr32(p, 1), 0);
   p = wr64(wr64(wr64(p, L.chunks + 2), key->plan->n), L.chunks);
-  for (uint64_t c = 0; c < L.chunks; ++c) wr64(p + c * L.chunk_bytes, FFT_M);
+  for (uint64_t c = 0; c < L.chunks; ++c) wr64(p + c * L.chunk_bytes, m);
   uint8_t* t = p + L.chunks * L.chunk_bytes;
   for (const uint64_t v : {L.n_lwe, L.glwe, L.base_log, L.level}) {
     if (ver) t = wr32(t, 0);
@@ -418,10 +485,9 @@ int mi_fft64_pbs_key_write(const mi_fft64_pbs_key* key, int format, uint8_t* out
   DeviceGuard g(key->plan->device);
   const hipStream_t s = (hipStream_t)stream;
   double* tmp = nullptr;
-  if (hipMalloc(&tmp, L.chunks * 16 * FFT_M) != hipSuccess) return fail(MI_ERR_OOM, "scratch allocation failed");
-  hipError_t e = mi::launch_fft64_reorder(tmp, key->fbsk, L.chunks, true, s);
-  if (e == hipSuccess)
-    e = hipMemcpy2DAsync(p + 8, L.chunk_bytes, tmp, 16 * FFT_M, 16 * FFT_M, L.chunks, hipMemcpyDeviceToHost, s);
+  if (hipMalloc(&tmp, L.chunks * 16 * m) != hipSuccess) return fail(MI_ERR_OOM, "scratch allocation failed");
+  hipError_t e = reorder_any(key->plan, tmp, key->fbsk, L.chunks, true, s);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(p + 8, L.chunk_bytes, tmp, 16 * m, 16 * m, L.chunks, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   (void)hipFree(tmp);
   return e == hipSuccess ? MI_OK : hip_fail(e, "Fourier key download");
@@ -444,8 +510,12 @@ int mi_fft64_pbs_batch(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uin
   if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(key->plan->device);
-  const hipError_t e = mi::launch_fft64_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
-                                            key->level, ms_mode, key->plan->tables, (hipStream_t)stream);
+  const mi_fft64_plan* plan = key->plan;
+  const hipError_t e =
+      plan->generic ? mi::launch_fftg_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
+                                          key->level, ms_mode, plan->gtables, (hipStream_t)stream)
+                    : mi::launch_fft64_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
+                                           key->level, ms_mode, plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 pbs launch");
 }
 

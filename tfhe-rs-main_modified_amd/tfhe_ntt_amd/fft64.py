@@ -171,8 +171,8 @@ class FourierLweBootstrapKey:
         ``versionize()`` form), written by the library (``mi_fft64_pbs_key_write``: natural Fourier order, see
         ``fourier_bsk_format``)."""
         size = ctypes.c_size_t()
-        check(lib().mi_fft64_bsk_serialized_size(self.input_lwe_dimension, self.glwe_dimension, self.level,
-                                                 int(bool(versioned)), ctypes.byref(size)))
+        check(lib().mi_fft64_bsk_serialized_size(self.polynomial_size, self.input_lwe_dimension, self.glwe_dimension,
+                                                 self.level, int(bool(versioned)), ctypes.byref(size)))
         out = ctypes.create_string_buffer(size.value)
         check(lib().mi_fft64_pbs_key_write(self._h, int(bool(versioned)), out, size.value, self._stream()))
         return out.raw
@@ -185,8 +185,13 @@ class FourierLweBootstrapKey:
     @classmethod
     def load(cls, buf: bytes, versioned: bool = False, fft: Fft | None = None, device: int = 0):
         """A key from the reference's bytes through the library (``mi_fft64_pbs_key_load``: validated, one strided
-        upload, reordered into this engine's order on the device; the key owns that copy, ``fbsk`` is None)."""
-        fft = fft or Fft(2048, device)
+        upload, reordered into this engine's order on the device; the key owns that copy, ``fbsk`` is None).
+        Without ``fft`` the plan is the cached one of the polynomial size the bytes declare."""
+        if fft is None:
+            head = 8 if versioned else 0  # the list's u64 sequence length, then u64 polynomial_size
+            if len(buf) < head + 16:
+                raise ValueError("Fourier BSK: truncated")
+            fft = Fft(int.from_bytes(bytes(buf[head + 8:head + 16]), "little"), device)
         self = cls.__new__(cls)
         self.fft, self.fbsk = fft, None
         h = ctypes.c_void_p()
