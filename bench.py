@@ -367,6 +367,62 @@ def cpu_baseline_pbs_shape(name, seconds: float):
                       f"ntt64_bnf_pbs.rs, OpenMP {threads} threads"}
 
 
+def bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist):
+    """The default (f64-FFT) shortint PBS at another parameter set's shape: the shape-generic engine
+    (fft64_generic.hip: row / column four-step transforms, accumulators in HBM), synthetic Fourier key resident."""
+    F = eng.fft64
+    n, k, n_lwe, base_log, level, batch = SHAPE_LEGS[name]
+    fft = F.Fft(n, dev.index)
+    std = torch.empty((n_lwe, level, k + 1, k + 1, n), dtype=torch.int64, device=dev)
+    eng.fill_uniform(std, SEED + 93, 0)
+    fbsk = torch.empty((n_lwe, level, k + 1, k + 1, n // 2, 2), dtype=torch.float64, device=dev)
+    F.convert_standard_lwe_bootstrap_key_to_fourier(std, fbsk, fft)
+    del std
+    key = F.FourierLweBootstrapKey(fbsk, base_log, level, fft)
+    lut = torch.empty((k + 1, n), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 94, 0)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 95, 0)
+    out = torch.empty((batch, k * n + 1), dtype=torch.int64, device=dev)
+    run = lambda: F.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, key, F.MS_CENTERED)
+    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=1)
+    del key, fbsk
+    return {"metric": f"PBS/sec, f64-FFT PBS at the {name.upper()} shape", "value": world * batch * K / el,
+            "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms, "dtype": "f64",
+            "config": {"workload": f"programmable_bootstrap_lwe_ciphertext (tfhe-fft path), N={n} k={k} n={n_lwe} "
+                                   f"base_log={base_log} level={level} (shortint {name.upper()} shape), centered "
+                                   "modulus switch, synthetic key",
+                       "batch_per_gpu": batch, "engine": "shape-generic f64 engine (fft64_generic.hip)"},
+            "cpu_baseline": None}
+
+
+def cpu_baseline_pbs_fft(n, k, n_lwe, base_log, level, seconds: float, threads_note="numpy, 1 thread"):
+    """The numpy restatement of the f64 PBS (oracle/fft_oracle.py: np.fft transforms, one batch vectorised) on a
+    bounded sample: a batch of 8 ciphertexts over the first n' mask elements, timed and scaled to n (every CMUX
+    step costs the same)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import fft_oracle as FO
+
+    g = np.random.default_rng(SEED + 96)
+    sample, steps = 8, 4
+    bsk = g.integers(0, 2**64, size=(steps, level, k + 1, k + 1, n), dtype=np.uint64)
+    fbsk = FO.forward_as_torus(bsk)
+    lut = g.integers(0, 2**64, size=(k + 1, n), dtype=np.uint64)
+    lwe = g.integers(0, 2**64, size=(sample, steps + 1), dtype=np.uint64)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        FO.pbs(lwe, lut, fbsk, base_log, level)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    per_pbs = el / (reps * sample) * n_lwe / steps
+    return {"value": 1.0 / per_pbs, "unit": "PBS/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x {sample} PBS of {steps} CMUX steps (N={n}, k={k}, l={level}) in {el:.1f}s, scaled to "
+                      f"n={n_lwe} steps; numpy restatement of fft64_pbs.rs ({threads_note})"}
+
+
 def bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist):
     """The default shortint PBS, f64-FFT path (programmable_bootstrap_lwe_ciphertext, fft64_pbs.rs:924-1060)
     at PARAM_MESSAGE_2_CARRY_2's shape: native 2^64 ciphertexts, Fourier key (60 MB of complex f64) resident."""
@@ -857,6 +913,8 @@ def main():
         legs["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
         legs["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier, dist)
         legs["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist)
+        legs["pbs_shapes_fft"] = {name: bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist)
+                                  for name in SHAPE_LEGS}
         legs["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
@@ -968,6 +1026,11 @@ def main():
             out["bsk_conversion"]["cpu_baseline"] = cpu_baseline_bsk(min(args.cpu_seconds, 3.0))
             for name in ("message_1_carry_1", "message_3_carry_3"):  # 4_4: ~0.1 s per CMUX step per core, unbounded
                 out["pbs_shapes"][name]["cpu_baseline"] = cpu_baseline_pbs_shape(name, min(args.cpu_seconds, 4.0))
+            out["pbs_fft"]["cpu_baseline"] = cpu_baseline_pbs_fft(N, 1, PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL,
+                                                                  min(args.cpu_seconds, 3.0))
+            for name, (n_, k_, nl_, bl_, lv_, _) in SHAPE_LEGS.items():
+                out["pbs_shapes_fft"][name]["cpu_baseline"] = cpu_baseline_pbs_fft(n_, k_, nl_, bl_, lv_,
+                                                                                   min(args.cpu_seconds, 3.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

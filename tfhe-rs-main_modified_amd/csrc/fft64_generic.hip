@@ -233,8 +233,31 @@ struct AccSink {
 };
 
 // ---- row pass: one C-point DFT per row in LDS ---------------------------------------------------------------
-// radix-8 step on block size L = 2^LOGL: group g = (block, j0), elements block L + j0 + t L/8
-template <int LOGC, int LOGL, bool INV>
+// Register t of a radix-8 group needs W_L^(j0 bitrev(t)): all seven from the one table value W_L^j0 (six products,
+// a few ulps, far below the transform's own f64 error), instead of seven table reads.
+__device__ __forceinline__ void r8_twiddles(cplx (&w)[8], cplx w1) {
+  const cplx w2 = cmul(w1, w1), w3 = cmul(w1, w2), w4 = cmul(w2, w2);
+  w[1] = w4, w[2] = w2, w[3] = cmul(w2, w4), w[4] = w1, w[5] = cmul(w1, w4), w[6] = w3, w[7] = cmul(w3, w4);
+}
+
+// radix-8 butterfly of a group on block size L = 2^LOGL (forward: DFT8 then twiddles; INV: the conjugate transpose)
+template <int LOGL, bool INV>
+__device__ __forceinline__ void r8_core(cplx (&a)[8], uint32_t j0, const cplx* __restrict__ wm, uint32_t logm) {
+  cplx w[8];
+  r8_twiddles(w, wm[j0 << (logm - LOGL)]);
+  if constexpr (!INV) {
+    small_dft<8, false>(a);
+#pragma unroll
+    for (int t = 1; t < 8; ++t) a[t] = cmul(a[t], w[t]);
+  } else {
+#pragma unroll
+    for (int t = 1; t < 8; ++t) a[t] = cmulc(a[t], w[t]);
+    small_dft<8, true>(a);
+  }
+}
+
+// radix-8 step in LDS: group g = (block, j0), elements block L + j0 + t L/8
+template <int LOGL, bool INV>
 __device__ __forceinline__ void radix8_step(cplx* buf, int g, const cplx* __restrict__ wm, uint32_t logm) {
   constexpr int SL = LOGL - 3;
   const uint32_t j0 = (uint32_t)g & ((1u << SL) - 1u);
@@ -242,15 +265,7 @@ __device__ __forceinline__ void radix8_step(cplx* buf, int g, const cplx* __rest
   cplx a[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) a[t] = buf[base + ((uint32_t)t << SL)];
-  if constexpr (!INV) {
-    small_dft<8, false>(a);
-#pragma unroll
-    for (int t = 1; t < 8; ++t) a[t] = cmul(a[t], wm[(j0 * brev(t, 3)) << (logm - LOGL)]);  // W_L^(j0 bitrev(t))
-  } else {
-#pragma unroll
-    for (int t = 1; t < 8; ++t) a[t] = cmulc(a[t], wm[(j0 * brev(t, 3)) << (logm - LOGL)]);
-    small_dft<8, true>(a);
-  }
+  r8_core<LOGL, INV>(a, j0, wm, logm);
 #pragma unroll
   for (int t = 0; t < 8; ++t) buf[base + ((uint32_t)t << SL)] = a[t];
 }
@@ -272,18 +287,23 @@ __device__ __forceinline__ void rem_step(cplx* buf, int g) {
   }
 }
 
-template <int LOGC, int I, bool INV>
+// steps I = FIRST .. END - 1 of the S8 radix-8 steps, each followed by a barrier; step I runs at LOGL = LOGC - 3 I
+// (forward) or at LOGL = LOGC - 3 (S8 - 1 - I) (inverse: the same steps in reverse order)
+template <int LOGC, int I, int END, bool INV>
 __device__ __forceinline__ void radix8_steps(cplx* buf, int g, const cplx* __restrict__ wm, uint32_t logm) {
-  // forward: I = 0 .. S8 - 1 at LOGL = LOGC - 3 I; inverse: the same steps in reverse order
   using G = RowGeom<LOGC>;
-  if constexpr (I < G::S8) {
+  if constexpr (I < END) {
     constexpr int STEP = INV ? (G::S8 - 1 - I) : I;
-    radix8_step<LOGC, LOGC - 3 * STEP, INV>(buf, g, wm, logm);
+    radix8_step<LOGC - 3 * STEP, INV>(buf, g, wm, logm);
     __syncthreads();
-    radix8_steps<LOGC, I + 1, INV>(buf, g, wm, logm);
+    radix8_steps<LOGC, I + 1, END, INV>(buf, g, wm, logm);
   }
 }
 
+// One row per TPR threads.  The radix-8 step on the whole row (L = C) touches g + t C/8, t < 8 — the coalesced
+// pattern of a row copy — so the forward takes its first step straight from the source and the inverse stores its
+// last step straight to the sink; the other steps run in LDS, and the forward's result (bit-reversed) and the
+// inverse's input are copied out / in coalesced.
 template <int LOGC, bool INV, class Src, class Dst>
 __global__ __launch_bounds__(RowGeom<LOGC>::T) void rows_kernel(Src src, Dst dst, uint64_t rows,
                                                                const cplx* __restrict__ wm, uint32_t logm) {
@@ -293,30 +313,45 @@ __global__ __launch_bounds__(RowGeom<LOGC>::T) void rows_kernel(Src src, Dst dst
   const uint64_t row = (uint64_t)blockIdx.x * G::RPW + rl;
   const bool ok = row < rows;  // every thread takes part in the barriers
   cplx* buf = lds + rl * G::C;
+  if constexpr (!INV) {
+    cplx a[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t x = (uint32_t)(g + j * G::TPR);
-    buf[x] = ok ? src.load(row, x) : cplx{0.0, 0.0};
-  }
-  __syncthreads();
-  if constexpr (INV) {
-    if constexpr (G::REM) {
-      rem_step<LOGC, true>(buf, g);
-      __syncthreads();
-    }
-    radix8_steps<LOGC, 0, true>(buf, g, wm, logm);
-  } else {
-    radix8_steps<LOGC, 0, false>(buf, g, wm, logm);
+    for (int t = 0; t < 8; ++t) a[t] = ok ? src.load(row, (uint32_t)(g + t * G::TPR)) : cplx{0.0, 0.0};
+    r8_core<LOGC, false>(a, (uint32_t)g, wm, logm);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) buf[g + t * G::TPR] = a[t];
+    __syncthreads();
+    radix8_steps<LOGC, 1, G::S8, false>(buf, g, wm, logm);
     if constexpr (G::REM) {
       rem_step<LOGC, false>(buf, g);
       __syncthreads();
     }
-  }
-  if (ok) {
+    if (ok) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t x = (uint32_t)(g + j * G::TPR);
+        dst.store(row, x, buf[x]);
+      }
+    }
+  } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t x = (uint32_t)(g + j * G::TPR);
-      dst.store(row, x, buf[x]);
+      buf[x] = ok ? src.load(row, x) : cplx{0.0, 0.0};
+    }
+    __syncthreads();
+    if constexpr (G::REM) {
+      rem_step<LOGC, true>(buf, g);
+      __syncthreads();
+    }
+    radix8_steps<LOGC, 0, G::S8 - 1, true>(buf, g, wm, logm);
+    cplx a[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) a[t] = buf[g + t * G::TPR];
+    r8_core<LOGC, true>(a, (uint32_t)g, wm, logm);
+    if (ok) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) dst.store(row, (uint32_t)(g + t * G::TPR), a[t]);
     }
   }
 }
