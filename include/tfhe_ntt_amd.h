@@ -42,7 +42,9 @@ const char *mi_last_error_message(void);
  * returns None for N < 16, N not a power of two, p not prime, or no 2N-th root; here those are
  * MI_ERR_INVALID_ARG / MI_ERR_NOT_PRIME / MI_ERR_NO_ROOT.  Twiddles are built on the host exactly
  * as init_negacyclic_twiddles (prime64.rs:159-204) and uploaded to `device`.  A plan is immutable
- * after creation and may be shared by any number of streams / host threads. */
+ * after creation and may be shared by any number of streams / host threads.  Sizes 16 <= N <= 2^31
+ * (the Solinas field's 2N-th roots end at 2N = 2^32, roots.rs:96-107); N > 2^14 runs as passes of
+ * top stages through HBM plus 2^14-element blocks. */
 int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan **out_plan);
 int mi_ntt64_plan_destroy(mi_ntt64_plan *plan);
 

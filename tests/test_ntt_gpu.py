@@ -51,6 +51,32 @@ def test_fwd_inv_all_sizes_solinas(engine, oracle, logn):
     assert np.array_equal(host(t), ora.inv(x, threads=8))
 
 
+@pytest.mark.parametrize("logn,batch", [(19, 2), (20, 1), (21, 1), (22, 1), (24, 1)])
+def test_fwd_inv_beyond_2_18(engine, oracle, logn, batch):
+    """N = 2^19 ... 2^24 (plans past the reference's root table, find_root_solinas_64, roots.rs:96-107):
+    k = logn - 14 top stages run in passes of at most 4 (s0 = 0, 4, ...) before the 2^14 blocks; bit-exact vs the
+    oracle both directions, plus a non-Solinas prime with 2^22 | p - 1 at N = 2^21."""
+    n = 1 << logn
+    plan, ora = engine.Plan.try_new(n, SOLINAS_P), oracle.Plan.try_new(n, SOLINAS_P)
+    x = oracle.fill_uniform(0x1A26E + logn, SOLINAS_P, batch * n).reshape(batch, n)
+    t = dev(x)
+    plan.fwd(t)
+    fx = ora.fwd(x, threads=16)
+    assert np.array_equal(host(t), fx)
+    plan.inv(t)
+    assert np.array_equal(host(t), ora.inv(fx, threads=16))
+    if logn == 21:
+        p = oracle.largest_prime_in_arithmetic_progression64(1 << 22, 1, 1 << 62, 1 << 63)
+        plan, ora = engine.Plan.try_new(n, p), oracle.Plan.try_new(n, p)
+        x = oracle.fill_uniform(0x1A26F, p, n).reshape(1, n)
+        t = dev(x)
+        plan.fwd(t)
+        assert np.array_equal(host(t), ora.fwd(x, threads=16))
+        t = dev(x)
+        plan.inv(t)
+        assert np.array_equal(host(t), ora.inv(x, threads=16))
+
+
 @pytest.mark.parametrize("name", ["p64", "p63", "p62", "p50", "p30"])
 @pytest.mark.parametrize("logn", [4, 5, 10, 11, 12, 15, 16])
 def test_fwd_inv_other_primes(engine, oracle, name, logn):

@@ -64,8 +64,9 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   auto root = mi::host::find_primitive_root64(p, 2 * (u64)n);
   if (!root) return fail(MI_ERR_NO_ROOT, "no primitive 2N-th root of unity");
   const int logn = __builtin_ctzll(n);
-  // up to 2^18: N > 2^14 runs as top stages + 2^(logn - 14) blocks (ntt64_kernels.hip dispatch_large)
-  if (logn > 18) return fail(MI_ERR_UNSUPPORTED, "this build runs N <= 262144 on device");
+  // N > 2^14 runs as passes of <= 4 top stages + 2^(logn - 14) blocks (ntt64_kernels.hip dispatch_large); the
+  // reference's Solinas root exists up to 2N = 2^32 (roots.rs:96-107), other primes need 2N | p - 1 (checked above)
+  if (logn > 31) return fail(MI_ERR_UNSUPPORTED, "this build runs N <= 2^31 on device");
 
   mi_ntt64_plan* plan = new (std::nothrow) mi_ntt64_plan;
   if (!plan) return fail(MI_ERR_OOM, "host allocation failed");

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "ntt64_regs.hpp"
@@ -71,21 +73,27 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Large-N plans (N > 2^14, beyond one workgroup's registers): the transform is split in two passes
-// through memory, the decomposition the reference's depth-first recursion also uses
-// (generic_solinas.rs:931-1032: top stages on the whole polynomial, then independent halves).
-//   forward = K top CT stages on strided columns (this kernel), then 2^K independent blocks of
-//             2^14 with the remaining stages (ntt_window_kernel<SUB>, twiddle multiplier 2^K + b);
-//   inverse = the blocks' GS stages first, then the K bottom GS stages on strided columns.
-// Thread j of polynomial q owns the 2^K elements j + i N / 2^K (i < 2^K): coalesced across j.
+// Large-N plans (N > 2^14, beyond one workgroup's registers): the transform is split into passes through memory, the
+// decomposition the reference's depth-first recursion also uses (generic_solinas.rs:931-1032: top stages on the whole
+// polynomial, then independent halves).
+//   forward = the k = logn - 14 top CT stages in passes of at most 4 stages on strided columns (this kernel), then
+//             2^k independent blocks of 2^14 with the remaining stages (ntt_window_kernel<SUB>, multiplier 2^k + b);
+//   inverse = the blocks' GS stages first, then the top GS passes in reverse order.
+// A pass that starts after S0 stages works inside each of the 2^S0 blocks of 2^(logn - S0) elements the stages above
+// left independent: thread j of block b owns the 2^K elements b 2^(logn - S0) + j + i cols (i < 2^K, cols =
+// 2^(logn - S0 - K), coalesced across j), and its local stage s (m = 2^s local groups) reads the table at
+// (2^S0 + b) 2^s + g, the global stage S0 + s's twiddle of the block's group.
 template <int K, bool FWD, class Mod, class IO>
-__global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn,
+__global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn, uint32_t s0,
                                                       const u64* __restrict__ tw, Mod mod) {
   constexpr int R = 1 << K;
-  const uint64_t cols = (uint64_t)1 << (logn - K);
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= cols) return;
-  IO* __restrict__ src = data + (uint64_t)blockIdx.y * stride + j;
+  const uint32_t logc = logn - s0 - K;
+  const uint64_t cols = (uint64_t)1 << logc;
+  const uint64_t jg = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (jg >= ((uint64_t)1 << (logn - K))) return;
+  const uint64_t blk = jg >> logc, j = jg & (cols - 1);
+  const uint64_t twc = ((uint64_t)1 << s0) + blk;
+  IO* __restrict__ src = data + (uint64_t)blockIdx.y * stride + (blk << (logn - s0)) + j;
   u64 x[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = (u64)src[i * cols];
@@ -96,7 +104,7 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (i & d) continue;
-      const u64 wv = tw[m + (i >> (K - s))];
+      const u64 wv = tw[twc * m + (uint64_t)(i >> (K - s))];
       if (FWD) {
         const u64 z = mod.mul(x[i + d], wv);
         const u64 a = x[i];
@@ -127,14 +135,15 @@ static hipError_t launch_window(IO* data, size_t batch, size_t stride, const u64
 }
 
 constexpr int SUB_LOGN = 14;  // block size of the large-N second pass
+constexpr int MAX_LOGN = 31;  // 2N-th roots of unity exist in the Solinas field up to 2N = 2^32
 
 template <int K, bool FWD, class Mod, class IO>
-static hipError_t launch_top(IO* data, size_t batch, size_t stride, int logn, const u64* tw, const Mod& mod,
+static hipError_t launch_top(IO* data, size_t batch, size_t stride, int logn, int s0, const u64* tw, const Mod& mod,
                              hipStream_t s) {
-  const uint64_t cols = (uint64_t)1 << (logn - K);
-  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)batch);
+  const uint64_t threads = (uint64_t)1 << (logn - K);
+  const dim3 grid((unsigned)((threads + 255) / 256), (unsigned)batch);
   hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Mod, IO>), grid, dim3(256), 0, s, data, (uint64_t)stride, (uint32_t)logn,
-                     tw, mod);
+                     (uint32_t)s0, tw, mod);
   return hipGetLastError();
 }
 
@@ -142,22 +151,34 @@ template <bool FWD, class Mod, class IO>
 static hipError_t dispatch_large(int logn, IO* data, size_t batch, size_t stride, const u64* tw, const Mod& mod,
                                  hipStream_t s) {
   const int k = logn - SUB_LOGN;
-  if (k < 1 || k > 4) return hipErrorInvalidValue;
-  if (batch > 65535) {  // the top pass puts polynomials on grid.y
-    for (size_t b0 = 0; b0 < batch; b0 += 65535) {
-      const size_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+  if (k < 1 || logn > MAX_LOGN) return hipErrorInvalidValue;
+  // the top passes put polynomials on grid.y, the blocks pass batch x 2^k workgroups on grid.x
+  const size_t max_batch = std::min<size_t>(65535, ((size_t)1 << 31) >> k);
+  if (batch > max_batch) {
+    for (size_t b0 = 0; b0 < batch; b0 += max_batch) {
+      const size_t nb = batch - b0 < max_batch ? batch - b0 : max_batch;
       const hipError_t e = dispatch_large<FWD>(logn, data + b0 * stride, nb, stride, tw, mod, s);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
   }
-  auto top = [&]() -> hipError_t {
-    switch (k) {
-      case 1: return launch_top<1, FWD>(data, batch, stride, logn, tw, mod, s);
-      case 2: return launch_top<2, FWD>(data, batch, stride, logn, tw, mod, s);
-      case 3: return launch_top<3, FWD>(data, batch, stride, logn, tw, mod, s);
-      default: return launch_top<4, FWD>(data, batch, stride, logn, tw, mod, s);
+  auto top = [&](int s0, int kk) -> hipError_t {
+    switch (kk) {
+      case 1: return launch_top<1, FWD>(data, batch, stride, logn, s0, tw, mod, s);
+      case 2: return launch_top<2, FWD>(data, batch, stride, logn, s0, tw, mod, s);
+      case 3: return launch_top<3, FWD>(data, batch, stride, logn, s0, tw, mod, s);
+      default: return launch_top<4, FWD>(data, batch, stride, logn, s0, tw, mod, s);
     }
+  };
+  auto tops = [&]() -> hipError_t {  // passes of <= 4 stages: s0 = 0, 4, 8, ...; the inverse runs them in reverse
+    const int passes = (k + 3) / 4;
+    for (int q = 0; q < passes; ++q) {
+      const int pi = FWD ? q : passes - 1 - q;
+      const int s0 = 4 * pi, kk = std::min(4, k - s0);
+      const hipError_t e = top(s0, kk);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   };
   auto blocks = [&]() -> hipError_t {
     using G = Geo<SUB_LOGN, 4>;
@@ -166,8 +187,8 @@ static hipError_t dispatch_large(int logn, IO* data, size_t batch, size_t stride
                        (uint32_t)batch, (uint64_t)stride, tw, mod, (uint32_t)k);
     return hipGetLastError();
   };
-  hipError_t e = FWD ? top() : blocks();
-  if (e == hipSuccess) e = FWD ? blocks() : top();
+  hipError_t e = FWD ? tops() : blocks();
+  if (e == hipSuccess) e = FWD ? blocks() : tops();
   return e;
 }
 
