@@ -26,9 +26,10 @@ def test_host_single_poly_bit_exact(engine, oracle, n):
 
 
 def test_host_batches_grow_the_staging_slot(engine, oracle):
-    """A small call, then a larger one (the slot's buffers grow), then a small one again."""
+    """A small call, then larger ones (the slot's buffers grow), then a small one again; batch 128 (2 MiB) is the
+    last in-place call on the mapped host buffer, 129 the first staged one (c_api.cpp ZERO_COPY_BYTES)."""
     plan, ora = engine.Plan.try_new(2048, P), oracle.Plan.try_new(2048, P)
-    for batch in (1, 64, 3):
+    for batch in (1, 64, 128, 129, 3):
         x = oracle.fill_uniform(0xB0 + batch, P, batch * 2048).reshape(batch, 2048)
         y = x.copy()
         plan.fwd(y)
@@ -85,3 +86,16 @@ def test_host_call_does_not_wait_for_other_streams(engine):
     plan.fwd(x)
     assert not done.query(), "the host call waited for an unrelated stream"
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n,prime", [(32768, "solinas"), (1024, "p62"), (64, "solinas")])
+def test_host_other_plans(engine, oracle, n, prime):
+    """The host form over the large-N passes (N = 2^15 on the mapped buffer) and a Montgomery-path prime."""
+    p = P if prime == "solinas" else oracle.largest_prime_in_arithmetic_progression64(1 << 16, 1, 1 << 61, 1 << 62)
+    plan, ora = engine.Plan.try_new(n, p), oracle.Plan.try_new(n, p)
+    x = oracle.fill_uniform(0xD00D + n, p, 2 * n).reshape(2, n)
+    y = x.copy()
+    plan.fwd(y)
+    assert np.array_equal(y, ora.fwd(x))
+    plan.inv(y)
+    assert np.array_equal(y, ora.inv(ora.fwd(x)))

@@ -335,10 +335,12 @@ int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan* plan, uint64_t* acc, cons
 
 // The `&mut [u64]` host form (Plan::fwd / Plan::inv on a caller slice, as Ntt64View::forward / add_backward call
 // it per polynomial, ntt64.rs:89-137).  Each call borrows a staging slot of the plan's device from a process-wide
-// pool: a private non-blocking stream, a device buffer and a pinned host buffer, all grown on demand and reused.
-// A call is memcpy -> async H2D -> transform -> async D2H -> wait on that stream only -> memcpy: no allocation in
-// the steady state, and nothing else of the process is synchronised (no hipDeviceSynchronize), so concurrent
-// callers (rayon workers) each run on their own slot and stream.
+// pool: a private non-blocking stream, a device buffer and a mapped, coherent pinned host buffer, all grown on
+// demand and reused.  Up to ZERO_COPY_BYTES the transform runs in place on the pinned buffer itself (the kernel
+// reads and writes host memory over PCIe: one launch and one wait per call instead of two copies around the
+// launch); above it a call is memcpy -> async H2D -> transform -> async D2H -> wait -> memcpy.  No allocation in the
+// steady state, and nothing else of the process is synchronised (no hipDeviceSynchronize), so concurrent callers
+// (rayon workers) each run on their own slot and stream.
 }  // extern "C"
 
 namespace {
@@ -346,9 +348,15 @@ struct HostSlot {
   int device = 0;
   hipStream_t stream = nullptr;
   u64* dbuf = nullptr;
-  u64* hbuf = nullptr;  // pinned
-  size_t cap = 0;       // u64 elements of both buffers
+  u64* hbuf = nullptr;   // pinned, mapped, coherent
+  u64* hdev = nullptr;   // hbuf's device address
+  size_t cap = 0;        // u64 elements of both buffers
 };
+
+// in-place transform on the mapped host buffer up to this size (profiles/r3/host_path_zero_copy.json against the
+// staged rows of profiles/r3/bench_line_driver_cmd.json: faster up to 2 MiB per call — 39.8 vs 46.8 us for one
+// N = 1024 round trip, 51.6 vs 87.5 us at 16 polynomials — and level with the staged call at 4 MiB)
+constexpr size_t ZERO_COPY_BYTES = (size_t)2 << 20;
 
 struct HostSlotPool {
   std::mutex mu;
@@ -393,10 +401,12 @@ hipError_t slot_reserve(HostSlot* s, size_t elems) {
   hipError_t e = hipStreamSynchronize(s->stream);
   if (s->dbuf) (void)hipFree(s->dbuf);
   if (s->hbuf) (void)hipHostFree(s->hbuf);
-  s->dbuf = s->hbuf = nullptr;
+  s->dbuf = s->hbuf = s->hdev = nullptr;
   s->cap = 0;
   if (e == hipSuccess) e = hipMalloc(&s->dbuf, elems * sizeof(u64));
-  if (e == hipSuccess) e = hipHostMalloc(&s->hbuf, elems * sizeof(u64), hipHostMallocDefault);
+  if (e == hipSuccess)
+    e = hipHostMalloc(&s->hbuf, elems * sizeof(u64), hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->hdev, s->hbuf, 0);
   if (e == hipSuccess) s->cap = elems;
   return e;
 }
@@ -418,9 +428,13 @@ static int run_host(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t b
     return fail(MI_ERR_OOM, std::string("staging buffer allocation failed: ") + hipGetErrorString(e));
   }
   std::memcpy(slot->hbuf, buf, bytes);
-  e = hipMemcpyAsync(slot->dbuf, slot->hbuf, bytes, hipMemcpyHostToDevice, slot->stream);
-  if (e == hipSuccess) e = launch_transform(fwd, plan, slot->dbuf, batch, plan->n, slot->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(slot->hbuf, slot->dbuf, bytes, hipMemcpyDeviceToHost, slot->stream);
+  if (bytes <= ZERO_COPY_BYTES) {
+    e = launch_transform(fwd, plan, slot->hdev, batch, plan->n, slot->stream);
+  } else {
+    e = hipMemcpyAsync(slot->dbuf, slot->hbuf, bytes, hipMemcpyHostToDevice, slot->stream);
+    if (e == hipSuccess) e = launch_transform(fwd, plan, slot->dbuf, batch, plan->n, slot->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(slot->hbuf, slot->dbuf, bytes, hipMemcpyDeviceToHost, slot->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(slot->stream);
   if (e == hipSuccess) std::memcpy(buf, slot->hbuf, bytes);
   release_slot(slot);
