@@ -292,12 +292,13 @@ def test_pbs_solinas_reference_params(engine, plan, ctx, oracle):
     assert np.array_equal(got[:4], want)
 
 
-def test_pbs_config4_full_batch_real_keys(engine, plan, ctx):
+def test_pbs_config4_full_batch_real_keys(engine, plan, ctx, oracle):
     """Config 4 at its full size: 4096 BNF PBS at the PARAM_MESSAGE_2_CARRY_2 shape (n = 918, N = 2048,
     B = 2^23, l = 1, 2+2-bit messages with padding, TUniform noise bounds 2^45 LWE / 2^17 GLWE as ks_pbs.rs:29-47)
     under real keys, key converted on the GPU.  Size-independent property over the whole batch: every output
-    decrypts to f(m) (lwe_programmable_bootstrapping.rs:1002-1163); bit-exact vs the oracle on 64 ciphertexts
-    spread over the batch (first, last and every 64th)."""
+    decrypts to f(m) (lwe_programmable_bootstrapping.rs:1002-1163); bit-exact vs the oracle on ALL 4096 outputs
+    (the oracle's blind rotation with its AVX-512 transform restatement, itself checked equal to the scalar
+    restatement on 8 of them first)."""
     n_lwe, base_log, level, msg_mod, batch = 918, 23, 1, 16, 4096
     delta = (1 << 63) // msg_mod
     g = H.rng(4096918)
@@ -321,9 +322,40 @@ def test_pbs_config4_full_batch_real_keys(engine, plan, ctx):
     with np.errstate(over="ignore"):
         dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
     assert np.array_equal(dec, np.array([f(int(m)) for m in msgs], np.uint64))
-    idx = np.unique(np.concatenate([np.arange(0, batch, 64), [batch - 1]]))
-    want = ctx.pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, threads=16)
-    assert np.array_equal(got[idx], want)
+    idx = np.array([0, 1, 511, 1024, 2047, 2048, 3071, batch - 1])
+    scalar = ctx.pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, threads=8)
+    assert np.array_equal(got[idx], scalar)
+    oracle.pbs_set_fast_ntt(True)
+    try:
+        fast8 = ctx.pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, threads=8)
+        assert np.array_equal(fast8, scalar)
+        want = ctx.pbs_batch_bnf(lwe, lut.reshape(-1), nbsk.reshape(-1), K, base_log, level, threads=16)
+    finally:
+        oracle.pbs_set_fast_ntt(False)
+    assert np.array_equal(got, want)
+
+
+def test_external_product_config3_full_batch(engine, plan, ctx):
+    """Config 3 at its full size: 8192 BNF external products (N = 2048, k = 1, B = 2^23, l = 1) against one shared
+    GGSW, the bench's workload, bit-exact vs the oracle on every product; then the same batch as CMUX."""
+    batch, base_log, level = 8192, 23, 1
+    g = H.rng(8192 + 3)
+    ggsw = rand_q(g, (level, K + 1, K + 1, N), P)
+    glwe = rand_q(g, (batch, K + 1, N), 0)
+    out0 = rand_q(g, (batch, K + 1, N), 0)
+    want = ctx.ext_product_batch_bnf(out0.reshape(-1), ggsw.reshape(-1), glwe.reshape(-1), K, base_log, level,
+                                     threads=16).reshape(batch, K + 1, N)
+    out, tg = dev(out0), dev(glwe)
+    engine.ntt64_pbs.add_external_product_ntt64_bnf_assign(plan, out, dev(ggsw), tg, base_log, level)
+    assert np.array_equal(host(out), want)
+    t0, t1 = dev(out0), dev(glwe)
+    engine.ntt64_pbs.cmux_ntt64_bnf_assign(plan, t0, t1, dev(ggsw), base_log, level)
+    with np.errstate(over="ignore"):
+        diff = glwe - out0
+    assert np.array_equal(host(t1), diff)
+    want_c = ctx.ext_product_batch_bnf(out0.reshape(-1), ggsw.reshape(-1), diff.reshape(-1), K, base_log, level,
+                                       threads=16).reshape(batch, K + 1, N)
+    assert np.array_equal(host(t0), want_c)
 
 
 @pytest.mark.parametrize("batch", [1, 37])
