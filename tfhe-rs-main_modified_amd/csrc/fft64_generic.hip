@@ -561,23 +561,6 @@ hipError_t inverse(const Geo& g, Src src, Sink sink, cplx* tmp, uint64_t polys, 
   return cols_inv(g.logr, sink, tmp, polys, g.logc, g.wm, s);
 }
 
-// A producer / consumer as its own streaming pass (grid-stride, full occupancy) instead of fused into the row
-// kernel's loads: out[p M + n] = src.load(p, n)
-template <class Src>
-__global__ __launch_bounds__(256) void stream_kernel(Src src, cplx* __restrict__ out, uint64_t polys, uint32_t logm) {
-  const uint32_t mmask = (1u << logm) - 1u;
-  for (uint64_t i = gs_start(); i < (polys << logm); i += gs_stride()) out[i] = src.load(i >> logm, (uint32_t)i & mmask);
-}
-template <class Src>
-hipError_t stream(Src src, cplx* out, uint64_t polys, uint32_t logm, hipStream_t s) {
-  hipLaunchKernelGGL((stream_kernel<Src>), dim3(blocks_for(polys << logm)), dim3(256), 0, s, src, out, polys, logm);
-  return hipGetLastError();
-}
-#ifndef MI_FFTG_STREAM
-#define MI_FFTG_STREAM 1
-#endif
-constexpr bool STREAM_R1 = MI_FFTG_STREAM;  // R = 1 PBS: digits and MAC as streaming passes
-
 // items per chunk: digits (level (k + 1) M complex), products (R > 1: (k + 1) M complex) and accumulators stay
 // below ~1 GiB of scratch
 inline size_t chunk_for(const Geo& g, uint32_t kp1, uint32_t level, size_t batch) {
@@ -693,13 +676,13 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
   const uint32_t kp1 = (uint32_t)k + 1, lv = (uint32_t)level;
   const size_t per = (size_t)kp1 << g.logn;
   const size_t chunk = chunk_for(g, kp1, lv, batch);
-  const size_t dig = ((chunk * lv * kp1) << g.logm), prod = (g.logr || STREAM_R1) ? ((chunk * kp1) << g.logm) : 0;
+  const size_t dig = ((chunk * lv * kp1) << g.logm), prod = g.logr ? ((chunk * kp1) << g.logm) : 0;
   const size_t acc_u64 = chunk * per;
   cplx* scratch = nullptr;
   hipError_t e = hipMallocAsync((void**)&scratch, (dig + prod) * sizeof(cplx) + (acc_u64 + chunk) * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
   cplx* d = scratch;
-  cplx* y = prod ? scratch + dig : nullptr;
+  cplx* y = g.logr ? scratch + dig : nullptr;
   uint64_t* acc = reinterpret_cast<uint64_t*>(scratch + dig + prod);
   uint64_t* corr = acc + acc_u64;
   const cplx* key = reinterpret_cast<const cplx*>(fbsk);
@@ -713,20 +696,11 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
                        ms_mode == 1 ? (const uint64_t*)corr : nullptr, (uint32_t)n_lwe, nb, g.logn, kp1, ms_mode);
     if ((e = hipGetLastError()) != hipSuccess) break;
     for (uint32_t i = 0; i < (uint32_t)n_lwe && e == hipSuccess; ++i) {
-      const RotDigitSrc rot{acc, in, g.tw, g.logn, kp1, lv, (uint32_t)n_lwe, i, base_log, ms_mode};
-      const MacSrc mac{d, key + i * ggsw_len, g.logm, g.logc, g.logr, kp1, lv};
-      const AccSink sink{acc, g.untw, g.logn};
-      const uint64_t n_dig = (uint64_t)nb * lv * kp1, n_out = (uint64_t)nb * kp1;
-      if (STREAM_R1 && g.logr == 0) {
-        e = stream(rot, d, n_dig, g.logm, s);
-        if (e == hipSuccess) e = rows<false>(g.logc, PlainIO{d, g.logc}, PlainIO{d, g.logc}, n_dig, g.wm, g.logm, s);
-        if (e == hipSuccess) e = stream(mac, y, n_out, g.logm, s);
-        if (e == hipSuccess) e = rows<true>(g.logc, PlainIO{y, g.logc}, sink, n_out, g.wm, g.logm, s);
-        continue;
-      }
-      e = forward(g, rot, d, n_dig, s);
+      e = forward(g, RotDigitSrc{acc, in, g.tw, g.logn, kp1, lv, (uint32_t)n_lwe, i, base_log, ms_mode}, d,
+                  (uint64_t)nb * lv * kp1, s);
       if (e != hipSuccess) break;
-      e = inverse(g, mac, sink, y, n_out, s);
+      e = inverse(g, MacSrc{d, key + i * ggsw_len, g.logm, g.logc, g.logr, kp1, lv}, AccSink{acc, g.untw, g.logn}, y,
+                  (uint64_t)nb * kp1, s);
     }
     if (e != hipSuccess) break;
     const uint64_t outs = (uint64_t)nb * (((uint64_t)k << g.logn) + 1);
