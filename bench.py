@@ -988,6 +988,7 @@ def main():
             "order": "cold_start (W + K steps from idle) -> component legs (external product last) -> headline "
                      "(W + K steps) -> steady_state",
             "hip_runtime": eng._lib.hip_runtimes(),
+            "build": eng._lib.build_provenance(),
         },
         "kernels": {"timed_launch_ms": launch_ms, "fwd_ms": fwd_ms, "inv_ms": inv_ms,
                     "note": "timed_launch_ms: HIP events around the timed region / (2 K launches); "

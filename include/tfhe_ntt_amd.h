@@ -36,6 +36,10 @@ typedef struct mi_ntt64_plan mi_ntt64_plan;
 /* Human-readable text for a status code, and the detail of the last error on this thread. */
 const char *mi_status_string(int status);
 const char *mi_last_error_message(void);
+/* Build provenance (no reference counterpart): sha256 of the sources this library was built from
+ * (tools/source_hash.py: csrc sources and headers, the asm-body generators, this header, the Makefile), so a
+ * caller can tell whether the loaded library matches the tree beside it. */
+const char *mi_build_source_hash(void);
 
 /* ---- Plan -------------------------------------------------------------------------------
  * Replaces tfhe_ntt::prime64::Plan::try_new (tfhe-ntt/src/prime64.rs:764-862): the reference

@@ -98,3 +98,12 @@ def test_integration_rust_binding_declares_every_opaque_type():
     doc = open(os.path.join(root, "INTEGRATION.md")).read()
     opaque = set(re.findall(r"typedef struct (mi_\w+) \1;", hdr))
     assert opaque <= set(re.findall(r"pub struct (mi_\w+)", doc)), opaque - set(re.findall(r"pub struct (mi_\w+)", doc))
+
+
+def test_library_built_from_this_tree():
+    """Build provenance: the loaded library's embedded source hash (tools/source_hash.py, written by the Makefile)
+    equals the hash of the sources beside it, so the tests and the bench never run a stale or foreign .so."""
+    from tfhe_ntt_amd import _lib
+    prov = _lib.build_provenance()
+    assert len(prov["so_source_hash"]) == 64
+    assert prov["match"] is True, prov

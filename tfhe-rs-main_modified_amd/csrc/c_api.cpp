@@ -18,6 +18,7 @@
 #include <tuple>
 #include <vector>
 
+#include "build_info.hpp"  // build/ (Makefile): MI_SOURCE_HASH
 #include "c_api_internal.hpp"
 #include "ntt64_tw_tables.hpp"
 
@@ -54,6 +55,8 @@ const char* mi_status_string(int status) {
 }
 
 const char* mi_last_error_message(void) { return last_error().c_str(); }
+
+const char* mi_build_source_hash(void) { return MI_SOURCE_HASH; }
 
 int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_plan) {
   if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
@@ -335,7 +338,7 @@ int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan* plan, uint64_t* acc, cons
 
 // The `&mut [u64]` host form (Plan::fwd / Plan::inv on a caller slice, as Ntt64View::forward / add_backward call
 // it per polynomial, ntt64.rs:89-137).  Each call borrows a staging slot of the plan's device from a process-wide
-// pool: a private non-blocking stream, a device buffer and a mapped, coherent pinned host buffer, all grown on
+// pool: a private non-blocking stream of the highest priority, a device buffer and a mapped, coherent pinned host buffer, all grown on
 // demand and reused.  Up to ZERO_COPY_BYTES the transform runs in place on the pinned buffer itself (the kernel
 // reads and writes host memory over PCIe: one launch and one wait per call instead of two copies around the
 // launch); above it a call is memcpy -> async H2D -> transform -> async D2H -> wait -> memcpy.  No allocation in the
@@ -383,7 +386,11 @@ HostSlot* acquire_slot(int device) {
   HostSlot* s = new (std::nothrow) HostSlot;
   if (!s) return nullptr;
   s->device = device;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+  // the highest stream priority: a per-polynomial host call is latency-bound, and a high-priority stream gets
+  // hardware queues of its own, so it is never queued behind bulk work of the process's normal-priority streams
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+  if (hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
     delete s;
     return nullptr;
   }

@@ -39,6 +39,7 @@ class MiError(RuntimeError):
 _SIGS = {
     "mi_status_string": (ctypes.c_char_p, [_int]),
     "mi_last_error_message": (ctypes.c_char_p, []),
+    "mi_build_source_hash": (ctypes.c_char_p, []),
     "mi_ntt64_plan_create": (_int, [_sz, _u64, _int, ctypes.POINTER(_vp)]),
     "mi_ntt64_plan_destroy": (_int, [_vp]),
     "mi_ntt64_plan_cached": (_int, [_sz, _u64, _int, ctypes.POINTER(_vp)]),
@@ -173,6 +174,24 @@ def hip_runtimes() -> list[str]:
     except OSError:
         pass
     return sorted(paths)
+
+
+def build_provenance() -> dict:
+    """The loaded library's embedded source hash against the hash of the sources beside it (tools/source_hash.py,
+    when the repository tree is present): `match` False means the .so was not built from this tree."""
+    so = (lib().mi_build_source_hash() or b"").decode()
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    tool = os.path.join(root, "tools", "source_hash.py")
+    tree = None
+    if os.path.exists(tool):
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("_mi_source_hash", tool)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        tree = mod.source_hash(root)
+    return {"so_source_hash": so, "tree_source_hash": tree, "match": (tree == so) if tree else None,
+            "so_path": LIB_PATH}
 
 
 def check(status: int) -> None:
