@@ -548,6 +548,35 @@ def bench_ext_product(args, eng, torch, dev, world, barrier, dist):
             "cpu_baseline": None}
 
 
+def bench_ext_product_fft(args, eng, torch, dev, world, barrier, dist):
+    """Config 3 on the default (f64-FFT) path: add_external_product_assign (fft64_pbs.rs:270-330) of a batch of
+    native GLWEs (k = 1, N = 2048, l = 1, base 2^23) with one shared Fourier GGSW; the one-ciphertext workgroups of
+    fft64_pbs.hip (2 waves per product).  Also the k = 2, level-2 shape on the same engine."""
+    F = eng.fft64
+    fft = F.Fft(N, dev.index)
+    res = {}
+    for k, level, base_log in ((1, 1, PBS_BASE_LOG), (2, 2, 12)):
+        batch = args.batch
+        std = torch.empty((level, k + 1, k + 1, N), dtype=torch.int64, device=dev)
+        eng.fill_uniform(std, SEED + 33 + k, 0)
+        fg = torch.empty((level, k + 1, k + 1, N // 2, 2), dtype=torch.float64, device=dev)
+        F.convert_standard_lwe_bootstrap_key_to_fourier(std, fg, fft)
+        glwe = torch.empty((batch, k + 1, N), dtype=torch.int64, device=dev)
+        eng.fill_uniform(glwe, SEED + 35 + k, 0)
+        out = torch.zeros((batch, k + 1, N), dtype=torch.int64, device=dev)
+        run = lambda: F.add_external_product_assign(out, fg, glwe, base_log, level, fft)
+        K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev)
+        res[f"k{k}_l{level}"] = {"value": world * batch * K / el, "unit": "external products/s", "steps": K,
+                                 "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms,
+                                 "hbm_frac": (k + 1) * N * 8 * 3 * batch / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                 "config": {"k": k, "level": level, "base_log": base_log, "batch_per_gpu": batch}}
+    out = res["k1_l1"]
+    out.update({"metric": "GGSW x GLWE external products/sec, f64-FFT path (config 3 shape)", "dtype": "f64",
+                "config": dict(out["config"], workload="add_external_product_assign (tfhe-fft path), N=2048"),
+                "k2_l2": res["k2_l2"]})
+    return out
+
+
 def cpu_baseline_ext(seconds: float):
     """Oracle restatement of add_external_product_ntt64_bnf_assign (ntt64_bnf_pbs.rs:541-681) with the AVX-512
     transform restatement, OpenMP over a bounded batch of products."""
@@ -918,6 +947,7 @@ def main():
         legs["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
+        legs["ext_product_fft"] = bench_ext_product_fft(args, eng, torch, dev, world, barrier, dist)
         legs["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier, dist)
         # last before the headline: the external product, an integer-VALU load like the transform's, so the headline
         # always follows the same kind of work (the held clock depends on what ran just before)
