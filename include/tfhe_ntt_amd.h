@@ -318,6 +318,15 @@ int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key *key);
 int mi_fft64_pbs_key_info(const mi_fft64_pbs_key *key, size_t *n_lwe, int *k, int *base_log, int *level);
 int mi_fft64_pbs_batch(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
+/* The multi-GPU bootstrap of mi_pbs_ntt64_multi_gpu[_ordered] (same sharding, active-GPU count, scatter / gather and
+ * producer-stream ordering) on the f64-FFT path: keys[i] (bound to a plan of devices[i], same shape) and luts[i] on
+ * devices[i], lwe_in / lwe_out on devices[0]. */
+int mi_fft64_pbs_multi_gpu(mi_multi_gpu *m, const mi_fft64_pbs_key *const *keys, uint64_t *lwe_out,
+                           const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
+                           void *stream);
+int mi_fft64_pbs_multi_gpu_ordered(mi_multi_gpu *m, const mi_fft64_pbs_key *const *keys, uint64_t *lwe_out,
+                                   const uint64_t *lwe_in, const uint64_t *const *luts, size_t batch, int ms_mode,
+                                   void *stream, void *const *producer_streams);
 /* The reference's serialised FourierLweBootstrapKey (fft_impl/fft64/crypto/bootstrap.rs:30-39, the list's custom
  * Serialize fft_impl/fft64/math/fft/mod.rs:642-690, bincode 1.3 defaults as for the NTT key): format
  * MI_NTT_BSK_PLAIN = bincode::serialize(&key): u64 (2 + P), u64 polynomial_size, u64 P, then P polynomials each as

@@ -369,3 +369,46 @@ def test_config5_device_set_65536_real_keys(engine, oracle):
     want = oracle.NttContext(N).pbs_batch_bnf(lwe[idx], lut.reshape(-1), nbsk.reshape(-1), 1, base_log, level,
                                               threads=16)
     assert np.array_equal(got[idx], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,level,base_log,entries,batch", [(2048, 1, 1, 23, 8, 4096), (512, 4, 1, 23, 3, 37)])
+def test_device_set_fft_pbs_real_keys(engine, oracle, n, k, level, base_log, entries, batch):
+    """The default f64-FFT PBS through the same multi-GPU bootstrap (`mi_fft64_pbs_multi_gpu_ordered`): config 4's
+    shape (N = 2048, the one-wave engine, 8 entries, 4096 ciphertexts) and the MESSAGE_1_CARRY_1 shape (N = 512,
+    k = 4, the generic engine, a ragged 37 over 3 entries).  The sharded output equals one launch bit for bit (each
+    ciphertext's f64 arithmetic does not depend on which shard or workgroup holds it) and every output decrypts."""
+    import torch
+    F = engine.fft64
+    n_lwe, msg_mod = 64, 16
+    delta = (1 << 63) // msg_mod
+    g = H.rng(7700 + n + entries)
+    lwe_sk = H.binary_key(g, n_lwe)
+    glwe_sk = H.binary_key(g, (k, n))
+    bsk = H.bsk_gen_fast(g, oracle, lwe_sk, glwe_sk, base_log, level, 17)
+    fft = F.Fft(n)
+    fbsk = torch.zeros((n_lwe, level, k + 1, k + 1, n // 2, 2), dtype=torch.float64, device="cuda")
+    F.convert_standard_lwe_bootstrap_key_to_fourier(_dev(bsk), fbsk, fft)
+    key = F.FourierLweBootstrapKey(fbsk, base_log, level, fft)
+    f = lambda x: (3 * x + 5) % msg_mod
+    lut = _dev(H.pbs_lut(n, k, msg_mod, delta, f))
+    msgs = np.arange(batch) % msg_mod
+    src = _dev(H.lwe_encrypt_batch(g, msgs.astype(np.uint64) * np.uint64(delta), lwe_sk, 30))
+    ds = engine.multi_gpu.DeviceSet([0] * entries)
+    active = ds.active_count(batch)
+    out = torch.zeros((batch, k * n + 1), dtype=torch.int64, device="cuda")
+    ds.programmable_bootstrap([key] * active + [None] * (entries - active), src, out,
+                              [lut] * active + [None] * (entries - active), F.MS_CENTERED)
+    one = torch.zeros_like(out)
+    F.programmable_bootstrap_lwe_ciphertext(src, one, lut, key, F.MS_CENTERED)
+    torch.cuda.synchronize()
+    assert torch.equal(out, one), "sharded f64 PBS != single launch"
+    pts = H.lwe_decrypt_batch(_host(out), H.glwe_sk_as_lwe_sk(glwe_sk))
+    with np.errstate(over="ignore"):
+        dec = ((pts + np.uint64(delta // 2)) // np.uint64(delta)) % np.uint64(2 * msg_mod)
+    assert np.array_equal(dec, np.array([f(int(m)) for m in msgs], np.uint64))
+    with pytest.raises(ValueError):  # one engine per call
+        ntt_key = engine.ntt64_pbs.NttBootstrapKey(engine.Plan.try_new(2048, P),
+                                                   _dev(np.zeros((n_lwe, 1, 2, 2, 2048), np.uint64)), 23, 1,
+                                                   engine.ntt64_pbs.BNF)
+        ds.programmable_bootstrap([key, ntt_key] + [key] * (entries - 2), src, out, [lut] * entries)

@@ -20,25 +20,6 @@
 
 using namespace mi::capi;
 
-struct mi_fft64_plan {
-  size_t n = 0;
-  int device = 0;
-  bool cached = false;
-  bool generic = false;        // the shape-generic engine (N != 2048)
-  double* d_tables = nullptr;  // N = 2048: t1 (2048) | t2 (96, padded to 128) | cm (32) | cmi (32) doubles;
-                               // generic: tw | untw | wm (M complex each)
-  mi::FftTables tables{};
-  mi::FftGenTables gtables{};
-};
-
-struct mi_fft64_pbs_key {
-  const mi_fft64_plan* plan = nullptr;
-  const double* fbsk = nullptr;  // caller-owned Fourier key, or `owned`
-  double* owned = nullptr;       // device copy made by mi_fft64_pbs_key_load
-  size_t n_lwe = 0;
-  int k = 1, base_log = 0, level = 0;
-};
-
 namespace {
 
 constexpr size_t FFT_N = 2048, FFT_M = 1024;

@@ -8,6 +8,7 @@
 
 #include "../../include/tfhe_ntt_amd.h"
 #include "host_math.hpp"
+#include "fft64_launch.hpp"
 #include "ntt64_launch.hpp"
 
 using mi::host::u128;
@@ -31,6 +32,25 @@ struct mi_ntt64_plan {
   u64* d_twist_f = nullptr;
   u64* d_twist_i = nullptr;
   u64* d_twist_fn = nullptr;  // forward twist rows x N^-1 + the forward lane-pair twiddles (normalising key conversion)
+};
+
+struct mi_fft64_plan {
+  size_t n = 0;
+  int device = 0;
+  bool cached = false;
+  bool generic = false;        // the shape-generic engine (N != 2048)
+  double* d_tables = nullptr;  // N = 2048: t1 (2048) | t2 (96, padded to 128) | cm (32) | cmi (32) doubles;
+                               // generic: tw | untw | wm (M complex each)
+  mi::FftTables tables{};
+  mi::FftGenTables gtables{};
+};
+
+struct mi_fft64_pbs_key {
+  const mi_fft64_plan* plan = nullptr;
+  const double* fbsk = nullptr;  // caller-owned Fourier key, or `owned`
+  double* owned = nullptr;       // device copy made by mi_fft64_pbs_key_load
+  size_t n_lwe = 0;
+  int k = 1, base_log = 0, level = 0;
 };
 
 struct mi_pbs_ntt64_key {

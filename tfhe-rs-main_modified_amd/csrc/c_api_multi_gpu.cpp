@@ -220,9 +220,31 @@ int mi_multi_gpu_gather(mi_multi_gpu* m, void* dst, const void* const* srcs, siz
 // keys[i]: shard i starts after the work queued on it so far, and it is ordered after shard i's last use of them,
 // so the caller's allocator may free or reuse them on that stream as soon as the call returns.  Shard 0 runs in
 // place on `stream`; the other shards use stream-ordered scratch on their device.
-int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,
-                                   const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode,
-                                   void* stream, void* const* producer_streams) {
+}  // extern "C"
+
+namespace {
+// what the multi-GPU bootstrap needs of a key: its device and shape, and its single-device batch launch
+struct KeyShape {
+  int device;
+  size_t n_lwe, n;
+  int k, variant;
+};
+KeyShape shape_of(const mi_pbs_ntt64_key* key) {
+  return {key->plan->device, key->n_lwe, key->plan->n, key->k, key->variant};
+}
+KeyShape shape_of(const mi_fft64_pbs_key* key) { return {key->plan->device, key->n_lwe, key->plan->n, key->k, -1}; }
+int pbs_batch(const mi_pbs_ntt64_key* key, uint64_t* out, const uint64_t* in, const uint64_t* lut, size_t n,
+              int ms_mode, void* stream) {
+  return mi_pbs_ntt64_batch(key, out, in, lut, n, ms_mode, stream);
+}
+int pbs_batch(const mi_fft64_pbs_key* key, uint64_t* out, const uint64_t* in, const uint64_t* lut, size_t n,
+              int ms_mode, void* stream) {
+  return mi_fft64_pbs_batch(key, out, in, lut, n, ms_mode, stream);
+}
+
+template <class Key>
+int multi_gpu_pbs(mi_multi_gpu* m, const Key* const* keys, uint64_t* lwe_out, const uint64_t* lwe_in,
+                  const uint64_t* const* luts, size_t batch, int ms_mode, void* stream, void* const* producer_streams) {
   if (!m || !keys || !luts) return fail(MI_ERR_INVALID_ARG, "NULL argument");
   if (batch == 0) return MI_OK;
   if (!lwe_out || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
@@ -232,12 +254,13 @@ int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* cons
   const size_t G = active;
   for (size_t i = 0; i < G; ++i) {
     if (!keys[i] || !luts[i]) return fail(MI_ERR_INVALID_ARG, "key / lut of an active entry is NULL");
-    if (keys[i]->plan->device != m->devices[i]) return fail(MI_ERR_INVALID_ARG, "keys[i] is not on devices[i]");
-    if (keys[i]->n_lwe != keys[0]->n_lwe || keys[i]->k != keys[0]->k || keys[i]->variant != keys[0]->variant ||
-        keys[i]->plan->n != keys[0]->plan->n)
+    const KeyShape a = shape_of(keys[i]), b = shape_of(keys[0]);
+    if (a.device != m->devices[i]) return fail(MI_ERR_INVALID_ARG, "keys[i] is not on devices[i]");
+    if (a.n_lwe != b.n_lwe || a.k != b.k || a.variant != b.variant || a.n != b.n)
       return fail(MI_ERR_INVALID_ARG, "keys differ in shape");
   }
-  const size_t in_w = keys[0]->n_lwe + 1, out_w = (size_t)keys[0]->k * keys[0]->plan->n + 1;
+  const KeyShape k0 = shape_of(keys[0]);
+  const size_t in_w = k0.n_lwe + 1, out_w = (size_t)k0.k * k0.n + 1;
   auto producer = [&](size_t i) -> hipStream_t {
     return producer_streams ? (hipStream_t)producer_streams[i] : nullptr;
   };
@@ -286,7 +309,7 @@ int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* cons
     size_t off = 0, n = 0;
     shard(batch, i, G, &off, &n);
     if (n == 0) continue;
-    st = mi_pbs_ntt64_batch(keys[i], outs[i], ins[i], luts[i], n, ms_mode, i == 0 ? stream : m->streams[i]);
+    st = pbs_batch(keys[i], outs[i], ins[i], luts[i], n, ms_mode, i == 0 ? stream : m->streams[i]);
   }
   if (st == MI_OK) st = mi_multi_gpu_gather(&sub, lwe_out, srcs.data(), batch, out_w * 8, stream);
   for (size_t i = 1; i < G; ++i)
@@ -302,6 +325,28 @@ int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* cons
     if (e != hipSuccess) st = hip_fail(e, "producer-stream ordering");
   }
   return st;
+}
+}  // namespace
+
+extern "C" {
+
+int mi_pbs_ntt64_multi_gpu_ordered(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,
+                                   const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode,
+                                   void* stream, void* const* producer_streams) {
+  return multi_gpu_pbs(m, keys, lwe_out, lwe_in, luts, batch, ms_mode, stream, producer_streams);
+}
+
+// the same sharding for the f64-FFT bootstrap (the default shortint PBS; the CUDA backend's multi-GPU PBS is the
+// FFT one, helper_multi_gpu.cu)
+int mi_fft64_pbs_multi_gpu_ordered(mi_multi_gpu* m, const mi_fft64_pbs_key* const* keys, uint64_t* lwe_out,
+                                   const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode,
+                                   void* stream, void* const* producer_streams) {
+  return multi_gpu_pbs(m, keys, lwe_out, lwe_in, luts, batch, ms_mode, stream, producer_streams);
+}
+
+int mi_fft64_pbs_multi_gpu(mi_multi_gpu* m, const mi_fft64_pbs_key* const* keys, uint64_t* lwe_out,
+                           const uint64_t* lwe_in, const uint64_t* const* luts, size_t batch, int ms_mode, void* stream) {
+  return multi_gpu_pbs(m, keys, lwe_out, lwe_in, luts, batch, ms_mode, stream, nullptr);
 }
 
 int mi_pbs_ntt64_multi_gpu(mi_multi_gpu* m, const mi_pbs_ntt64_key* const* keys, uint64_t* lwe_out,

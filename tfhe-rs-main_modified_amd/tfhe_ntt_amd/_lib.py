@@ -79,6 +79,8 @@ _SIGS = {
     "mi_multi_gpu_gather": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "mi_pbs_ntt64_multi_gpu": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp]),
     "mi_pbs_ntt64_multi_gpu_ordered": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp, _vp]),
+    "mi_fft64_pbs_multi_gpu": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_fft64_pbs_multi_gpu_ordered": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _int, _vp, _vp]),
     "mi_fft64_plan_create": (_int, [_sz, _int, ctypes.POINTER(_vp)]),
     "mi_fft64_plan_cached": (_int, [_sz, _int, ctypes.POINTER(_vp)]),
     "mi_fft64_plan_destroy": (_int, [_vp]),

@@ -177,7 +177,8 @@ class DeviceSet:
         return lib_active_count(batch, len(self.devices))
 
     def programmable_bootstrap(self, keys, lwe_in, lwe_out, luts, ms_mode: int = 0):
-        """Batched PBS over the set (``mi_pbs_ntt64_multi_gpu_ordered``): ``keys[i]`` / ``luts[i]`` on
+        """Batched PBS over the set (``mi_pbs_ntt64_multi_gpu_ordered``, or ``mi_fft64_pbs_multi_gpu_ordered`` for
+        ``fft64.FourierLweBootstrapKey`` keys: the default f64-FFT path): ``keys[i]`` / ``luts[i]`` on
         ``devices[i]``, ``lwe_in`` / ``lwe_out`` on ``devices[0]``; results land in ``lwe_out`` as one launch
         would.  Only the first ``active_count(batch)`` entries run (their keys / LUTs are the only ones read;
         the others may be None).  Each device's current torch stream is passed as the producer of its key and
@@ -203,9 +204,13 @@ class DeviceSet:
         lp = (ctypes.c_void_p * len(luts))(*[t.data_ptr() if t is not None else None for t in luts])
         prod = (ctypes.c_void_p * len(self.devices))(
             *[torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream for d in self.devices])
-        check(lib().mi_pbs_ntt64_multi_gpu_ordered(self._h, kp, ctypes.c_void_p(lwe_out.data_ptr()),
-                                                   ctypes.c_void_p(lwe_in.data_ptr()), lp, batch, ms_mode,
-                                                   self._stream(lwe_out), prod))
+        from .fft64 import FourierLweBootstrapKey
+        fft = isinstance(k0, FourierLweBootstrapKey)
+        if any(k is not None and isinstance(k, FourierLweBootstrapKey) != fft for k in keys):
+            raise ValueError("keys mix the NTT and the f64-FFT engines")
+        fn = lib().mi_fft64_pbs_multi_gpu_ordered if fft else lib().mi_pbs_ntt64_multi_gpu_ordered
+        check(fn(self._h, kp, ctypes.c_void_p(lwe_out.data_ptr()), ctypes.c_void_p(lwe_in.data_ptr()), lp, batch,
+                 ms_mode, self._stream(lwe_out), prod))
 
 
 def lib_shard(total: int, index: int, count: int):
