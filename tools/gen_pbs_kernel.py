@@ -197,7 +197,7 @@ def decompose_sol(sg, sl, xl, xh, signed=False):
     sg.add(f"v_mad_i64_i32 {xp}, {JUNK}, {m}, s{T.S_X15}, {xp}", [m, xl, xh], [xl, xh, JUNK])
 
 
-def stage0_signed(B, tabs, dmap):
+def stage0_signed(B, tabs, dmap, rows=range(16)):
     """The forward's first stage (registers r, r + 16, twiddle 2^48) straight from the signed level-1 digits the
     decomposition leaves in the low words (|d| < 2^31), instead of mapping each digit into [0, p) and running a
     general shift-class butterfly.  With bh = d_b >> 16 (arithmetic) and T = (d_b mod 2^16) 2^48 (high word
@@ -209,7 +209,7 @@ def stage0_signed(B, tabs, dmap):
     assert all(e == 48 for e in tabs["G1_FWD"][0]), "stage 0 twiddle is not 2^48"
     sg = Seg()
     sls = B.slots(free_blocks_except(dmap))
-    for r in range(16):
+    for r in rows:
         sl = sls[r % len(sls)]
         v, c = sl.v, sl.c
         al, ah, ap = X(dmap, r)
@@ -455,6 +455,9 @@ def gen_pbs(tabs, sol=False):
     return B
 
 
+EXT_PROGRESSIVE = True  # external product: decompose + first stage per group of rows as they arrive
+
+
 def gen_ext(tabs, cmux, sol=False):
     """One external product (cmux=False: out += GGSW . glwe) or CMUX (glwe -= out, then
     out += GGSW . glwe), level 1; wave w handles polynomial w of one GLWE pair.  BNF (native GLWEs, Raw
@@ -471,6 +474,34 @@ def gen_ext(tabs, cmux, sol=False):
           f"s_mov_b32 s{S_OUT}, %[out_lo]", f"s_mov_b32 s{S_OUT + 1}, %[out_hi]")
     if cmux:  # ct1 -= ct0 needs the out rows (ct0) first
         B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
+    elif EXT_PROGRESSIVE:
+        # the GLWE rows in butterfly-pair order (r, r + 16), then the first two GGSW chunks; the decomposition and
+        # the first forward stage run in 4 groups of 4 pairs as their rows arrive (loads return in issue order), and
+        # the out rows — read only by the final accumulate — are issued after them (the MAC's chunk waits
+        # over-cover them, which is safe)
+        rows = load_rows(64, S_GL)
+        B.raw(*[rows[q] for k in range(16) for q in (k, k + 16)], *gload(0), *gload(1))
+        sls = slots_at([8, 16, 24, 32, 40, 48, 56])
+        dmap0 = [64 + 2 * r for r in range(32)]
+        for g in range(4):
+            B.raw(f"s_waitcnt vmcnt({16 + 32 - 8 * (g + 1)})")
+            sg = Seg()
+            for k in range(4 * g, 4 * g + 4):
+                for r in (k, k + 16):
+                    (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}",
+                                                          signed=True)
+            sched(B, sg)
+            stage0_signed(B, tabs, dmap0, rows=range(4 * g, 4 * g + 4))
+        B.raw(*load_rows(ACC, S_OUT))
+        dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1)
+        mac(B, dmap)
+        dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
+        if sol:
+            add_acc_sol(B, dmap)
+        else:
+            modswitch_acc(B, dmap)
+        B.raw(*store_rows(ACC, S_OUT))
+        return B
     else:  # the out rows are only read by the final accumulate: issued last, waited for only by the MAC's waits
         # (vmcnt waits for at most the count given, so the MAC's chunk waits over-cover them, which is safe)
         B.raw(*load_rows(64, S_GL), *gload(0), *gload(1), *load_rows(ACC, S_OUT), "s_waitcnt vmcnt(48)")
