@@ -490,14 +490,14 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   return MI_OK;
 }
 
-extern "C" {
-
 // the twisted-transform bodies (pbs_tw.hip) cover level 1, base_log <= 31 (BNF and Solinas) on the
 // Solinas N = 2048 plan; every other shape runs the generic kernels (pbs_kernels.hip)
-static bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level) {
+bool mi::capi::twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level) {
   (void)variant;
   return k == 1 && level == 1 && base_log <= 31 && plan->twisted;
 }
+
+extern "C" {
 
 int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t* bsk_ntt, size_t n_polys,
                     unsigned in_modulus_width, int normalize, void* stream) {
@@ -576,10 +576,22 @@ int mi_cmux_ntt64_batch_indexed(const mi_ntt64_plan* plan, uint64_t* ct0, uint64
 
 }  // extern "C"
 
-int mi::capi::prepare_bnf_key(const mi_ntt64_plan* plan, u64* dst, const u64* src, size_t count, hipStream_t stream) {
-  hipError_t e = mi::launch_scale(dst, src, count, plan->n_inv, stream);
+bool mi::capi::pbs_key_needs_copy(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level) {
+  return variant == MI_NTT64_BNF || twisted_ext_applies(plan, variant, k, base_log, level);
+}
+
+int mi::capi::prepare_pbs_key(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level, u64* dst,
+                              const u64* src, size_t count, hipStream_t stream) {
+  const bool bnf = variant == MI_NTT64_BNF;
+  hipError_t e = hipSuccess;
+  if (twisted_ext_applies(plan, variant, k, base_log, level))
+    e = mi::launch_prepare_tw_key(dst, src, count / plan->n, plan->n_inv, bnf ? 1 : 0, stream);
+  else if (bnf)
+    e = mi::launch_scale(dst, src, count, plan->n_inv, stream);
+  else if (dst != src)
+    e = hipMemcpyAsync(dst, src, count * sizeof(u64), hipMemcpyDeviceToDevice, stream);
   if (e == hipSuccess) e = hipStreamSynchronize(stream);
-  return e == hipSuccess ? MI_OK : hip_fail(e, "bootstrap key normalisation");
+  return e == hipSuccess ? MI_OK : hip_fail(e, "bootstrap key preparation");
 }
 
 extern "C" {
@@ -601,7 +613,7 @@ int mi_pbs_ntt64_key_create(const mi_ntt64_plan* plan, const uint64_t* bsk_ntt, 
   key->level = level;
   key->variant = variant;
   key->bsk = bsk_ntt;
-  if (variant == MI_NTT64_BNF) {
+  if (pbs_key_needs_copy(plan, variant, k, base_log, level)) {
     const size_t count = n_lwe * (size_t)(k + 1) * (k + 1) * level * plan->n;
     DeviceGuard g(plan->device);
     if (hipMalloc(&key->owned, count * sizeof(u64)) != hipSuccess) {
@@ -609,7 +621,7 @@ int mi_pbs_ntt64_key_create(const mi_ntt64_plan* plan, const uint64_t* bsk_ntt, 
       return fail(MI_ERR_OOM, "bootstrap key copy allocation failed");
     }
     // ordered after the work that produced bsk_ntt on `stream` (the caller's stream)
-    st = prepare_bnf_key(plan, key->owned, bsk_ntt, count, (hipStream_t)stream);
+    st = prepare_pbs_key(plan, variant, k, base_log, level, key->owned, bsk_ntt, count, (hipStream_t)stream);
     if (st != MI_OK) {
       (void)hipFree(key->owned);
       delete key;

@@ -58,7 +58,7 @@ struct mi_pbs_ntt64_key {
   size_t n_lwe = 0;
   int k = 1, base_log = 0, level = 0, variant = 0;
   const u64* bsk = nullptr;  // what the kernel reads
-  u64* owned = nullptr;      // BNF: private copy with N^{-1} folded in; loaded keys: the uploaded bytes
+  u64* owned = nullptr;      // private copy (prepare_pbs_key: BNF N^{-1} folded in; twisted engine: W1' order); loaded keys
 };
 
 namespace mi {
@@ -90,8 +90,15 @@ struct DeviceGuard {
 
 // shared by mi_pbs_ntt64_key_create and mi_pbs_ntt64_key_load
 int check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, int level, int variant);
-// BNF keys: N^{-1} folded into `dst` (dst may equal src); synchronises `stream`
-int prepare_bnf_key(const mi_ntt64_plan* plan, u64* dst, const u64* src, size_t count, hipStream_t stream);
+// whether a consumer shape runs on the twisted N = 2048 engine (pbs_tw.hip: k = 1, level 1)
+bool twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level);
+// whether a PBS key of this shape needs a private device copy: BNF keys (N^{-1} folded in) and every key of the
+// twisted engine (its blind rotation reads the key in its W1' register order)
+bool pbs_key_needs_copy(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level);
+// fill that copy from src (dst may equal src; a no-op for a key that needs no copy when dst == src); synchronises
+// `stream`
+int prepare_pbs_key(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level, u64* dst, const u64* src,
+                    size_t count, hipStream_t stream);
 
 }  // namespace capi
 }  // namespace mi

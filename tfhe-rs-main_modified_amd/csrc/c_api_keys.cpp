@@ -177,11 +177,9 @@ int mi_pbs_ntt64_key_load(const mi_ntt64_plan* plan, const uint8_t* bytes, size_
   }
   hipError_t e = hipMemcpyAsync(key->owned, bytes + h.data_offset, h.count * sizeof(u64), hipMemcpyHostToDevice, s);
   st = e == hipSuccess ? MI_OK : hip_fail(e, "bootstrap key upload");
-  if (st == MI_OK && variant == MI_NTT64_BNF) st = prepare_bnf_key(plan, key->owned, key->owned, h.count, s);
-  if (st == MI_OK && variant != MI_NTT64_BNF) {
-    e = hipStreamSynchronize(s);  // the host bytes may be freed once this returns
-    if (e != hipSuccess) st = hip_fail(e, "bootstrap key upload");
-  }
+  // (synchronises s: the host bytes may be freed once this returns)
+  if (st == MI_OK)
+    st = prepare_pbs_key(plan, variant, key->k, key->base_log, key->level, key->owned, key->owned, h.count, s);
   if (st != MI_OK) {
     (void)hipFree(key->owned);
     delete key;

@@ -87,6 +87,10 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
                          int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx = nullptr,
                          uint32_t n_ggsw = 1);
 // Solinas PBS on the twisted engine: switched = pre-switched mask + body values in [0, 2N)
+// the twisted bodies' key order (pbs_tw.hip): per N = 2048 polynomial, positions permuted to the W1' step layout
+// when the blind-rotation (ext: external-product) body reads that order, times c when scale (dst may equal src)
+hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_polys, uint64_t c, int scale,
+                                 hipStream_t s, bool ext = false);
 hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s);
 hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,
                              size_t n_lwe, size_t batch, int base_log, const uint64_t* tab, hipStream_t s);

@@ -241,12 +241,53 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
 }
 
+// The blind-rotation body keeps the NTT-domain data in the forward's W1' register layout through the MAC
+// (tools/gen_pbs_kernel.py PBS_W1P / tw_key_index), so it reads its key in that order: position 64 R + L of each
+// polynomial holds NTT-domain coefficient 64 (L >> 1) + 32 (L & 1) + 2 (R & 15) + (R >> 4).  One workgroup per
+// polynomial stages it in LDS (so dst may equal src) and optionally multiplies by c (BNF: N^-1 folded in, exact).
+__global__ __launch_bounds__(256) void prepare_tw_key_kernel(u64* dst, const u64* src, size_t n_polys, u64 c, int scale,
+                                                             int permute) {
+  __shared__ u64 poly[N];
+  for (size_t q = blockIdx.x; q < n_polys; q += gridDim.x) {
+    const u64* in = src + q * N;
+    for (int e = threadIdx.x; e < N; e += 256) poly[e] = in[e];
+    __syncthreads();
+    u64* out = dst + q * N;
+    for (int pos = threadIdx.x; pos < N; pos += 256) {
+      const int R = pos >> 6, L = pos & 63;
+      const u64 v = poly[permute ? 64 * (L >> 1) + 32 * (L & 1) + 2 * (R & 15) + (R >> 4) : pos];
+      out[pos] = scale ? Goldilocks().mul(v, c) : v;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace pbstw
+
+hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_polys, uint64_t c, int scale,
+                                 hipStream_t s, bool ext) {
+  if (n_polys == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)(n_polys < 65535 ? n_polys : 65535);
+  hipLaunchKernelGGL(pbstw::prepare_tw_key_kernel, dim3(blocks), dim3(256), 0, s, dst, src, n_polys, c, scale,
+                     ext ? MI_EXT_W1P : MI_PBS_W1P);
+  return hipGetLastError();
+}
 
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                          int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
+  u64* perm = nullptr;  // MI_EXT_W1P: the caller's GGSWs in the body's W1' order, stream-ordered scratch
+  if (MI_EXT_W1P) {
+    hipError_t e = hipMallocAsync((void**)&perm, (size_t)n_ggsw * 4 * pbstw::N * sizeof(u64), s);
+    if (e != hipSuccess) return e;
+    e = launch_prepare_tw_key(perm, ggsw, (size_t)n_ggsw * 4, 0, 0, s, true);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(perm, s);
+      return e;
+    }
+    ggsw = perm;
+  }
   const dim3 g((unsigned)batch), blk(128);
   if (sol && cmux)
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
@@ -256,7 +297,9 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<false>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (perm) (void)hipFreeAsync(perm, s);
+  return e;
 }
 
 hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s) {

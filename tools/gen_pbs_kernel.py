@@ -408,6 +408,33 @@ def add_acc_sol(B, dmap):
     sched(B, sg)
 
 
+# The blind-rotation step keeps the NTT-domain data in registers from the forward's lane-pair stage to the inverse's
+# DIT stages: the MAC runs in the forward's W1' layout (the exchange with the partner wave is lane-linear in any
+# layout) and the inverse starts from it (gen_tw_kernel.w1p_as_w1pp), so the step does no T2 and no T1'' transpose.
+# The key the body reads is then the private copy in that order (row R, lane L of polynomial position 64 R + L holds
+# NTT-domain coefficient tw_key_index(64 R + L); pbs_tw.hip prepare_tw_key builds it).
+PBS_W1P = True
+
+
+def tw_key_index(pos):
+    """NTT-domain coefficient index (the reference's order) that the key copy of the W1' step holds at position pos."""
+    R, L = pos >> 6, pos & 63
+    return 64 * (L >> 1) + 32 * (L & 1) + 2 * (R & 15) + (R >> 4)
+
+
+def fwd_mac_inv(B, tabs, dmap0, w1p):
+    """Forward transform (its stage 0 already run), the MAC with the partner wave and the inverse; returns the output
+    dmap (W0, canonical).  w1p: the MAC and the inverse's input stay in the forward's W1' layout (PBS_W1P)."""
+    if w1p:
+        dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1, stop="last")
+        mac(B, dmap)
+        assert dmap == [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)], dmap
+        return T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64))
+    dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1)
+    mac(B, dmap)
+    return T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
+
+
 def gen_pbs(tabs, sol=False):
     """BNF (sol=False): native ciphertexts, ms computed here from the raw mask, acc from the LUT rows.
     Solinas (sol=True, ntt64_pbs.rs:213-286): the mask arrives pre-switched (lwe = the switched values,
@@ -438,9 +465,7 @@ def gen_pbs(tabs, sol=False):
     B.raw(*gload(0), *gload(1))
     rotate_decompose(B, sol)
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
-    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
-    mac(B, dmap)
-    dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
+    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], PBS_W1P)
     if sol:
         add_acc_sol(B, dmap)
     else:
@@ -455,6 +480,9 @@ def gen_pbs(tabs, sol=False):
     return B
 
 
+# the external product / CMUX bodies: the same W1' step on a GGSW permuted into the body's order per call
+# (pbs_tw.hip launch_ext_tw: the caller's Raw / Normalize GGSW stays in the reference's order)
+EXT_W1P = False
 EXT_PROGRESSIVE = True  # external product: decompose + first stage per group of rows as they arrive
 
 
@@ -493,9 +521,7 @@ def gen_ext(tabs, cmux, sol=False):
             sched(B, sg)
             stage0_signed(B, tabs, dmap0, rows=range(4 * g, 4 * g + 4))
         B.raw(*load_rows(ACC, S_OUT))
-        dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1)
-        mac(B, dmap)
-        dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
+        dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P)
         if sol:
             add_acc_sol(B, dmap)
         else:
@@ -527,9 +553,7 @@ def gen_ext(tabs, cmux, sol=False):
         (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
     sched(B, sg)
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
-    dmap = T.fwd_core(B, tabs, [64 + 2 * r for r in range(32)], FWD_ADDR, first_stage=1)
-    mac(B, dmap)
-    dmap = T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
+    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], EXT_W1P)
     if sol:
         add_acc_sol(B, dmap)
     else:
@@ -553,6 +577,8 @@ def main():
     print("// and CMUXes (BNF and Solinas) as asm bodies per wave (pbs_tw.hip).  Own v8..v255, s20..s31 + s36..s93")
     print("// (+ s94..s95 in the Solinas bodies), exec (restored).")
     print("#pragma once")
+    print(f"#define MI_PBS_W1P {int(PBS_W1P)}  // blind rotation reads its key in the W1' order (tw_key_index)")
+    print(f"#define MI_EXT_W1P {int(EXT_W1P)}  // external product / CMUX read their GGSW in the W1' order")
     print(emit("bnf_l1", b))
     e, c = gen_ext(tabs, False), gen_ext(tabs, True)
     print(emit("ext_bnf_l1", e))

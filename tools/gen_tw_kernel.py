@@ -1128,12 +1128,24 @@ def pair_stage_dit(B, dmap, ad, pre, busy):
         B.out(sg.schedule())
 
 
-def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64):
+def w1p_as_w1pp(dmap):
+    """The forward's output layout after its lane-pair stage (W1': lane 2 i + par, register R < 16 holds output
+    64 i + 32 par + 2 R, register R + 16 the next one) is W1'' (lane 2 i + j5, register r = j & 31) up to a renaming
+    of registers: r = 2 (R mod 16) + [R >= 16].  So a consumer that keeps the NTT-domain data in registers (the PBS
+    step: forward -> MAC -> inverse) needs neither the forward's T2 nor the inverse's T1''."""
+    return [dmap[(r >> 1) + 16 * (r & 1)] for r in range(32)]
+
+
+def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=False):
     """W0 data -> T1'' -> DIT stages 0..4 in registers -> the lane-pair DIT stage -> W0.  The lane-pair stage's
     table twiddles load right after T1'' (into pre_base..), five stages ahead of their use.  Register plan
     (standalone defaults; the PBS bodies pass their own): `dst` (32 pairs) may reuse only rows 0..15 of `dmap`,
-    pre_base.. (8 registers) must be free of `dst`, and `ybase` (the first output half) must be free of `dst`."""
-    dmap = t1_w1pp(B, dmap, dst or [8 + 2 * r for r in range(32)], ad)
+    pre_base.. (8 registers) must be free of `dst`, and `ybase` (the first output half) must be free of `dst`.
+    w1p_in: `dmap` already holds the data in the forward's W1' layout (no T1'', see w1p_as_w1pp)."""
+    if w1p_in:
+        dmap = w1p_as_w1pp(dmap)
+    else:
+        dmap = t1_w1pp(B, dmap, dst or [8 + 2 * r for r in range(32)], ad)
     ms = pair_stage_dit_gmul_ms()
     pre = {m: pre_base + 2 * i for i, m in enumerate(ms)}
     assert len(ms) <= 4
