@@ -1,17 +1,20 @@
 #!/usr/bin/env python3
 """bench.py's config-3 external-product leg alone, repeated (diagnostic A/B of body variants):
-python tools/ext_probe.py [reps]"""
+python tools/ext_probe.py [reps] [package dir holding tfhe_ntt_amd/]"""
 import json
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "tfhe-rs-main_modified_amd")]
+PKG = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "tfhe-rs-main_modified_amd")
+sys.path[:0] = [ROOT, PKG]
 
 import torch  # noqa: E402
 
+import tfhe_ntt_amd as eng  # noqa: E402  (first: bench.py puts the in-tree package on the path too)
 import bench  # noqa: E402
-import tfhe_ntt_amd as eng  # noqa: E402
+
+assert os.path.dirname(eng.__file__).startswith(os.path.abspath(PKG)), eng.__file__
 
 
 class A:

@@ -481,7 +481,9 @@ def gen_pbs(tabs, sol=False):
 
 
 # the external product / CMUX bodies: the same W1' step on a GGSW permuted into the body's order per call
-# (pbs_tw.hip launch_ext_tw: the caller's Raw / Normalize GGSW stays in the reference's order)
+# (pbs_tw.hip launch_ext_tw: the caller's Raw / Normalize GGSW stays in the reference's order).  Off: emulator- and
+# GPU-exact, but 26.72 vs 26.57 M products/s in a one-box A/B (+0.5 %, profiles/r3/ext_w1p_ab/): the per-call
+# reorder launch costs about what the two transposes saved (~5 us of a 307 us launch)
 EXT_W1P = False
 EXT_PROGRESSIVE = True  # external product: decompose + first stage per group of rows as they arrive
 
