@@ -3,6 +3,7 @@
 into the committed profile artefacts.
 
   python tools/summarize_rocpd.py gpurun_out/prof_r3/run_results.db profiles/r3 [bench_line.json]
+  python tools/summarize_rocpd.py gpurun_out/prof/run_kernel_trace.csv profiles/r3/... [bench_line.json]
 
 Writes <dst>/kernel_stats.csv (per kernel: calls, total / average / min / max duration in ns, the columns of
 rocprofv3 --stats) and <dst>/trace_roofline.json: for the headline transform kernels (ntt_tw_body_kernel at the
@@ -25,8 +26,13 @@ def main():
     db, dst = sys.argv[1], sys.argv[2]
     line = json.load(open(sys.argv[3])) if len(sys.argv) > 3 else None
     os.makedirs(dst, exist_ok=True)
-    c = sqlite3.connect(db)
-    rows = c.execute("select name, duration, grid_x, start from kernels order by start").fetchall()
+    if db.endswith(".csv"):  # rocprofv3 --output-format csv: <prefix>_kernel_trace.csv
+        with open(db, newline="") as f:
+            rows = sorted(((r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), int(r["Grid_Size_X"]),
+                            int(r["Start_Timestamp"])) for r in csv.DictReader(f)), key=lambda t: t[3])
+    else:
+        c = sqlite3.connect(db)
+        rows = c.execute("select name, duration, grid_x, start from kernels order by start").fetchall()
     stats = defaultdict(list)
     for name, dur, grid, _ in rows:
         stats[name].append((int(dur), int(grid)))
