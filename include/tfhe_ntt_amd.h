@@ -156,11 +156,12 @@ int mi_cmux_ntt64_batch_indexed(const mi_ntt64_plan *plan, uint64_t *ct0, uint64
 /* A bootstrap key made ready for mi_pbs_ntt64_batch on the plan's device.  MI_NTT64_BNF keys
  * (converted Raw, as ntt64_bnf_pbs.rs tests do) are copied once with N^{-1} folded in — the
  * reference normalises each product at run time (ntt64_bnf_pbs.rs:670); in exact mod-p arithmetic
- * both orders give identical values.  MI_NTT64_SOLINAS keys are referenced, not copied (the caller
- * keeps `bsk_ntt` alive).  Replaces the reference's PodStack scratch (ntt64_pbs.rs:705-751). */
+ * both orders give identical values.  Keys of the fused N = 2048, k = 1, level-1 engine (either variant) are
+ * copied once in the order its blind rotation reads (pbs_tw.hip prepare_tw_key_kernel); other
+ * MI_NTT64_SOLINAS keys are referenced, not copied (the caller keeps `bsk_ntt` alive).  Replaces the
+ * reference's PodStack scratch (ntt64_pbs.rs:705-751). */
 typedef struct mi_pbs_ntt64_key mi_pbs_ntt64_key;
-/* The BNF preparation runs on `stream` (the stream that produced bsk_ntt) and synchronises it before
- * returning. */
+/* The copy runs on `stream` (the stream that produced bsk_ntt) and synchronises it before returning. */
 int mi_pbs_ntt64_key_create(const mi_ntt64_plan *plan, const uint64_t *bsk_ntt, size_t n_lwe, int k, int base_log,
                             int level, int variant, void *stream, mi_pbs_ntt64_key **out_key);
 int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key *key);

@@ -129,7 +129,8 @@ class NttBootstrapKey:
     ``bsk`` is the device tensor (n_lwe, level, k+1, k+1, N) (k = the GLWE dimension) produced by
     ``convert_standard_lwe_bootstrap_key_to_ntt64``: Raw for ``BNF`` (a private copy with N^-1
     folded in is made once, on the tensor's current stream), Normalize for ``SOLINAS`` (referenced;
-    keep the tensor alive)."""
+    keep the tensor alive; the fused N = 2048, k = 1, level-1 engine copies either variant once, into the
+    order its blind rotation reads)."""
 
     def __init__(self, plan, bsk, base_log: int, level: int, variant: int = BNF):
         n = plan.ntt_size()
