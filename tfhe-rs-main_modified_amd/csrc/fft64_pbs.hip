@@ -123,6 +123,40 @@ __device__ __forceinline__ void swap_c(cplx& a, cplx& b) {
   swap_dw<X>(a.im, b.im);
 }
 
+// The per-m twist factor exp(i pi m / 32) (the host table's cm, rounded the same way from long double): built in SGPRs
+// right at its use by volatile scalar moves (volatile: not hoisted out of the blind-rotation loop, where 30 live
+// constants would spill), so the pass-1 twist and the inverse's untwist read no table (16 serialised LDS loads per
+// transform otherwise, each a full LDS latency in front of 4 FMAs)
+__device__ __forceinline__ double sconst(u64 bits) {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)bits));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(bits >> 32)));
+  return __longlong_as_double((long long)(((u64)hi << 32) | lo));
+}
+template <bool CONJ_SCALED>  // false: exp(i pi m / 32); true: exp(-i pi m / 32) / M (the host table's cmi)
+__device__ __forceinline__ cplx cm_const(int m) {
+  constexpr u64 T[16][2] = {
+      {0x3ff0000000000000ull, 0x0000000000000000ull},
+      {0x3fefd88da3d12526ull, 0x3fb917a6bc29b42cull},
+      {0x3fef6297cff75cb0ull, 0x3fc8f8b83c69a60bull},
+      {0x3fee9f4156c62ddaull, 0x3fd294062ed59f06ull},
+      {0x3fed906bcf328d46ull, 0x3fd87de2a6aea963ull},
+      {0x3fec38b2f180bdb1ull, 0x3fde2b5d3806f63bull},
+      {0x3fea9b66290ea1a3ull, 0x3fe1c73b39ae68c8ull},
+      {0x3fe8bc806b151741ull, 0x3fe44cf325091dd6ull},
+      {0x3fe6a09e667f3bcdull, 0x3fe6a09e667f3bcdull},
+      {0x3fe44cf325091dd6ull, 0x3fe8bc806b151741ull},
+      {0x3fe1c73b39ae68c8ull, 0x3fea9b66290ea1a3ull},
+      {0x3fde2b5d3806f63bull, 0x3fec38b2f180bdb1ull},
+      {0x3fd87de2a6aea963ull, 0x3fed906bcf328d46ull},
+      {0x3fd294062ed59f06ull, 0x3fee9f4156c62ddaull},
+      {0x3fc8f8b83c69a60bull, 0x3fef6297cff75cb0ull},
+      {0x3fb917a6bc29b42cull, 0x3fefd88da3d12526ull}};
+  const cplx c = {sconst(T[m][0]), sconst(T[m][1])};
+  if (CONJ_SCALED) return {c.re * (1.0 / 1024.0), -c.im * (1.0 / 1024.0)};  // 1 / M: a power of two, exact
+  return c;
+}
+
 // Forward: u[m] = folded value at n = lane + 64 m (untwisted); out: the Fourier layout.  M = 16 x 64 with
 // n = j + 64 m, j = jl + 16 jh (jl = lane & 15, jh = lane >> 4), frequency f = k1 + 16 q1 + 64 q2:
 //   pass 1  in-lane DFT16 over m -> k1 (register), twiddle T1[k1][j] = w^j omega^(j k1) (`t1`, twist folded in;
@@ -136,8 +170,9 @@ __device__ __forceinline__ void swap_c(cplx& a, cplx& b) {
 // q1 = ((L >> 3) & 1) | ((L >> 2) & 1) << 1.
 __device__ __forceinline__ void fft_fwd(cplx (&u)[16], cplx* buf, const cplx* __restrict__ t1, const cplx* t2,
                                         const cplx* __restrict__ cm, int lane) {
+  (void)cm;  // the table's values are cm_const<false>'s
 #pragma unroll
-  for (int m = 1; m < 16; ++m) u[m] = cmul(u[m], cm[m]);
+  for (int m = 1; m < 16; ++m) u[m] = cmul(u[m], cm_const<false>(m));
   dft16<false>(u);
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) u[k1] = cmul(u[k1], t1[k1 * 64 + lane]);
@@ -214,8 +249,9 @@ __device__ __forceinline__ void fft_inv(cplx (&u)[16], cplx* buf, const cplx* __
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) u[k1] = cmulc(u[k1], t1[k1 * 64 + lane]);
   dft16<true>(u);
+  (void)cmi;  // the table's values are cm_const<true>'s
 #pragma unroll
-  for (int m = 0; m < 16; ++m) u[m] = cmul(u[m], cmi[m]);
+  for (int m = 0; m < 16; ++m) u[m] = cmul(u[m], cm_const<true>(m));
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
