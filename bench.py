@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-pbs", action="store_true", help="skip the config-4 PBS leg")
+    ap.add_argument("--no-shapes", action="store_true",
+                    help="skip the other-shortint-shape PBS legs (the PMC passes of tools/profile_session.sh: rocprofv3 "
+                         "--pmc segfaults on the host inside the shape-generic f64 engine's launch)")
     ap.add_argument("--pbs-batch", type=int, default=PBS_BATCH)
     ap.add_argument("--pbs-steps", type=int, default=10, help="steps of the config-5 sharded leg (N > 1)")
     ap.add_argument("--steady-seconds", type=float, default=1.0, help="length of the steady_state loop")
@@ -937,13 +940,15 @@ def main():
             "note": "the same W + K steps measured first, from an idle GPU, before any leg ran"}
     legs = {}
     if not args.no_pbs:
-        legs["pbs_shapes"] = {name: bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist)
-                              for name in SHAPE_LEGS}
+        if not args.no_shapes:
+            legs["pbs_shapes"] = {name: bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist)
+                                  for name in SHAPE_LEGS}
         legs["pbs"] = bench_pbs(args, eng, torch, dev, rank, world, barrier, dist)
         legs["pbs_solinas"] = bench_pbs_solinas(args, eng, torch, dev, world, barrier, dist)
         legs["pbs_fft"] = bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist)
-        legs["pbs_shapes_fft"] = {name: bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist)
-                                  for name in SHAPE_LEGS}
+        if not args.no_shapes:
+            legs["pbs_shapes_fft"] = {name: bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist)
+                                      for name in SHAPE_LEGS}
         legs["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
@@ -1055,11 +1060,12 @@ def main():
             out["pbs_solinas"]["cpu_baseline"] = cpu_baseline_pbs_solinas(min(args.cpu_seconds, 6.0))
             out["keyswitch"]["cpu_baseline"] = cpu_baseline_ks(min(args.cpu_seconds, 4.0))
             out["bsk_conversion"]["cpu_baseline"] = cpu_baseline_bsk(min(args.cpu_seconds, 3.0))
-            for name in ("message_1_carry_1", "message_3_carry_3"):  # 4_4: ~0.1 s per CMUX step per core, unbounded
+            for name in ("message_1_carry_1", "message_3_carry_3") if not args.no_shapes else ():
+                # (4_4: ~0.1 s per CMUX step per core, unbounded)
                 out["pbs_shapes"][name]["cpu_baseline"] = cpu_baseline_pbs_shape(name, min(args.cpu_seconds, 4.0))
             out["pbs_fft"]["cpu_baseline"] = cpu_baseline_pbs_fft(N, 1, PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL,
                                                                   min(args.cpu_seconds, 3.0))
-            for name, (n_, k_, nl_, bl_, lv_, _) in SHAPE_LEGS.items():
+            for name, (n_, k_, nl_, bl_, lv_, _) in (SHAPE_LEGS.items() if not args.no_shapes else ()):
                 out["pbs_shapes_fft"][name]["cpu_baseline"] = cpu_baseline_pbs_fft(n_, k_, nl_, bl_, lv_,
                                                                                    min(args.cpu_seconds, 3.0))
     if rank == 0:
