@@ -334,6 +334,11 @@ def mac2(sg, m1, m2, x, g1, p, g2):
     sg.add(f"v_cndmask_b32_e64 {xhi}, {a[1]}, {a[5]}, {cb}", [a[1], a[5], cb], [xhi])
 
 
+# The partner's rows of MAC chunk c + 1 are read while chunk c multiplies (a second 4-row buffer in the registers the
+# multiply slots leave free), so each chunk waits only for its GGSW rows, not for an LDS round trip as well.
+MAC_PARTNER_AHEAD = True
+
+
 def mac(B, dmap):
     B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(dmap[r])} offset:{512 * r}" for r in range(32)],
           "s_waitcnt lgkmcnt(0)", "s_barrier")
@@ -344,17 +349,29 @@ def mac(B, dmap):
     ms = [MulSlot(regs[12 * i], SG0 + 6 * i) for i in range(4)]
     # the zero high halves of the product addends, set once for the whole MAC (prod128)
     B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
+    ahead = MAC_PARTNER_AHEAD and len(regs) >= 56
+    pbufs = [PBUF, regs[48]] if ahead else [PBUF]
+    assert not ahead or regs[48:56] == list(range(regs[48], regs[48] + 8)), regs
+    pread = lambda c: [f"ds_read_b64 {pv(pbufs[c % len(pbufs)] + 2 * k)}, v{V_PX} offset:{512 * (4 * c + k)}"
+                       for k in range(4)]
+    if ahead:
+        B.raw(*pread(0))
     for c in range(8):
-        B.raw(*[f"ds_read_b64 {pv(PBUF + 2 * k)}, v{V_PX} offset:{512 * (4 * c + k)}" for k in range(4)],
-              f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt(0)")
+        if ahead:
+            # chunk c's partner rows were issued a chunk ago: allow the next chunk's 4 reads to stay in flight
+            nxt = pread(c + 1) if c + 1 < 8 else []
+            B.raw(*nxt, f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt({len(nxt)})")
+        else:
+            B.raw(*pread(c), f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt(0)")
+        pb = pbufs[c % len(pbufs)]
         sg = Seg()
         gb = GBUF + 16 * (c % 2)
         for k in range(4):
             r = 4 * c + k
             m1, m2 = ms[(2 * k) % 4], ms[(2 * k + 1) % 4]
             x = X(dmap, r)
-            pl, ph = f"v{PBUF + 2 * k}", f"v{PBUF + 2 * k + 1}"
-            mac2(sg, m1, m2, x, (f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}"), (pl, ph, pv(PBUF + 2 * k)),
+            pl, ph = f"v{pb + 2 * k}", f"v{pb + 2 * k + 1}"
+            mac2(sg, m1, m2, x, (f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}"), (pl, ph, pv(pb + 2 * k)),
                  (f"v{gb + 8 + 2 * k}", f"v{gb + 9 + 2 * k}"))
         sched(B, sg)
         if c + 2 < 8:
