@@ -8,7 +8,7 @@
 // complete CMUX step — rotation, decomposition, forward transform, GGSW multiply-accumulate (the
 // partner's transformed polynomial comes through LDS), inverse transform, exact prime -> 2^64
 // modulus switch — as one generated asm body (tools/gen_pbs_kernel.py -> pbs_tw_body.hpp).  256
-// VGPRs and 32 KiB of LDS per workgroup: 2 waves per SIMD.  This wrapper computes the centered body
+// VGPRs and 33.5 KiB of LDS per workgroup (two 16.5 KiB wave buffers + tables): 2 waves per SIMD.  This wrapper computes the centered body
 // correction (if asked) before the loop and does the final rotation by -ms(b) + sample extraction.
 // Bit-exactness: the same restatement as pbs_kernels.hip (N^-1 folded into the key copy).
 #include <hip/hip_runtime.h>
@@ -22,6 +22,10 @@ namespace mi {
 namespace pbstw {
 
 static constexpr int N = 2048;
+// per-wave LDS buffer of the blind-rotation kernels (u64): N, padded to a 32 x 66 tile when the bodies run one-pass
+// transposes (tools/gen_pbs_kernel.py PBS_FULL_T); 2 x 16.5 KiB + the 512 B table per workgroup keeps 4 per CU
+static constexpr int NPW = MI_PBS_LDS_STRIDE;
+static_assert(NPW >= N, "a wave buffer holds at least one polynomial");
 static constexpr unsigned LOG_MOD = 12;  // PolynomialSize::to_blind_rotation_input_modulus_log
 
 __device__ __forceinline__ u64 modulus_switch(u64 input, unsigned log_modulus) {  // fft_impl/common.rs:10-23
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
                                                      const u64* __restrict__ lut, const u64* __restrict__ bsk,
                                                      uint32_t n_lwe, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab, int centered) {
-  __shared__ u64 buf[2 * N];
+  __shared__ u64 buf[2 * NPW];
   __shared__ u64 lwtab[64];
   const int t = threadIdx.x;
   const uint32_t lane = t & 63;
@@ -80,7 +84,7 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   u64 body_corr = 0;
   if (centered) body_corr = centered_body_correction(lwe, n_lwe, t, buf);
 
-  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
+  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * NPW), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * NPW);
   const u64* lutw = lut + (size_t)w * N;
   const u64* gown = bsk + (size_t)3 * w * N;
   const u64* gpar = bsk + (size_t)(2 - w) * N;
@@ -94,9 +98,9 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
                      [gpar_hi] "s"(gpar_hi), [lwe_lo] "s"(lwe_lo), [lwe_hi] "s"(lwe_hi), [n] "s"(n_lwe),
                      [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log),
                      [LW] "s"((uint32_t)(uintptr_t)lwtab));
-  // buf[w N + e] = acc_w[e].  Final rotation by -ms(b) (ntt64_bnf_pbs.rs:262-270), then sample
+  // buf[w NPW + e] = acc_w[e].  Final rotation by -ms(b) (ntt64_bnf_pbs.rs:262-270), then sample
   // extraction at nth = 0 (glwe_sample_extraction.rs:89-160): out[0] = A'[0], out[j] = -A'[N - j].
-  const u64* acc = buf + w * N;
+  const u64* acc = buf + w * NPW;
   const u64 body = modulus_switch(lwe[n_lwe] + body_corr, LOG_MOD);
   const int full = (int)(body / N) & 1, rem = (int)(body % N);
   u64* out = lwe_out + (size_t)b * (N + 1);
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
                                                          const u64* __restrict__ lut, const u64* __restrict__ bsk,
                                                          uint32_t n_lwe, uint32_t batch, int base_log,
                                                          const u64* __restrict__ tab) {
-  __shared__ u64 buf[2 * N];
+  __shared__ u64 buf[2 * NPW];
   __shared__ u64 lwtab[64];
   const int t = threadIdx.x;
   const uint32_t lane = t & 63;
@@ -163,11 +167,11 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
       const int m = 64 * r + (int)lane;  // new[m] = old[(m + rem) % N], negated for m >= N - rem
       u64 v = l[(m + rem) & (N - 1)];
       if (full ^ (m >= N - rem)) v = neg_custom(v);
-      buf[w * N + m] = v;
+      buf[w * NPW + m] = v;
     }
   }
   __syncthreads();
-  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
+  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * NPW), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * NPW);
   const u64* gown = bsk + (size_t)3 * w * N;
   const u64* gpar = bsk + (size_t)(2 - w) * N;
   const uint32_t gown_lo = (uint32_t)(uintptr_t)gown, gown_hi = (uint32_t)((uintptr_t)gown >> 32);
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
                      [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [lwe_lo] "s"(lwe_lo), [lwe_hi] "s"(lwe_hi),
                      [n] "s"(n_lwe), [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log),
                      [LW] "s"((uint32_t)(uintptr_t)lwtab));
-  const u64* acc = buf + w * N;
+  const u64* acc = buf + w * NPW;
   u64* out = lwe_out + (size_t)b * (N + 1);
   if (w == 0) {
 #pragma unroll 4

@@ -413,17 +413,24 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False):
     return out if out_of_place else data
 
 
-def _lds_with_lane_pair_tables(tab, N):
-    """Workgroup LDS as pbs_tw.hip lays it out: 2 x N exchange buffers, then the 32 forward lane-pair twiddles
-    (tab[N:N+32]) and the W1'' inverse's 32 last-DIT-stage twiddles, entry m + 16 par = 2^(-3 (2 m + par) mod 192)
-    (the plan's fourth table region, c_api.cpp)."""
+def _lds_with_lane_pair_tables(tab, N, stride=None):
+    """Workgroup LDS as pbs_tw.hip lays it out: 2 exchange buffers of `stride` u64 (default N), then the 32 forward
+    lane-pair twiddles (tab[N:N+32]) and the W1'' inverse's 32 last-DIT-stage twiddles, entry m + 16 par =
+    2^(-3 (2 m + par) mod 192) (the plan's fourth table region, c_api.cpp)."""
     P = 0xFFFFFFFF00000001
-    lds = np.zeros(2 * N + 64, dtype=np.uint64)
+    st = stride or N
+    lds = np.zeros(2 * st + 64, dtype=np.uint64)
     t = np.array(tab, dtype=np.uint64)
-    lds[2 * N:2 * N + 32] = t[N:N + 32]
-    lds[2 * N + 32:2 * N + 64] = [pow(2, (192 - 3 * (2 * m + par) % 192) % 192, P)
-                                  for par in range(2) for m in range(16)]
+    lds[2 * st:2 * st + 32] = t[N:N + 32]
+    lds[2 * st + 32:2 * st + 64] = [pow(2, (192 - 3 * (2 * m + par) % 192) % 192, P)
+                                    for par in range(2) for m in range(16)]
     return lds
+
+
+def pbs_lds_stride(hdr):
+    """MI_PBS_LDS_STRIDE of a generated pbs_tw_body.hpp (u64 per wave buffer of the blind-rotation bodies)."""
+    m = re.search(r"#define MI_PBS_LDS_STRIDE (\d+)", open(hdr).read())
+    return int(m.group(1)) if m else 2048
 
 
 def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1", acc0=None):
@@ -436,18 +443,21 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1", acc0=None):
     LB, UB, KB, TB = 0x100000000, 0x200000000, 0x300000000, 0x400000000
     mem = {LB: np.array(lwe, dtype=np.uint64), UB: np.array(lut, dtype=np.uint64).reshape(-1),
            KB: np.array(bsk, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
-    lds = _lds_with_lane_pair_tables(tab, N)
+    st = pbs_lds_stride(hdr)
+    lds = _lds_with_lane_pair_tables(tab, N, st)
     if acc0 is not None:
-        lds[:2 * N] = np.array(acc0, dtype=np.uint64).reshape(-1)
+        a0 = np.array(acc0, dtype=np.uint64).reshape(2, N)
+        for w in range(2):
+            lds[w * st:w * st + N] = a0[w]
     lines = body_lines(hdr, name, "MI_PBS_BODY_")
     waves = []
     for w in range(2):
-        ops = {"lane": "v0", "S": str(w * N * 8), "SP": str((1 - w) * N * 8),
+        ops = {"lane": "v0", "S": str(w * st * 8), "SP": str((1 - w) * st * 8),
                "lut_lo": str((UB + w * N * 8) & 0xFFFFFFFF), "lut_hi": str((UB + w * N * 8) >> 32),
                "gown_lo": str((KB + 3 * w * N * 8) & 0xFFFFFFFF), "gown_hi": str((KB + 3 * w * N * 8) >> 32),
                "gpar_lo": str((KB + (2 - w) * N * 8) & 0xFFFFFFFF), "gpar_hi": str((KB + (2 - w) * N * 8) >> 32),
                "lwe_lo": str(LB & 0xFFFFFFFF), "lwe_hi": str(LB >> 32), "n": str(n_lwe),
-               "tab_lo": str(TB & 0xFFFFFFFF), "tab_hi": str(TB >> 32), "bl": str(base_log), "LW": str(2 * N * 8)}
+               "tab_lo": str(TB & 0xFFFFFFFF), "tab_hi": str(TB >> 32), "bl": str(base_log), "LW": str(2 * st * 8)}
         wv = Wave(ops, mem, lds=lds)
         wv.v[0] = np.arange(LANES, dtype=np.uint64)
         wv.load(lines)
@@ -460,7 +470,7 @@ def run_pbs(hdr, lwe, lut, bsk, tab, base_log, n_lwe, name="bnf_l1", acc0=None):
                     next(waves[k])
                 except StopIteration:
                     live[k] = False
-    return lds[:2 * N].reshape(2, N).copy()
+    return np.stack([lds[w * st:w * st + N] for w in range(2)]).copy()
 
 
 def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False, sol=False):

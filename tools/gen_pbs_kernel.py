@@ -65,13 +65,25 @@ def addr_for(tab):
 
 
 FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
+# The blind-rotation bodies own 16.5 KiB of LDS per wave (PBS_LDS_STRIDE u64): their forward T1 and inverse W1'' -> W0
+# transposes run in one pass through a 32 x 66 tile (gen_tw_kernel.t1_full) instead of two lane halves with exec flips
+# and three waits.  V_TB = S + 8 (66 (lane >> 1) + (lane & 1)); the tile's other address is V_T4R = S + 8 lane.
+PBS_FULL_T = True
+PBS_LDS_STRIDE = 32 * 66 if PBS_FULL_T else 2048   # u64 per wave buffer (pbs_tw.hip MI_PBS_LDS_STRIDE)
+V_TB = 250
+FWD_ADDR_P, INV_ADDR_P = addr_for(S_TWF), addr_for(S_TWI)
+for _a in (FWD_ADDR_P, INV_ADDR_P):
+    _a.full_t, _a.tfw, _a.tfb = PBS_FULL_T, f"v{V_T4R}", f"v{V_TB}"
 # the lane-pair twiddles (32 forward + the inverse's 32 last-DIT-stage twiddles of the W1'' layout) live in the
 # workgroup's LDS (copied by pbs_tw.hip at kernel start): lookups at LDS instead of L2 latency.
 # V_LWL = table base + 128 * (lane & 1).
 V_LWL = 248
-FWD_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
-INV_ADDR.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
-FWD_ADDR.lw_wait = INV_ADDR.lw_wait = "s_waitcnt lgkmcnt(0)"
+for _a in (FWD_ADDR, FWD_ADDR_P):
+    _a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
+for _a in (INV_ADDR, INV_ADDR_P):
+    _a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
+for _a in (FWD_ADDR, INV_ADDR, FWD_ADDR_P, INV_ADDR_P):
+    _a.lw_wait = "s_waitcnt lgkmcnt(0)"
 
 
 def sched(B, sg):
@@ -119,7 +131,9 @@ def prologue(B):
           f"v_lshlrev_b32 v{V_LWO}, 7, v9", f"v_add_u32 v{V_LWO}, 0x4000, v{V_LWO}",
           f"v_lshlrev_b32 v{V_LWL}, 7, v9", f"v_add_u32 v{V_LWL}, %[LW], v{V_LWL}",
           "v_lshrrev_b32 v17, 5, %[lane]", "v_add_u32 v17, %[lane], v17", "v_lshlrev_b32 v17, 3, v17",
-          f"v_add_u32 v{V_T1X}, %[S], v17")
+          f"v_add_u32 v{V_T1X}, %[S], v17",
+          "v_mul_u32_u24 v18, 66, v10", "v_add_u32 v18, v18, v9", "v_lshlrev_b32 v18, 3, v18",
+          f"v_add_u32 v{V_TB}, %[S], v18")
 
 
 def load_rows(dst, base):
@@ -439,14 +453,16 @@ def tw_key_index(pos):
     return 64 * (L >> 1) + 32 * (L & 1) + 2 * (R & 15) + (R >> 4)
 
 
-def fwd_mac_inv(B, tabs, dmap0, w1p):
+def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False):
     """Forward transform (its stage 0 already run), the MAC with the partner wave and the inverse; returns the output
     dmap (W0, canonical).  w1p: the MAC and the inverse's input stay in the forward's W1' layout (PBS_W1P)."""
     if w1p:
-        dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1, stop="last")
+        fa, ia = (FWD_ADDR_P, INV_ADDR_P) if full_t else (FWD_ADDR, INV_ADDR)
+        dmap = T.fwd_core(B, tabs, dmap0, fa, first_stage=1, stop="last")
         mac(B, dmap)
-        assert dmap == [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)], dmap
-        return T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64))
+        assert dmap == ([64 + 2 * q for q in range(32)] if full_t else
+                        [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)]), dmap
+        return T.inv_core(B, tabs, dmap, ia, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64))
     dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1)
     mac(B, dmap)
     return T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
@@ -482,7 +498,7 @@ def gen_pbs(tabs, sol=False):
     B.raw(*gload(0), *gload(1))
     rotate_decompose(B, sol)
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
-    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], PBS_W1P)
+    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], PBS_W1P, full_t=PBS_W1P and PBS_FULL_T)
     if sol:
         add_acc_sol(B, dmap)
     else:
@@ -598,6 +614,7 @@ def main():
     print("#pragma once")
     print(f"#define MI_PBS_W1P {int(PBS_W1P)}  // blind rotation reads its key in the W1' order (tw_key_index)")
     print(f"#define MI_EXT_W1P {int(EXT_W1P)}  // external product / CMUX read their GGSW in the W1' order")
+    print(f"#define MI_PBS_LDS_STRIDE {PBS_LDS_STRIDE}  // u64 per wave LDS buffer of the blind-rotation bodies")
     print(emit("bnf_l1", b))
     e, c = gen_ext(tabs, False), gen_ext(tabs, True)
     print(emit("ext_bnf_l1", e))

@@ -602,9 +602,29 @@ NTT_ADDR = Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, %[l8], s[{S_
                 **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw", "t1x", "t1y")})
 
 
+FULL_STRIDE = 66  # row stride (u64) of the one-pass transposes of a wave with a 16.5 KiB LDS buffer (ad.full_t)
+
+
+def t1_full(body, dmap, ad):
+    """W0 -> W1 in one pass through a 32 x 66 (u64) LDS tile: lane j writes its 32 rows at i 66 + j (%[tfw] = S + 8 lane,
+    row in the offset field), lane 2 i + j0 reads element j = 2 q + j0 of row i into register q (%[tfb] = S + 8 (66 i + j0),
+    q in the offset field).  Both sides conflict-free (the reads' 64-bank pattern is 4 i + 2 j0).  For waves that own
+    16.5 KiB of LDS (the blind rotation); the 8.5 KiB standalone waves run the two-half t1.  The data stays in the same
+    registers (every write has landed before the first read)."""
+    L = [f"ds_write_b64 {ad.tfw}, {pv(dmap[r])} offset:{r * FULL_STRIDE * 8}" for r in range(32)]
+    L.append("s_waitcnt lgkmcnt(0)")
+    L += [f"ds_read_b64 {pv(dmap[q])}, {ad.tfb} offset:{q * 16}" for q in range(32)]
+    L.append("s_waitcnt lgkmcnt(0)")
+    body.raw(*L)
+    return list(dmap)
+
+
 def t1(body, dmap, ybase, newhi, ad=NTT_ADDR, row_waits=None):
     """W0 -> W1 (split by j half).  Returns the new dmap (x[q] in y for q < 16, x[16+q] at newhi).
     row_waits: a wait line before each first-half row write (rows written as their loads land)."""
+    if getattr(ad, "full_t", False):
+        assert row_waits is None
+        return t1_full(body, dmap, ad)
     L = []
     L += [f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"]
     for r in range(32):
@@ -1065,7 +1085,16 @@ def t1_w1pp(body, dmap, dst, ad=NTT_ADDR):
 
 def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR):
     """After pair_stage_dit lane 2 i + par holds output n = 2 m + par + 32 q in register 2 m + q: -> W0 through
-    LDS, halves split by i (rows (i & 15) 66, columns n + (n >> 5)); reads at %[t1x] + 66 rho."""
+    LDS, halves split by i (rows (i & 15) 66, columns n + (n >> 5)); reads at %[t1x] + 66 rho.  ad.full_t: one pass
+    through the 32 x 66 tile of t1_full (writes at %[tfb] + 2 m + 32 q, reads at %[tfw] + 66 i), the rows landing in
+    the registers of dmap."""
+    if getattr(ad, "full_t", False):
+        L = [f"ds_write_b64 {ad.tfb}, {pv(dmap[R])} offset:{(2 * (R >> 1) + 32 * (R & 1)) * 8}" for R in range(32)]
+        L.append("s_waitcnt lgkmcnt(0)")
+        L += [f"ds_read_b64 {pv(dmap[i])}, {ad.tfw} offset:{i * FULL_STRIDE * 8}" for i in range(32)]
+        L.append("s_waitcnt lgkmcnt(0)")
+        body.raw(*L)
+        return list(dmap)
     L = []
     for h in range(2):
         L += EXEC_LO if h == 0 else EXEC_HI
@@ -1145,6 +1174,7 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
     if w1p_in:
         dmap = w1p_as_w1pp(dmap)
     else:
+        assert not getattr(ad, "full_t", False)
         dmap = t1_w1pp(B, dmap, dst or [8 + 2 * r for r in range(32)], ad)
     ms = pair_stage_dit_gmul_ms()
     pre = {m: pre_base + 2 * i for i, m in enumerate(ms)}
@@ -1157,7 +1187,7 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
     for s in range(5):
         B.stage("ct", 1 << s, dit_exps_pp(s), dmap, fb, cf, by_reg=True)
     pair_stage_dit(B, dmap, ad, pre, busy)
-    assert not set(range(ybase, ybase + 32)) & {r for b in dmap for r in (b, b + 1)}
+    assert getattr(ad, "full_t", False) or not set(range(ybase, ybase + 32)) & {r for b in dmap for r in (b, b + 1)}
     return t_w1pp_w0(B, dmap, ybase, newhi, ad)
 
 
