@@ -249,6 +249,9 @@ def stage0_signed(B, tabs, dmap, rows=range(16)):
     sched(B, sg)
 
 
+ROT_ALL_READS = True   # the rotation's 32 LDS reads issued together (one exposed LDS round trip instead of two)
+
+
 def rotate_decompose(B, sol=False):
     """dmap v64..v127 <- decompose(+-acc[(e - a) mod N] - acc[e]); Solinas bodies negate and subtract
     modulo p (polynomial_wrapping_monic_monomial_mul_assign_custom_mod, then the CMUX difference)."""
@@ -256,16 +259,29 @@ def rotate_decompose(B, sol=False):
           f"s_lshr_b32 s{S_FULL}, s{S_AMS}, 11", f"s_sub_u32 s{S_FULL}, 0, s{S_FULL}",
           f"v_subrev_u32 v{V_U8}, s{S_R8}, v{VOFF}")
     B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(ACC + 2 * r)} offset:{512 * r}" for r in range(32)])
-    for h in range(2):
-        rows = list(range(16 * h, 16 * h + 16))
+    if ROT_ALL_READS:
+        # all 32 source addresses (v8..v39), all 32 reads in flight, then half 0 computes while half 1 lands
         sg = Seg()
-        for q, r in enumerate(rows):
-            a = f"v{8 + q}"
+        for r in range(32):
+            a = f"v{8 + r}"
             sg.add(f"v_add_u32 {a}, {512 * r}, v{V_U8}", [f"v{V_U8}"], [a])
             sg.add(f"v_and_b32 {a}, 0x3ff8, {a}", [a], [a])
             sg.add(f"v_add_u32 {a}, %[S], {a}", [a], [a])
         sched(B, sg)
-        B.raw(*[f"ds_read_b64 {pv(64 + 2 * r)}, v{8 + q}" for q, r in enumerate(rows)], "s_waitcnt lgkmcnt(0)")
+        B.raw(*[f"ds_read_b64 {pv(64 + 2 * r)}, v{8 + r}" for r in range(32)])
+    for h in range(2):
+        rows = list(range(16 * h, 16 * h + 16))
+        if ROT_ALL_READS:
+            B.raw("s_waitcnt lgkmcnt(15)" if h == 0 else "s_waitcnt lgkmcnt(0)")  # (in order: <= 15 left = rows 0..16)
+        else:
+            sg = Seg()
+            for q, r in enumerate(rows):
+                a = f"v{8 + q}"
+                sg.add(f"v_add_u32 {a}, {512 * r}, v{V_U8}", [f"v{V_U8}"], [a])
+                sg.add(f"v_and_b32 {a}, 0x3ff8, {a}", [a], [a])
+                sg.add(f"v_add_u32 {a}, %[S], {a}", [a], [a])
+            sched(B, sg)
+            B.raw(*[f"ds_read_b64 {pv(64 + 2 * r)}, v{8 + q}" for q, r in enumerate(rows)], "s_waitcnt lgkmcnt(0)")
         sg = Seg()
         sls = slots_at([8, 16, 24, 32, 40, 48, 56])
         for q, r in enumerate(rows):
