@@ -249,7 +249,9 @@ def stage0_signed(B, tabs, dmap, rows=range(16)):
     sched(B, sg)
 
 
-ROT_ALL_READS = True   # the rotation's 32 LDS reads issued together (one exposed LDS round trip instead of two)
+# the rotation's 32 LDS reads issued together (one exposed LDS round trip instead of two): emulator-exact, but BNF
+# 35.9 k -> 35.2 k PBS/s in a one-box A/B (profiles/r3/pbs_rot_all_reads_ab/): off
+ROT_ALL_READS = False
 
 
 def rotate_decompose(B, sol=False):
