@@ -202,7 +202,7 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
                                                      const u64* __restrict__ ggsw_list, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab, const uint32_t* __restrict__ gidx,
                                                      uint32_t n_ggsw) {
-  __shared__ u64 buf[2 * N];
+  __shared__ u64 buf[2 * MI_EXT_LDS_STRIDE];
   __shared__ u64 lwtab[64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -213,7 +213,8 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
   if (gi >= n_ggsw) return;  // uniform per workgroup
   const u64* ggsw = ggsw_list + (size_t)gi * 4 * N;
   load_lane_pair_tables(lwtab, tab, threadIdx.x);
-  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * N), SP = (uint32_t)(uintptr_t)(buf + (1 - w) * N);
+  const uint32_t S = (uint32_t)(uintptr_t)(buf + w * MI_EXT_LDS_STRIDE),
+                 SP = (uint32_t)(uintptr_t)(buf + (1 - w) * MI_EXT_LDS_STRIDE);
   u64* o = out + ((size_t)b * 2 + w) * N;
   u64* g = glwe + ((size_t)b * 2 + w) * N;
   const u64* gown = ggsw + (size_t)3 * w * N;

@@ -427,9 +427,9 @@ def _lds_with_lane_pair_tables(tab, N, stride=None):
     return lds
 
 
-def pbs_lds_stride(hdr):
-    """MI_PBS_LDS_STRIDE of a generated pbs_tw_body.hpp (u64 per wave buffer of the blind-rotation bodies)."""
-    m = re.search(r"#define MI_PBS_LDS_STRIDE (\d+)", open(hdr).read())
+def pbs_lds_stride(hdr, which="PBS"):
+    """MI_PBS_LDS_STRIDE (MI_EXT_LDS_STRIDE: which="EXT") of a generated pbs_tw_body.hpp (u64 per wave buffer)."""
+    m = re.search(r"#define MI_%s_LDS_STRIDE (\d+)" % which, open(hdr).read())
     return int(m.group(1)) if m else 2048
 
 
@@ -481,19 +481,20 @@ def run_ext(hdr, glwe, out, ggsw, tab, base_log, cmux=False, sol=False):
     g = np.array(glwe, dtype=np.uint64).reshape(-1).copy()
     o = np.array(out, dtype=np.uint64).reshape(-1).copy()
     mem = {GB: g, OB: o, KB: np.array(ggsw, dtype=np.uint64).reshape(-1), TB: np.array(tab, dtype=np.uint64)}
-    lds = _lds_with_lane_pair_tables(tab, N)
+    st = pbs_lds_stride(hdr, "EXT")
+    lds = _lds_with_lane_pair_tables(tab, N, st)
     kind = "sol" if sol else "bnf"
     lines = body_lines(hdr, f"cmux_{kind}_l1" if cmux else f"ext_{kind}_l1", "MI_PBS_BODY_")
     waves = []
     for w in range(2):
         lo = lambda a: str(a & 0xFFFFFFFF)
         hi = lambda a: str(a >> 32)
-        ops = {"lane": "v0", "S": str(w * N * 8), "SP": str((1 - w) * N * 8),
+        ops = {"lane": "v0", "S": str(w * st * 8), "SP": str((1 - w) * st * 8),
                "glwe_lo": lo(GB + w * N * 8), "glwe_hi": hi(GB + w * N * 8),
                "out_lo": lo(OB + w * N * 8), "out_hi": hi(OB + w * N * 8),
                "gown_lo": lo(KB + 3 * w * N * 8), "gown_hi": hi(KB + 3 * w * N * 8),
                "gpar_lo": lo(KB + (2 - w) * N * 8), "gpar_hi": hi(KB + (2 - w) * N * 8),
-               "tab_lo": lo(TB), "tab_hi": hi(TB), "bl": str(base_log), "LW": str(2 * N * 8)}
+               "tab_lo": lo(TB), "tab_hi": hi(TB), "bl": str(base_log), "LW": str(2 * st * 8)}
         wv = Wave(ops, mem, lds=lds)
         wv.v[0] = np.arange(LANES, dtype=np.uint64)
         wv.load(lines)

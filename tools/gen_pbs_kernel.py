@@ -531,11 +531,12 @@ def gen_pbs(tabs, sol=False):
     return B
 
 
-# the external product / CMUX bodies: the same W1' step on a GGSW permuted into the body's order per call
-# (pbs_tw.hip launch_ext_tw: the caller's Raw / Normalize GGSW stays in the reference's order).  Off: emulator- and
-# GPU-exact, but 26.72 vs 26.57 M products/s in a one-box A/B (+0.5 %, profiles/r3/ext_w1p_ab/): the per-call
-# reorder launch costs about what the two transposes saved (~5 us of a 307 us launch)
-EXT_W1P = False
+# the external product / CMUX bodies: the same W1' step (with the one-pass transposes of PBS_FULL_T) on a GGSW permuted
+# into the body's order per call (pbs_tw.hip launch_ext_tw: the caller's Raw / Normalize GGSW stays in the reference's
+# order).  One-box A/Bs: without the one-pass transposes +0.5 % (profiles/r3/ext_w1p_ab/: the per-call reorder launch
+# costs about what the two skipped transposes saved), with them 27.70 -> 28.02 M products/s, +1.2 %
+# (profiles/r3/ext_w1p_full_t_ab/)
+EXT_W1P = True
 EXT_PROGRESSIVE = True  # external product: decompose + first stage per group of rows as they arrive
 
 
@@ -574,7 +575,7 @@ def gen_ext(tabs, cmux, sol=False):
             sched(B, sg)
             stage0_signed(B, tabs, dmap0, rows=range(4 * g, 4 * g + 4))
         B.raw(*load_rows(ACC, S_OUT))
-        dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P)
+        dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P, full_t=EXT_W1P and PBS_FULL_T)
         if sol:
             add_acc_sol(B, dmap)
         else:
@@ -606,7 +607,7 @@ def gen_ext(tabs, cmux, sol=False):
         (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
     sched(B, sg)
     stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
-    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], EXT_W1P)
+    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], EXT_W1P, full_t=EXT_W1P and PBS_FULL_T)
     if sol:
         add_acc_sol(B, dmap)
     else:
@@ -633,6 +634,7 @@ def main():
     print(f"#define MI_PBS_W1P {int(PBS_W1P)}  // blind rotation reads its key in the W1' order (tw_key_index)")
     print(f"#define MI_EXT_W1P {int(EXT_W1P)}  // external product / CMUX read their GGSW in the W1' order")
     print(f"#define MI_PBS_LDS_STRIDE {PBS_LDS_STRIDE}  // u64 per wave LDS buffer of the blind-rotation bodies")
+    print(f"#define MI_EXT_LDS_STRIDE {PBS_LDS_STRIDE if EXT_W1P else 2048}  // u64 per wave LDS buffer of the external-product bodies")
     print(emit("bnf_l1", b))
     e, c = gen_ext(tabs, False), gen_ext(tabs, True)
     print(emit("ext_bnf_l1", e))
