@@ -414,9 +414,10 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
 #pragma unroll
     for (int r = 0; r < 16; ++r) buf[r * 64 + lane] = u[r];
     // update_with_fmadd: y_w = sum_rr X_rr * G[rr][w] (own transform from registers, the other K from LDS).
-    // Branch-free (the other rows are rr = o + (o >= w), o < K); the key rows are loaded in batches of HB = 4
-    // positions, each issued one batch ahead (the first before the exchange barrier, so its latency overlaps the
-    // wait).  One-box A/Bs: HB = 4 is 0.9 % faster than 2, HB = 8 1.9 % slower than 4 (profiles/r3/fft_hb*_ab).
+    // Branch-free (the other rows are rr = o + (o >= w), o < K); the key rows are loaded in batches of HB positions,
+    // each issued one batch ahead (the first before the exchange barrier, so its latency overlaps the wait).  One-box
+    // A/Bs: in the 4-ciphertext PBS workgroups HB = 4 is 0.9 % faster than 2 and HB = 8 1.9 % slower than 4
+    // (profiles/r3/fft_hb*_ab); the one-ciphertext external-product workgroups (WGB) lost 10 % with 4, so they keep 2.
     const cplx* gw = ggsw + (size_t)(w * (K + 1) + w) * M + lane;
     const cplx* go[K];
     const cplx* xo[K];
@@ -426,7 +427,7 @@ __device__ __forceinline__ void ext_product_add(u64 (&acc)[NPL], const u64 (&ct1
       go[o] = ggsw + (size_t)(rr * (K + 1) + w) * M + lane;
       xo[o] = pair + rr * BUF + lane;
     }
-    constexpr int HB = 4;
+    constexpr int HB = WGB ? 2 : 4;
     cplx kw[HB], ko[K][HB];
 #pragma unroll
     for (int j = 0; j < HB; ++j) {

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """bench.py's config-3 external-product leg alone, repeated (diagnostic A/B of body variants):
-python tools/ext_probe.py [reps] [package dir holding tfhe_ntt_amd/]"""
+python tools/ext_probe.py [reps] [package dir holding tfhe_ntt_amd/] [fft: the f64 leg instead]"""
 import json
 import os
 import sys
@@ -25,5 +25,9 @@ dev = torch.device("cuda", 0)
 bench.SIMDS = torch.cuda.get_device_properties(dev).multi_processor_count * 4
 torch.cuda.set_stream(torch.cuda.Stream(device=dev))
 for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
+    if len(sys.argv) > 3 and sys.argv[3] == "fft":
+        r = bench.bench_ext_product_fft(A, eng, torch, dev, 1, lambda: None, None)
+        print(json.dumps({"value": r["value"], "kernel_ms": r["kernel_ms"], "k2_l2": r["k2_l2"]["value"]}), flush=True)
+        continue
     r = bench.bench_ext_product(A, eng, torch, dev, 1, lambda: None, None)
     print(json.dumps({"value": r["value"], "kernel_ms": r["kernel_ms"], "valu_frac": r["roofline"]["frac"]}), flush=True)
