@@ -8,6 +8,7 @@
 // and the f64-FFT mirror (namespace fft64) against exact integer arithmetic within the f64 error bound:
 //   forward_as_torus -> backward_as_torus round trip, add_external_product_assign vs the exact negacyclic product
 // Needs a HIP device.  Build: make -C tests/cpp.
+#include <cmath>
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
@@ -152,6 +153,13 @@ int main() {
       fft.to_standard_order(nat, four, batch);
       fft.from_standard_order(nat, nat, batch);
       EXPECT(hipMemcpy(h1.data(), nat, batch * NF * 8, hipMemcpyDeviceToHost) == hipSuccess);
+      if (h0 != h1) {
+        size_t bad = 0, first = 0;
+        for (size_t i = 0; i < h0.size(); ++i)
+          if (h0[i] != h1[i] && bad++ == 0) first = i;
+        std::fprintf(stderr, "f64 standard-order round trip N = %zu: %zu of %zu doubles differ, first at %zu\n", NF, bad,
+                     h0.size(), first);
+      }
       EXPECT(h0 == h1);
       (void)hipFree(nat);
     }
@@ -201,6 +209,8 @@ int main() {
         const int64_t d = (int64_t)(got[c * NF + e] - acc);
         worst = std::max(worst, d < 0 ? -d : d);
       }
+    if (worst >= (int64_t(1) << (NF > 2048 ? 50 : 48)))
+      std::fprintf(stderr, "f64 external product N = %zu: worst |error| 2^%.2f\n", NF, std::log2((double)worst));
     EXPECT(worst < (int64_t(1) << (NF > 2048 ? 50 : 48)));  // the f64 bound grows with sqrt(N log N)
     {  // the reference's FourierLweBootstrapKey bytes: write, load (a key owning its copy), write again: same bytes
       tfhe_ntt_amd::fft64::FourierBootstrapKey key(fft, fg, 1, bl, 1);

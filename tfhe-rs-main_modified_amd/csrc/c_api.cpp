@@ -18,6 +18,7 @@
 #include <tuple>
 #include <vector>
 
+#include "scratch.hpp"
 #include "build_info.hpp"  // build/ (Makefile): MI_SOURCE_HASH
 #include "c_api_internal.hpp"
 #include "ntt64_tw_tables.hpp"
@@ -662,27 +663,27 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
     const size_t count = batch * (key->n_lwe + 1);
     u64* sw = nullptr;
     if (ms_mode != MI_MS_PRE_SWITCHED) {
-      if (hipMallocAsync((void**)&sw, count * sizeof(u64), s) != hipSuccess)
+      if (mi::scratch_alloc((void**)&sw, count * sizeof(u64), s) != hipSuccess)
         return fail(MI_ERR_OOM, "scratch allocation failed");
       hipError_t e = mi::launch_ms_non_native(sw, lwe_in, count, s);
       if (e != hipSuccess) {
-        (void)hipFreeAsync(sw, s);
+        (void)mi::scratch_free(sw, s);
         return hip_fail(e, "modulus switch launch");
       }
     }
     hipError_t e = mi::launch_pbs_tw_sol(lwe_out, sw ? sw : lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
                                          plan->d_twist_f, s);
-    if (sw) (void)hipFreeAsync(sw, s);
+    if (sw) (void)mi::scratch_free(sw, s);
     return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
   }
   u64* lifted = nullptr;  // PRE_SWITCHED: stream-ordered copy lifted back to the standard switch
   if (ms_mode == MI_MS_PRE_SWITCHED) {
     const size_t count = batch * (key->n_lwe + 1);
-    if (hipMallocAsync((void**)&lifted, count * sizeof(u64), s) != hipSuccess)
+    if (mi::scratch_alloc((void**)&lifted, count * sizeof(u64), s) != hipSuccess)
       return fail(MI_ERR_OOM, "scratch allocation failed");
     hipError_t e = mi::launch_lift_switched(lifted, lwe_in, count, key->variant == MI_NTT64_BNF, plan->logn, s);
     if (e != hipSuccess) {
-      (void)hipFreeAsync(lifted, s);
+      (void)mi::scratch_free(lifted, s);
       return hip_fail(e, "lift launch");
     }
     lwe_in = lifted;
@@ -699,7 +700,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   else
     e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
                        key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);
-  if (lifted) (void)hipFreeAsync(lifted, s);
+  if (lifted) (void)mi::scratch_free(lifted, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
 }
 
@@ -892,7 +893,7 @@ int mi_native_polymul_batch(const mi_native_plan* plan, void* prod, const void* 
   const size_t count = batch * plan->n;
   DeviceGuard g(plan->device);
   u64* scratch = nullptr;  // [lhs residues: k planes | rhs residues: k planes], stream-ordered
-  hipError_t e = hipMallocAsync((void**)&scratch, 2 * (size_t)plan->k * count * sizeof(u64), s);
+  hipError_t e = mi::scratch_alloc((void**)&scratch, 2 * (size_t)plan->k * count * sizeof(u64), s);
   if (e != hipSuccess) return fail(MI_ERR_OOM, "scratch allocation failed");
   u64* a = scratch;
   u64* b = scratch + (size_t)plan->k * count;
@@ -912,7 +913,7 @@ int mi_native_polymul_batch(const mi_native_plan* plan, void* prod, const void* 
     e = mi::launch_crt_reconstruct(prod, a, count, plan->width, plan->crt, s);
     if (e != hipSuccess) st = hip_fail(e, "reconstruct launch");
   }
-  (void)hipFreeAsync(scratch, s);
+  (void)mi::scratch_free(scratch, s);
   return st;
 }
 
@@ -994,11 +995,11 @@ int mi_lwe_keyswitch_batch(const mi_lwe_ksk* key, uint64_t* lwe_out, const uint6
   const hipStream_t s = (hipStream_t)stream;
   DeviceGuard g(key->device);
   void* digits = nullptr;  // int8 digit fragments, stream-ordered scratch
-  if (hipMallocAsync(&digits, mi::ks_digit_bytes(key->in_dim, key->base_log, key->level, batch), s) != hipSuccess)
+  if (mi::scratch_alloc((void**)&digits, mi::ks_digit_bytes(key->in_dim, key->base_log, key->level, batch), s) != hipSuccess)
     return fail(MI_ERR_OOM, "scratch allocation failed");
   hipError_t e = mi::launch_keyswitch(lwe_out, lwe_in, key->frag, digits, batch, key->in_dim, key->out_dim,
                                       key->base_log, key->level, s);
-  (void)hipFreeAsync(digits, s);
+  (void)mi::scratch_free(digits, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "keyswitch launch");
 }
 

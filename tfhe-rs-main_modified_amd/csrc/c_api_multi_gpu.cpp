@@ -12,6 +12,7 @@
 #include <new>
 #include <vector>
 
+#include "scratch.hpp"
 #include "c_api_internal.hpp"
 
 using namespace mi::capi;
@@ -282,7 +283,7 @@ int multi_gpu_pbs(mi_multi_gpu* m, const Key* const* keys, uint64_t* lwe_out, co
       break;
     }
     uint64_t* buf = nullptr;
-    if (hipMallocAsync((void**)&buf, n * (in_w + out_w) * sizeof(uint64_t), m->streams[i]) != hipSuccess)
+    if (mi::scratch_alloc((void**)&buf, n * (in_w + out_w) * sizeof(uint64_t), m->streams[i]) != hipSuccess)
       st = fail(MI_ERR_OOM, "shard scratch allocation failed");
     scratch[i] = ins[i] = buf;
     outs[i] = buf ? buf + n * in_w : nullptr;
@@ -315,7 +316,7 @@ int multi_gpu_pbs(mi_multi_gpu* m, const Key* const* keys, uint64_t* lwe_out, co
   for (size_t i = 1; i < G; ++i)
     if (scratch[i]) {
       DeviceGuard g(m->devices[i]);
-      (void)hipFreeAsync(scratch[i], m->streams[i]);
+      (void)mi::scratch_free(scratch[i], m->streams[i]);
     }
   // the producer streams follow the last use of their key / LUT (shard 0's is `stream`, which the gather ordered)
   for (size_t i = 0; i < G && st == MI_OK; ++i) {

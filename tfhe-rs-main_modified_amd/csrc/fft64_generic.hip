@@ -35,6 +35,7 @@
 
 #include <algorithm>
 
+#include "scratch.hpp"
 #include "fft64_device.hpp"
 #include "fft64_launch.hpp"
 
@@ -411,6 +412,11 @@ __host__ __device__ __forceinline__ uint32_t frequency_at(uint32_t pos, uint32_t
   return (pos >> logc) | (brev(pos & ((1u << logc) - 1u), (int)logc) << logr);
 }
 
+// the in-place reorder's staging copy (a kernel, not an SDMA copy: ordered on the stream like every other launch)
+__global__ __launch_bounds__(256) void copy_cplx_kernel(cplx* __restrict__ out, const cplx* __restrict__ in, uint64_t n) {
+  for (uint64_t i = gs_start(); i < n; i += gs_stride()) out[i] = in[i];
+}
+
 template <bool TO_STD>
 __global__ __launch_bounds__(256) void reorder_kernel(cplx* __restrict__ out, const cplx* __restrict__ in,
                                                       uint64_t polys, uint32_t logc, uint32_t logr) {
@@ -596,10 +602,10 @@ hipError_t launch_fftg_bwd_torus(uint64_t* std_, const double* fourier, size_t b
   const TorusSink sink{std_, g.untw, g.logn, add ? 1 : 0};
   if (g.logr == 0) return inverse(g, in, sink, nullptr, batch, s);
   cplx* tmp = nullptr;
-  hipError_t e = hipMallocAsync((void**)&tmp, (batch << g.logm) * sizeof(cplx), s);
+  hipError_t e = mi::scratch_alloc((void**)&tmp, (batch << g.logm) * sizeof(cplx), s);
   if (e != hipSuccess) return e;
   e = inverse(g, in, sink, tmp, batch, s);
-  const hipError_t ef = hipFreeAsync(tmp, s);
+  const hipError_t ef = mi::scratch_free(tmp, s);
   return e != hipSuccess ? e : ef;
 }
 
@@ -613,9 +619,10 @@ hipError_t launch_fftg_reorder(double* out, const double* in, size_t polys, bool
   cplx* tmp = nullptr;
   hipError_t e = hipSuccess;
   if (out == in) {  // a permutation in place: stage the input
-    if ((e = hipMallocAsync((void**)&tmp, bytes, s)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(tmp, in, bytes, hipMemcpyDeviceToDevice, s)) != hipSuccess) {
-      (void)hipFreeAsync(tmp, s);
+    if ((e = mi::scratch_alloc((void**)&tmp, bytes, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(copy_cplx_kernel, dim3(blocks_for(polys << g.logm)), dim3(256), 0, s, tmp, src, (uint64_t)(polys << g.logm));
+    if ((e = hipGetLastError()) != hipSuccess) {
+      (void)mi::scratch_free(tmp, s);
       return e;
     }
     src = tmp;
@@ -629,7 +636,7 @@ hipError_t launch_fftg_reorder(double* out, const double* in, size_t polys, bool
                        (uint64_t)polys, g.logc, g.logr);
   e = hipGetLastError();
   if (tmp) {
-    const hipError_t ef = hipFreeAsync(tmp, s);
+    const hipError_t ef = mi::scratch_free(tmp, s);
     if (e == hipSuccess) e = ef;
   }
   return e;
@@ -645,7 +652,7 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
   const size_t chunk = chunk_for(g, kp1, lv, batch);
   const size_t dig = ((chunk * lv * kp1) << g.logm), prod = g.logr ? ((chunk * kp1) << g.logm) : 0;
   cplx* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, (dig + prod) * sizeof(cplx), s);
+  hipError_t e = mi::scratch_alloc((void**)&scratch, (dig + prod) * sizeof(cplx), s);
   if (e != hipSuccess) return e;
   cplx* d = scratch;
   cplx* y = g.logr ? scratch + dig : nullptr;
@@ -663,7 +670,7 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
     if (e != hipSuccess) break;
     e = inverse(g, MacSrc{d, gg, g.logm, g.logc, g.logr, kp1, lv}, AccSink{o, g.untw, g.logn}, y, nb * kp1, s);
   }
-  const hipError_t ef = hipFreeAsync(scratch, s);
+  const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;
 }
 
@@ -679,7 +686,7 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
   const size_t dig = ((chunk * lv * kp1) << g.logm), prod = g.logr ? ((chunk * kp1) << g.logm) : 0;
   const size_t acc_u64 = chunk * per;
   cplx* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, (dig + prod) * sizeof(cplx) + (acc_u64 + chunk) * sizeof(uint64_t), s);
+  hipError_t e = mi::scratch_alloc((void**)&scratch, (dig + prod) * sizeof(cplx) + (acc_u64 + chunk) * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
   cplx* d = scratch;
   cplx* y = g.logr ? scratch + dig : nullptr;
@@ -708,7 +715,7 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
                        (const uint64_t*)acc, nb, g.logn, (uint32_t)k);
     e = hipGetLastError();
   }
-  const hipError_t ef = hipFreeAsync(scratch, s);
+  const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;
 }
 

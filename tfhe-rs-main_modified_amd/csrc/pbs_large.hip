@@ -26,6 +26,7 @@
 
 #include <algorithm>
 
+#include "scratch.hpp"
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "pbs_device.hpp"
@@ -238,7 +239,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   const size_t per = (size_t)(k + 1) * sh.n, chunk = chunk_for(sh, batch);
   const size_t ggsw_len = (size_t)level * (k + 1) * per;
   u64 *scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, (chunk * ((size_t)level + 2) * per + chunk) * sizeof(u64), s);
+  hipError_t e = mi::scratch_alloc((void**)&scratch, (chunk * ((size_t)level + 2) * per + chunk) * sizeof(u64), s);
   if (e != hipSuccess) return e;
   u64* digits = scratch;
   u64* y = digits + chunk * level * per;
@@ -291,7 +292,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
                          (const u64*)nullptr, (uint32_t)n_lwe, nb, sh);
     e = hipGetLastError();
   }
-  const hipError_t ef = hipFreeAsync(scratch, s);
+  const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;
 }
 
@@ -318,7 +319,7 @@ hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int le
   const LargeShape sh{(uint32_t)logn, 1u << logn, (uint32_t)k, (uint32_t)level, base_log};
   const size_t per = (size_t)(k + 1) * sh.n, chunk = chunk_for(sh, batch);
   u64* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, chunk * ((size_t)level + 1) * per * sizeof(u64), s);
+  hipError_t e = mi::scratch_alloc((void**)&scratch, chunk * ((size_t)level + 1) * per * sizeof(u64), s);
   if (e != hipSuccess) return e;
   u64* digits = scratch;
   u64* y = digits + chunk * level * per;
@@ -351,7 +352,7 @@ hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int le
       hipLaunchKernelGGL(large_accumulate<false>, dim3(blocks_for(elems)), dim3(256), 0, s, o, y, nb, sh, gi, n_ggsw);
     e = hipGetLastError();
   }
-  const hipError_t ef = hipFreeAsync(scratch, s);
+  const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;
 }
 

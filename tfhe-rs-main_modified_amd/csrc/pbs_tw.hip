@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "scratch.hpp"
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "pbs_tw_body.hpp"
@@ -284,11 +285,11 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
   u64* perm = nullptr;  // MI_EXT_W1P: the caller's GGSWs in the body's W1' order, stream-ordered scratch
   if (MI_EXT_W1P) {
-    hipError_t e = hipMallocAsync((void**)&perm, (size_t)n_ggsw * 4 * pbstw::N * sizeof(u64), s);
+    hipError_t e = mi::scratch_alloc((void**)&perm, (size_t)n_ggsw * 4 * pbstw::N * sizeof(u64), s);
     if (e != hipSuccess) return e;
     e = launch_prepare_tw_key(perm, ggsw, (size_t)n_ggsw * 4, 0, 0, s, true);
     if (e != hipSuccess) {
-      (void)hipFreeAsync(perm, s);
+      (void)mi::scratch_free(perm, s);
       return e;
     }
     ggsw = perm;
@@ -303,7 +304,7 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
   else
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<false>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   const hipError_t e = hipGetLastError();
-  if (perm) (void)hipFreeAsync(perm, s);
+  if (perm) (void)mi::scratch_free(perm, s);
   return e;
 }
 
