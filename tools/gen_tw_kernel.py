@@ -605,18 +605,30 @@ NTT_ADDR = Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, %[l8], s[{S_
 FULL_STRIDE = 66  # row stride (u64) of the one-pass transposes of a wave with a 16.5 KiB LDS buffer (ad.full_t)
 
 
-def t1_full(body, dmap, ad):
+def t1_full(body, dmap, ad, written=False):
     """W0 -> W1 in one pass through a 32 x 66 (u64) LDS tile: lane j writes its 32 rows at i 66 + j (%[tfw] = S + 8 lane,
     row in the offset field), lane 2 i + j0 reads element j = 2 q + j0 of row i into register q (%[tfb] = S + 8 (66 i + j0),
     q in the offset field).  Both sides conflict-free (the reads' 64-bank pattern is 4 i + 2 j0).  For waves that own
     16.5 KiB of LDS (the blind rotation); the 8.5 KiB standalone waves run the two-half t1.  The data stays in the same
     registers (every write has landed before the first read)."""
-    L = [f"ds_write_b64 {ad.tfw}, {pv(dmap[r])} offset:{r * FULL_STRIDE * 8}" for r in range(32)]
+    L = [] if written else t1_full_writes(dmap, ad, range(32))
     L.append("s_waitcnt lgkmcnt(0)")
     L += [f"ds_read_b64 {pv(dmap[q])}, {ad.tfb} offset:{q * 16}" for q in range(32)]
     L.append("s_waitcnt lgkmcnt(0)")
     body.raw(*L)
     return list(dmap)
+
+
+def t1_full_writes(dmap, ad, rows):
+    return [f"ds_write_b64 {ad.tfw}, {pv(dmap[r])} offset:{r * FULL_STRIDE * 8}" for r in rows]
+
+
+# The one-pass transposes of the blind rotation overlap their LDS traffic with the neighbouring multiplies: the forward's
+# T1 writes each twist batch's 8 rows right after they are multiplied, the inverse's W1'' -> W0 writes each half of the
+# lane-pair DIT stage's registers as soon as that half is done, and the untwist's batches wait only for the rows they use.
+# Built at the end of round 3 and emulator-exact (its waits are not emulated: checked by reasoning only), but not yet
+# measured or GPU-tested (the GPU pool had no free slot): off, so the bodies are byte-identical to the measured ones.
+PROGRESSIVE_FULL_T = False
 
 
 def t1(body, dmap, ybase, newhi, ad=NTT_ADDR, row_waits=None):
@@ -877,10 +889,13 @@ def store_raw(dmap):
     return store_rows(dmap, S_GB) + ["s_waitcnt vmcnt(0)"]
 
 
-def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None, first_loaded=False):
+def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None, first_loaded=False, before_batch=None,
+               after_batch=None):
     """x[r] *= table row r (general multiplies) for the 32 registers, in 4 batches of 8 rows; the next
     batch's 8 table rows are loaded into the other buffer before this batch multiplies, so the table
-    latency (L2 or LDS) hides behind the multiplies.  The slots' zero addend halves are set once."""
+    latency (L2 or LDS) hides behind the multiplies.  The slots' zero addend halves are set once.
+    before_batch / after_batch (bt): extra lines before / after batch bt's multiplies (the progressive one-pass
+    transposes: a wait for the rows an LDS read brings, the LDS writes of the rows just multiplied)."""
     B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
     buf = (lambda i, k: bufs[i] + 2 * k) if contiguous else (lambda i, k: regs[16 * i + 2 * k])
     if not first_loaded:
@@ -890,7 +905,11 @@ def twist_rows(B, dmap, ad, bufs, ms, contiguous=True, regs=None, first_loaded=F
             B.raw(*[ad.tw_load(bt + 1, k, buf((bt + 1) % 2, k)) for k in range(8)], ad.tw_wait_n(8))
         else:
             B.raw(ad.tw_wait)
+        if before_batch:
+            B.raw(*before_batch(bt))
         B.mulrows(dmap, list(range(8 * bt, 8 * bt + 8)), [buf(bt % 2, k) for k in range(8)], ms, zero_hi=False)
+        if after_batch:
+            B.raw(*after_batch(bt))
 
 
 def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=0):
@@ -912,10 +931,13 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
         return dmap
     # twist: 4 batches of 8 rows; table rows double-buffered in v8..v23 / v48..v63 (batch bt + 1
     # loads while batch bt multiplies), 2 multiply slots in v24..v47
-    twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)], first_loaded=prefetch)
+    prog = getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T
+    after = (lambda bt: t1_full_writes(dmap, ad, range(8 * bt, 8 * bt + 8))) if prog else None
+    twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)], first_loaded=prefetch,
+               after_batch=after)
     if stop == "twist":
         return dmap
-    dmap = t1(B, dmap, 8, 64, ad)
+    dmap = t1_full(B, dmap, ad, written=True) if prog else t1(B, dmap, 8, 64, ad)
     if stop == "t1":
         return dmap
     pre, busy = None, ()
@@ -1083,16 +1105,26 @@ def t1_w1pp(body, dmap, dst, ad=NTT_ADDR):
     return list(dst)
 
 
-def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR):
+def t_w1pp_w0_full_writes(dmap, ad, regs):
+    return [f"ds_write_b64 {ad.tfb}, {pv(dmap[R])} offset:{(2 * (R >> 1) + 32 * (R & 1)) * 8}" for R in regs]
+
+
+# waits of the untwist batches on the progressive W1'' -> W0 reads (LDS completes in order; lgkmcnt saturates at 15):
+# batch bt multiplies rows 8 bt .. 8 bt + 7
+UNTWIST_ROW_WAITS = ["s_waitcnt lgkmcnt(15)", "s_waitcnt lgkmcnt(15)", "s_waitcnt lgkmcnt(8)", "s_waitcnt lgkmcnt(0)"]
+
+
+def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR, written=False, reads_pending=False):
     """After pair_stage_dit lane 2 i + par holds output n = 2 m + par + 32 q in register 2 m + q: -> W0 through
     LDS, halves split by i (rows (i & 15) 66, columns n + (n >> 5)); reads at %[t1x] + 66 rho.  ad.full_t: one pass
     through the 32 x 66 tile of t1_full (writes at %[tfb] + 2 m + 32 q, reads at %[tfw] + 66 i), the rows landing in
     the registers of dmap."""
     if getattr(ad, "full_t", False):
-        L = [f"ds_write_b64 {ad.tfb}, {pv(dmap[R])} offset:{(2 * (R >> 1) + 32 * (R & 1)) * 8}" for R in range(32)]
+        L = [] if written else t_w1pp_w0_full_writes(dmap, ad, range(32))
         L.append("s_waitcnt lgkmcnt(0)")
         L += [f"ds_read_b64 {pv(dmap[i])}, {ad.tfw} offset:{i * FULL_STRIDE * 8}" for i in range(32)]
-        L.append("s_waitcnt lgkmcnt(0)")
+        if not reads_pending:
+            L.append("s_waitcnt lgkmcnt(0)")
         body.raw(*L)
         return list(dmap)
     L = []
@@ -1115,7 +1147,7 @@ def pair_stage_dit_gmul_ms():
     return [m for m in range(16) if not lane_tmul_applies(inv_last_exp(2 * m), inv_last_exp(2 * m + 1))]
 
 
-def pair_stage_dit(B, dmap, ad, pre, busy):
+def pair_stage_dit(B, dmap, ad, pre, busy, after_half=None):
     """Last DIT stage of the inverse cyclic blocks in W1'': j and j + 32 sit in the two lanes of a pair (register
     r = j & 31).  Regroup registers (2 m, 2 m + 1) across the pair (even lane: elements 2 m, 2 m + 32; odd lane:
     2 m + 1, 2 m + 33), then a CT butterfly whose twiddle exponent differs by 3 between the lanes (tmul_lane), or
@@ -1155,6 +1187,8 @@ def pair_stage_dit(B, dmap, ad, pre, busy):
         for j, op in enumerate(sg.ops):
             op.idx = j
         B.out(sg.schedule())
+        if after_half:
+            B.raw(*after_half(half))
 
 
 def w1p_as_w1pp(dmap):
@@ -1186,9 +1220,11 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
     cf = [True] * 32  # loaded data is canonical
     for s in range(5):
         B.stage("ct", 1 << s, dit_exps_pp(s), dmap, fb, cf, by_reg=True)
-    pair_stage_dit(B, dmap, ad, pre, busy)
+    prog = getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T
+    after = (lambda h: t_w1pp_w0_full_writes(dmap, ad, range(16 * h, 16 * h + 16))) if prog else None
+    pair_stage_dit(B, dmap, ad, pre, busy, after_half=after)
     assert getattr(ad, "full_t", False) or not set(range(ybase, ybase + 32)) & {r for b in dmap for r in (b, b + 1)}
-    return t_w1pp_w0(B, dmap, ybase, newhi, ad)
+    return t_w1pp_w0(B, dmap, ybase, newhi, ad, written=prog, reads_pending=prog)
 
 
 def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False, w1pp_regs=None):
@@ -1228,8 +1264,9 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=Fa
         twist_rows(B, dmap, ad, None, ms, contiguous=False, regs=tregs, first_loaded=True)
     else:
         assert len(regs) >= 56, len(regs)
+        prog = w1pp and getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T  # the W1'' -> W0 reads are still landing
         twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(0, SG0 + 6 * i, regs[32 + 12 * i:44 + 12 * i]) for i in range(2)],
-                   contiguous=False, regs=regs)
+                   contiguous=False, regs=regs, before_batch=(lambda bt: [UNTWIST_ROW_WAITS[bt]]) if prog else None)
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
