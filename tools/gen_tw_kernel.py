@@ -626,8 +626,9 @@ def t1_full_writes(dmap, ad, rows):
 # The one-pass transposes of the blind rotation overlap their LDS traffic with the neighbouring multiplies: the forward's
 # T1 writes each twist batch's 8 rows right after they are multiplied, the inverse's W1'' -> W0 writes each half of the
 # lane-pair DIT stage's registers as soon as that half is done, and the untwist's batches wait only for the rows they use.
-# Built at the end of round 3 and emulator-exact (its waits are not emulated: checked by reasoning only), but not yet
-# measured or GPU-tested (the GPU pool had no free slot): off, so the bodies are byte-identical to the measured ones.
+# Built at the end of round 3 and emulator-exact (its waits are not emulated: checked by reasoning only).  One-box A/B:
+# BNF 35.2 k vs 35.3 k PBS/s (noise of +-1.5 k between repeats), Solinas equal (profiles/r3/pbs_progressive_full_t_ab/):
+# no measurable gain, not GPU-parity-tested, so off and the bodies stay byte-identical to the measured ones.
 PROGRESSIVE_FULL_T = False
 
 
