@@ -70,6 +70,10 @@ def parse():
 
 
 LEG_SECONDS = 0.3  # every non-headline leg times at least this much GPU work (no --steps-scaled legs)
+# order of the legs in the JSON line (not the order they run in): the driver keeps only the tail of stdout, so the
+# config-3 / config-4 legs come last, followed only by the compact legs_summary
+LEG_ORDER = ("pbs_shapes", "pbs_shapes_fft", "keyswitch", "ks_pbs", "ks_pbs_fft", "ext_product_fft", "bsk_conversion",
+             "pbs_fft", "ext_product", "pbs_solinas", "pbs")
 
 
 def timed_leg(run, torch, barrier, dist, dev, min_seconds=LEG_SECONDS, min_steps=2, max_steps=200000):
@@ -396,7 +400,11 @@ def bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist):
                                    f"base_log={base_log} level={level} (shortint {name.upper()} shape), centered "
                                    "modulus switch, synthetic key",
                        "batch_per_gpu": batch, "engine": "shape-generic f64 engine (fft64_generic.hip)"},
-            "cpu_baseline": None}
+            "cpu_baseline": None, "cpu_baseline_note": NO_FFT_BASELINE}
+
+
+NO_FFT_BASELINE = ("no comparable CPU baseline: the reference's f64 path is tfhe-fft (AVX-512 / FMA, Rust), absent here; "
+                   "cpu_numpy_restatement is a single-thread numpy timing, not a baseline")
 
 
 def cpu_baseline_pbs_fft(n, k, n_lwe, base_log, level, seconds: float, threads_note="numpy, 1 thread"):
@@ -449,7 +457,8 @@ def bench_pbs_fft(args, eng, torch, dev, rank, world, barrier, dist):
            "value": world * batch * K / el, "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3,
            "kernel_ms": kernel_ms, "dtype": "f64",
            "config": {"workload": "programmable_bootstrap_lwe_ciphertext (tfhe-fft path), n=918 k=1 N=2048 "
-                                  "base_log=23 level=1, standard modulus switch", "batch_per_gpu": batch}}
+                                  "base_log=23 level=1, standard modulus switch", "batch_per_gpu": batch},
+           "cpu_baseline": None, "cpu_baseline_note": NO_FFT_BASELINE}
     if dist is not None:
         res["sharded"] = bench_pbs_sharded(
             args, eng, torch, dev, rank, world, barrier,
@@ -1043,15 +1052,20 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": load_traffic(),
+            "traffic_source": "constant: PMC FETCH_SIZE + WRITE_SIZE per launch from the committed rocprofv3 passes "
+                              "(profiles/pmc_traffic.json), not measured in this run",
             "algorithmic_bytes_per_launch": bytes_launch,
         },
+        "cpu_baseline": None,
         "cold_start": cold,
         "steady_state": steady,
-        "cpu_baseline": None,
     }
-    out.update(legs)
     if rank == 0 and world == 1:
         out["host_path"] = bench_host_path(eng, torch)
+    # the driver keeps only the tail of stdout: the bulky legs first, configs 3 and 4 (external product, PBS) last
+    for name in LEG_ORDER:
+        if name in legs:
+            out[name] = legs[name]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if not args.no_pbs:
@@ -1063,15 +1077,41 @@ def main():
             for name in ("message_1_carry_1", "message_3_carry_3") if not args.no_shapes else ():
                 # (4_4: ~0.1 s per CMUX step per core, unbounded)
                 out["pbs_shapes"][name]["cpu_baseline"] = cpu_baseline_pbs_shape(name, min(args.cpu_seconds, 4.0))
-            out["pbs_fft"]["cpu_baseline"] = cpu_baseline_pbs_fft(N, 1, PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL,
-                                                                  min(args.cpu_seconds, 3.0))
+            # the f64 legs' CPU figure is a single-thread numpy restatement, not comparable with the reference's
+            # AVX-512 tfhe-fft: reported under its own key, never as `cpu_baseline`
+            out["pbs_fft"]["cpu_numpy_restatement"] = cpu_baseline_pbs_fft(N, 1, PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL,
+                                                                           min(args.cpu_seconds, 3.0))
             for name, (n_, k_, nl_, bl_, lv_, _) in (SHAPE_LEGS.items() if not args.no_shapes else ()):
-                out["pbs_shapes_fft"][name]["cpu_baseline"] = cpu_baseline_pbs_fft(n_, k_, nl_, bl_, lv_,
-                                                                                   min(args.cpu_seconds, 3.0))
+                out["pbs_shapes_fft"][name]["cpu_numpy_restatement"] = cpu_baseline_pbs_fft(
+                    n_, k_, nl_, bl_, lv_, min(args.cpu_seconds, 3.0))
+    out["legs_summary"] = legs_summary(out)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def legs_summary(out):
+    """One compact row per leg (value, unit, roofline frac), the last key of the line."""
+    rows = {}
+
+    def row(d):
+        roof = d.get("roofline") or {}
+        r = {"value": d.get("value"), "unit": d.get("unit"), "frac": roof.get("frac"), "bound": roof.get("bound")}
+        cpu = d.get("cpu_baseline") or {}
+        if cpu.get("value") is not None:
+            r["cpu"] = cpu["value"]
+        return r
+
+    for name in LEG_ORDER:
+        d = out.get(name)
+        if not isinstance(d, dict):
+            continue
+        if "value" in d:
+            rows[name] = row(d)
+        else:
+            rows.update({f"{name}.{k}": row(v) for k, v in d.items() if isinstance(v, dict) and "value" in v})
+    return rows
 
 
 if __name__ == "__main__":

@@ -212,6 +212,45 @@ int mi_pbs_ntt64_key_load(const mi_ntt64_plan *plan, const uint8_t *bytes, size_
 int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
 
+/* The same bootstrap with one LUT per item (the CUDA backend's lut_indexes, backends/tfhe-cuda-backend/cuda/include/
+ * pbs/programmable_bootstrap.h:41; the shortint many-LUT / per-block LUT batches): lut_list holds n_lut GLWEs
+ * ((k+1) N u64 each), item b uses GLWE lut_index[b] (device u32 array of `batch` entries).  An item whose index is
+ * >= n_lut is left untouched (lwe_out[b] not written). */
+int mi_pbs_ntt64_batch_lut_indexed(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in,
+                                   const uint64_t *lut_list, const uint32_t *lut_index, size_t n_lut, size_t batch,
+                                   int ms_mode, void *stream);
+
+/* Batched GLWE-output blind rotation, in place: acc_glwe[b] <- BlindRotate(acc_glwe[b], lwe_in[b]) for b < batch,
+ * every item rotating its own accumulator (one LUT per ciphertext).
+ *   MI_NTT64_BNF     : blind_rotate_ntt64_bnf_assign[_mem_optimized] (ntt64_bnf_pbs.rs:174-266): the CMUX loop over
+ *                      the switched mask, then the division by X^ms(body).  The reference takes a
+ *                      ModulusSwitchedLweCiphertext; here lwe_in is the native LWE switched inside the kernel
+ *                      (MI_MS_STANDARD = lwe_ciphertext_modulus_switch, MI_MS_CENTERED = the centered binary switch,
+ *                      algorithms/modulus_switch.rs) or already switched (MI_MS_PRE_SWITCHED, values in [0, 2N)).
+ *   MI_NTT64_SOLINAS : blind_rotate_ntt64_assign[_mem_optimized] (ntt64_pbs.rs:176-286): the division by
+ *                      X^ms(body) first, then the loop; lwe_in modulo p (MI_MS_STANDARD) or PRE_SWITCHED.
+ * acc_glwe: batch x (k+1) x N u64 on the key's device.  Same shapes as mi_pbs_ntt64_batch. */
+int mi_blind_rotate_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *acc_glwe, const uint64_t *lwe_in, size_t batch,
+                                int ms_mode, void *stream);
+
+/* extract_lwe_sample_from_glwe_ciphertext (algorithms/glwe_sample_extraction.rs:89-160) at
+ * MonomialDegree(nth_first + j * nth_stride) for j < nth_count, over a batch of GLWEs (k+1 polynomials of
+ * polynomial_size u64): lwe_out[b * nth_count + j] (k * polynomial_size + 1 u64).  The many-LUT extraction of a
+ * rotated accumulator is one call (e.g. mockups/tfhe-hpu-mockup/src/lib.rs:736-761: nth_stride = fn_stride,
+ * nth_count = lut_nb).  modulus 0 = native 2^64 (wrapping opposite), else the custom modulus q.  Every degree must be
+ * < polynomial_size (MI_ERR_INVALID_ARG otherwise).  Device pointers on `device`, async on `stream`. */
+int mi_sample_extract_batch(uint64_t *lwe_out, const uint64_t *glwe, size_t polynomial_size, int k, size_t batch,
+                            size_t nth_first, size_t nth_stride, size_t nth_count, uint64_t modulus, int device,
+                            void *stream);
+
+/* ---- Scratch pool (no reference counterpart: the reference's PodStack / ComputationBuffers) -----------------------
+ * Batched entry points that need temporary device memory take it from a per-device pool of blocks kept for reuse,
+ * ordered by events (a block is reissued only behind the last kernel that used it, on any stream; no call blocks the
+ * host).  _trim frees the idle blocks of `device` (-1: every device) once their last users retired; _bytes reports
+ * what the pool holds. */
+int mi_scratch_trim(int device, size_t *released);
+int mi_scratch_bytes(int device, size_t *bytes);
+
 /* ---- Multi-GPU helpers (single process, several devices) ----------------------------------------
  * The analogue of the CUDA backend's helper_multi_gpu (backends/tfhe-cuda-backend/cuda/src/utils/
  * helper_multi_gpu.cu:10-98, helper_multi_gpu.cuh:150-265) for a host that drives several GPUs from one

@@ -236,6 +236,33 @@ inline void programmable_bootstrap_ntt64_lwe_ciphertext(const NttBootstrapKey& k
   check(mi_pbs_ntt64_batch(key.raw(), lwe_out, lwe_in, lut, batch, ms_mode, stream));
 }
 
+// the same with one LUT per item: item b uses GLWE lut_index[b] (device u32) of the n_lut in lut_list
+inline void programmable_bootstrap_ntt64_lwe_ciphertext_lut_indexed(const NttBootstrapKey& key, const uint64_t* lwe_in,
+                                                                    uint64_t* lwe_out, const uint64_t* lut_list,
+                                                                    const uint32_t* lut_index, size_t n_lut,
+                                                                    size_t batch, int ms_mode = MI_MS_STANDARD,
+                                                                    void* stream = nullptr) {
+  check(mi_pbs_ntt64_batch_lut_indexed(key.raw(), lwe_out, lwe_in, lut_list, lut_index, n_lut, batch, ms_mode,
+                                       stream));
+}
+
+// blind_rotate_ntt64[_bnf]_assign (ntt64_pbs.rs:176-286 / ntt64_bnf_pbs.rs:174-266), batched and in place: every item
+// rotates its own accumulator acc_glwe[b] ((k+1) N u64) by lwe_in[b]
+inline void blind_rotate_ntt64_assign(const NttBootstrapKey& key, const uint64_t* lwe_in, uint64_t* acc_glwe,
+                                      size_t batch, int ms_mode = MI_MS_STANDARD, void* stream = nullptr) {
+  check(mi_blind_rotate_ntt64_batch(key.raw(), acc_glwe, lwe_in, batch, ms_mode, stream));
+}
+
+// extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160) at MonomialDegree(nth + j nth_stride),
+// j < nth_count, of every GLWE in a batch; modulus 0 = native
+inline void extract_lwe_sample_from_glwe_ciphertext(const uint64_t* glwe, uint64_t* lwe_out, size_t polynomial_size,
+                                                    int glwe_dimension, size_t batch, size_t nth, size_t nth_stride = 0,
+                                                    size_t nth_count = 1, uint64_t modulus = 0, int device = 0,
+                                                    void* stream = nullptr) {
+  check(mi_sample_extract_batch(lwe_out, glwe, polynomial_size, glwe_dimension, batch, nth, nth_stride, nth_count,
+                                modulus, device, stream));
+}
+
 // entities/lwe_keyswitch_key.rs + algorithms/lwe_keyswitch.rs:103-227 (native modulus); move-only
 class LweKeyswitchKey {
  public:

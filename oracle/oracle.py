@@ -226,6 +226,13 @@ _PBS_SIGS["ora_pbs_set_fast_ntt"] = (None, [ctypes.c_int])
 _PBS_SIGS["ora_pbs_solinas_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _p64, _sz, _sz,
                                          ctypes.c_int])
 _PBS_SIGS["ora_ext_product_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz, ctypes.c_int])
+_PBS_SIGS["ora_blind_rotate_solinas"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz,
+                                              ctypes.c_int])
+_PBS_SIGS["ora_sample_extract_nth"] = (None, [_p64, _p64, _sz, ctypes.c_int, _sz, _u64])
+_PBS_SIGS["ora_blind_rotate_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64, _sz,
+                                                _sz, ctypes.c_int, ctypes.c_int])
+_PBS_SIGS["ora_blind_rotate_solinas_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64,
+                                                    _sz, _sz, ctypes.c_int, ctypes.c_int])
 _pbs_ready = False
 
 
@@ -282,6 +289,28 @@ class NttContext:
         m = _u(msed_mask)
         _plib().ora_blind_rotate_bnf(self.tables, k, base_log, level, _ptr(acc), _ptr(m), int(msed_body),
                                      _ptr(_u(bsk)), m.size)
+        return acc
+
+    def blind_rotate_solinas(self, acc, lwe_in, bsk, k, base_log, level, pre_switched=False):
+        acc = _u(acc).copy()
+        lwe_in = _u(lwe_in)
+        _plib().ora_blind_rotate_solinas(self.tables, k, base_log, level, _ptr(acc), _ptr(lwe_in), _ptr(_u(bsk)),
+                                         lwe_in.size - 1, int(pre_switched))
+        return acc
+
+    def blind_rotate_batch(self, acc, lwe_in, bsk, k, base_log, level, bnf=True, ms_mode=0, threads=8):
+        """acc (batch, k+1, N) rotated item by item (a new array); BNF ms_mode 0 standard / 1 centered / 2 pre-switched,
+        Solinas 0 (raw mod p) or 2 (pre-switched)."""
+        acc = _u(acc).copy()
+        lwe_in = _u(lwe_in)
+        batch, n_lwe = lwe_in.shape[0], lwe_in.shape[1] - 1
+        if bnf:
+            _plib().ora_blind_rotate_bnf_batch(self.tables, k, base_log, level, _ptr(acc), _ptr(lwe_in), _ptr(_u(bsk)),
+                                               n_lwe, batch, int(ms_mode), threads)
+        else:
+            assert ms_mode in (0, 2)
+            _plib().ora_blind_rotate_solinas_batch(self.tables, k, base_log, level, _ptr(acc), _ptr(lwe_in),
+                                                   _ptr(_u(bsk)), n_lwe, batch, int(ms_mode == 2), threads)
         return acc
 
     def pbs(self, lwe_in, lut, bsk, k, base_log, level, bnf=True, centered=False):
@@ -372,6 +401,12 @@ def poly_monomial_div(poly, degree, q=0):
 def sample_extract(glwe, n, k, q=0):
     out = np.zeros(k * n + 1, np.uint64)
     _plib().ora_sample_extract(_ptr(_u(glwe)), _ptr(out), n, k, q)
+    return out
+
+
+def sample_extract_nth(glwe, n, k, nth, q=0):
+    out = np.zeros(k * n + 1, np.uint64)
+    _plib().ora_sample_extract_nth(_ptr(_u(glwe)), _ptr(out), n, k, nth, q)
     return out
 
 

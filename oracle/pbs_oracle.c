@@ -277,24 +277,88 @@ void ora_pbs_bnf_ms(const ora_ntt_tables *t, int k, int base_log, int level, uin
     free(acc); free(ms);
 }
 
-void ora_pbs_solinas(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
-                     const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe) {
+/* blind_rotate_ntt64_assign_mem_optimized (ntt64_pbs.rs:213-286): acc (the LUT, modulo p) is divided by X^ms(body)
+ * first, then the CMUX loop over the mask.  pre_switched: lwe_in holds the switched values in [0, 2N) (a value of 0
+ * skips the step like a raw 0 does: X^0 and X^2N leave ct1 - ct0 = 0). */
+void ora_blind_rotate_solinas(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                              const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, int pre_switched) {
     const size_t n = t->n, gs = (size_t)k + 1, ggsw_len = (size_t)level * gs * gs * n;
     const uint64_t q = t->p;
-    uint64_t *acc = (uint64_t *)malloc(gs * n * sizeof(uint64_t));
     uint64_t *ct1 = (uint64_t *)malloc(gs * n * sizeof(uint64_t));
-    memcpy(acc, lut, gs * n * sizeof(uint64_t));
-    const size_t deg_b = (size_t)ora_pbs_modulus_switch_non_native(lwe_in[n_lwe], n, q);
+    const size_t deg_b = pre_switched ? (size_t)lwe_in[n_lwe]
+                                      : (size_t)ora_pbs_modulus_switch_non_native(lwe_in[n_lwe], n, q);
     for (size_t c = 0; c < gs; ++c) ora_poly_monomial_div(acc + c * n, n, deg_b, q);
     for (size_t i = 0; i < n_lwe; ++i) {
         if (lwe_in[i] == 0) continue; /* ntt64_pbs.rs:257 */
         memcpy(ct1, acc, gs * n * sizeof(uint64_t));
-        const size_t deg = (size_t)ora_pbs_modulus_switch_non_native(lwe_in[i], n, q);
+        const size_t deg = pre_switched ? (size_t)lwe_in[i]
+                                        : (size_t)ora_pbs_modulus_switch_non_native(lwe_in[i], n, q);
         for (size_t c = 0; c < gs; ++c) ora_poly_monomial_mul(ct1 + c * n, n, deg, q);
         ora_cmux_solinas(t, k, base_log, level, acc, ct1, bsk + i * ggsw_len);
     }
-    ora_sample_extract(acc, lwe_out, n, k, q);
-    free(acc); free(ct1);
+    free(ct1);
+}
+
+void ora_pbs_solinas(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *lwe_out,
+                     const uint64_t *lwe_in, const uint64_t *lut, const uint64_t *bsk, size_t n_lwe) {
+    const size_t n = t->n, gs = (size_t)k + 1;
+    uint64_t *acc = (uint64_t *)malloc(gs * n * sizeof(uint64_t));
+    memcpy(acc, lut, gs * n * sizeof(uint64_t));
+    ora_blind_rotate_solinas(t, k, base_log, level, acc, lwe_in, bsk, n_lwe, 0);
+    ora_sample_extract(acc, lwe_out, n, k, t->p);
+    free(acc);
+}
+
+/* extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160) at MonomialDegree(nth), restated step by
+ * step: body = B[nth]; each mask polynomial copied, reversed, its first N - nth - 1 entries negated (wrapping, or
+ * modulo q), then rotated left by that count. */
+void ora_sample_extract_nth(const uint64_t *glwe, uint64_t *lwe_out, size_t n, int k, size_t nth, uint64_t q) {
+    const size_t opposite = n - nth - 1;
+    uint64_t *tmp = (uint64_t *)malloc(n * sizeof(uint64_t));
+    lwe_out[(size_t)k * n] = glwe[(size_t)k * n + nth];
+    for (int c = 0; c < k; ++c) {
+        uint64_t *m = lwe_out + (size_t)c * n;
+        for (size_t j = 0; j < n; ++j) m[j] = glwe[(size_t)c * n + (n - 1 - j)]; /* copy + reverse */
+        for (size_t j = 0; j < opposite; ++j) m[j] = neg_q(m[j], q);
+        for (size_t j = 0; j < n; ++j) tmp[j] = m[(j + opposite) % n];          /* rotate_left(opposite) */
+        memcpy(m, tmp, n * sizeof(uint64_t));
+    }
+    free(tmp);
+}
+
+/* the batched GLWE-output blind rotations (one accumulator per item, in place), one item per thread.
+ * BNF ms_mode: 0 standard switch of the native LWE, 1 centered (body corrected), 2 pre-switched values. */
+void ora_blind_rotate_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                                const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, size_t batch, int ms_mode,
+                                int threads) {
+    const size_t glwe = ((size_t)k + 1) * t->n, in_len = n_lwe + 1;
+    const unsigned log_mod = (unsigned)__builtin_ctzll(t->n) + 1u;
+    long long b;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
+    for (b = 0; b < (long long)batch; ++b) {
+        const uint64_t *in = lwe_in + (size_t)b * in_len;
+        uint64_t *ms = (uint64_t *)malloc(in_len * sizeof(uint64_t));
+        for (size_t i = 0; i < n_lwe; ++i) ms[i] = ms_mode == 2 ? in[i] : ora_modulus_switch(in[i], log_mod);
+        uint64_t body;
+        if (ms_mode == 2) body = in[n_lwe];
+        else {
+            const uint64_t corr = ms_mode == 1 ? ora_centered_ms_body_correction(in, n_lwe, log_mod) : 0;
+            body = ora_modulus_switch(in[n_lwe] + corr, log_mod);
+        }
+        ora_blind_rotate_bnf(t, k, base_log, level, acc + (size_t)b * glwe, ms, body, bsk, n_lwe);
+        free(ms);
+    }
+}
+
+void ora_blind_rotate_solinas_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                                    const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, size_t batch,
+                                    int pre_switched, int threads) {
+    const size_t glwe = ((size_t)k + 1) * t->n;
+    long long b;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : 1)
+    for (b = 0; b < (long long)batch; ++b)
+        ora_blind_rotate_solinas(t, k, base_log, level, acc + (size_t)b * glwe, lwe_in + (size_t)b * (n_lwe + 1), bsk,
+                                 n_lwe, pre_switched);
 }
 
 void ora_bsk_to_ntt(const ora_ntt_tables *t, const uint64_t *bsk_std, uint64_t *bsk_ntt, size_t n_polys,

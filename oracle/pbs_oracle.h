@@ -104,6 +104,19 @@ void ora_pbs_solinas_batch(const ora_ntt_tables *t, int k, int base_log, int lev
 void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
                                const uint64_t *ggsw, const uint64_t *glwe, size_t batch, int threads);
 
+/* ntt64_pbs.rs:213-286 blind_rotate_ntt64_assign_mem_optimized (acc in place; pre_switched: values in [0, 2N)) */
+void ora_blind_rotate_solinas(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                              const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, int pre_switched);
+/* glwe_sample_extraction.rs:89-160 at MonomialDegree(nth) (q = 0: native wrapping negation) */
+void ora_sample_extract_nth(const uint64_t *glwe, uint64_t *lwe_out, size_t n, int k, size_t nth, uint64_t q);
+/* batched in-place blind rotations, one accumulator per item (BNF ms_mode: 0 standard, 1 centered, 2 pre-switched) */
+void ora_blind_rotate_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                                const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, size_t batch, int ms_mode,
+                                int threads);
+void ora_blind_rotate_solinas_batch(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *acc,
+                                    const uint64_t *lwe_in, const uint64_t *bsk, size_t n_lwe, size_t batch,
+                                    int pre_switched, int threads);
+
 #ifdef __cplusplus
 }
 #endif

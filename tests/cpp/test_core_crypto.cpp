@@ -135,8 +135,49 @@ int main() {
     EXPECT(threw);
   }
 
+  // GLWE-output blind rotation (BNF, in place, one accumulator per item) + many-sample extraction == the oracle's
+  // blind_rotate_ntt64_bnf_assign + extract_lwe_sample_from_glwe_ciphertext at 0 and N/2; LUT-indexed PBS
+  {
+    const size_t batch = 3;
+    const auto acc = uniform(120, 0, batch * 2 * N), lwe = uniform(121, 0, batch * (n_lwe + 1));
+    std::vector<uint64_t> want_acc(acc), want_lwe(batch * 2 * (N + 1));
+    const unsigned log_mod = 12;
+    for (size_t b = 0; b < batch; ++b) {
+      std::vector<uint64_t> ms(n_lwe);
+      for (size_t i = 0; i < n_lwe; ++i) ms[i] = ora_modulus_switch(lwe[b * (n_lwe + 1) + i], log_mod);
+      ora_blind_rotate_bnf(&tabs, 1, 23, 1, want_acc.data() + b * 2 * N, ms.data(),
+                           ora_modulus_switch(lwe[b * (n_lwe + 1) + n_lwe], log_mod), bsk_ref.data(), n_lwe);
+      for (size_t j = 0; j < 2; ++j)
+        ora_sample_extract_nth(want_acc.data() + b * 2 * N, want_lwe.data() + (b * 2 + j) * (N + 1), N, 1, j * (N / 2), 0);
+    }
+    cc::NttBootstrapKey key(*plan, d_ntt.p, n_lwe, 23, 1, MI_NTT64_BNF);
+    Dev d_acc(acc), d_lwe(lwe), d_out(batch * 2 * (N + 1));
+    cc::blind_rotate_ntt64_assign(key, d_lwe.p, d_acc.p, batch);
+    EXPECT(d_acc.host() == want_acc);
+    cc::extract_lwe_sample_from_glwe_ciphertext(d_acc.p, d_out.p, N, 1, batch, 0, N / 2, 2);
+    EXPECT(d_out.host() == want_lwe);
+    // item b through LUT idx[b]: the rotated accumulators' first rows double as three LUTs
+    const std::vector<uint64_t> luts = uniform(122, 0, 3 * 2 * N);
+    const uint32_t idx_h[3] = {2, 0, 2};
+    uint32_t* idx = nullptr;
+    EXPECT(hipMalloc(reinterpret_cast<void**>(&idx), sizeof idx_h) == hipSuccess);
+    EXPECT(hipMemcpy(idx, idx_h, sizeof idx_h, hipMemcpyHostToDevice) == hipSuccess);
+    std::vector<uint64_t> want(batch * (N + 1));
+    for (size_t b = 0; b < batch; ++b)
+      ora_pbs_bnf(&tabs, 1, 23, 1, want.data() + b * (N + 1), lwe.data() + b * (n_lwe + 1),
+                  luts.data() + idx_h[b] * 2 * N, bsk_ref.data(), n_lwe);
+    Dev d_luts(luts), d_pbs(batch * (N + 1));
+    cc::programmable_bootstrap_ntt64_lwe_ciphertext_lut_indexed(key, d_lwe.p, d_pbs.p, d_luts.p, idx, 3, batch);
+    EXPECT(d_pbs.host() == want);
+    (void)hipFree(idx);
+  }
+
   // f64 FFT: round trip and an external product (k = 1, level 1, base 2^23) vs the exact product in Z_2^64[X]/(X^N+1),
-  // at N = 2048 (the one-wave engine) and at 1024 / 8192 (the shape-generic engine)
+  // at N = 2048 (the one-wave engine) and at 1024 / 8192 (the shape-generic engine), each on the legacy null stream and
+  // on a created non-blocking stream (the r3 stale-scratch sequence: in-place reorder, N = 8192 external product)
+  hipStream_t own = nullptr;
+  EXPECT(hipStreamCreateWithFlags(&own, hipStreamNonBlocking) == hipSuccess);
+  for (hipStream_t st : {(hipStream_t) nullptr, own})
   for (const size_t NF : {(size_t)2048, (size_t)1024, (size_t)8192}) {
     tfhe_ntt_amd::fft64::Fft fft(NF);
     const size_t batch = 2;
@@ -144,26 +185,28 @@ int main() {
     Dev d_x(x), d_back(batch * NF);
     double* four = nullptr;
     EXPECT(hipMalloc(reinterpret_cast<void**>(&four), batch * NF * 8) == hipSuccess);
-    fft.forward_as_torus(four, d_x.p, batch);
+    fft.forward_as_torus(four, d_x.p, batch, st);
+    EXPECT(hipStreamSynchronize(st) == hipSuccess);
     {  // serialised (natural) order and back: an exact permutation, out of place then in place
       double* nat = nullptr;
       EXPECT(hipMalloc(reinterpret_cast<void**>(&nat), batch * NF * 8) == hipSuccess);
       std::vector<double> h0(batch * NF), h1(batch * NF);
       EXPECT(hipMemcpy(h0.data(), four, batch * NF * 8, hipMemcpyDeviceToHost) == hipSuccess);
-      fft.to_standard_order(nat, four, batch);
-      fft.from_standard_order(nat, nat, batch);
+      fft.to_standard_order(nat, four, batch, st);
+      fft.from_standard_order(nat, nat, batch, st);
+      EXPECT(hipStreamSynchronize(st) == hipSuccess);
       EXPECT(hipMemcpy(h1.data(), nat, batch * NF * 8, hipMemcpyDeviceToHost) == hipSuccess);
       if (h0 != h1) {
         size_t bad = 0, first = 0;
         for (size_t i = 0; i < h0.size(); ++i)
           if (h0[i] != h1[i] && bad++ == 0) first = i;
-        std::fprintf(stderr, "f64 standard-order round trip N = %zu: %zu of %zu doubles differ, first at %zu\n", NF, bad,
-                     h0.size(), first);
+        std::fprintf(stderr, "f64 standard-order round trip N = %zu (%s stream): %zu of %zu doubles differ, first at %zu\n",
+                     NF, st ? "created" : "null", bad, h0.size(), first);
       }
       EXPECT(h0 == h1);
       (void)hipFree(nat);
     }
-    fft.backward_as_torus(d_back.p, four, batch);
+    fft.backward_as_torus(d_back.p, four, batch, false, st);
     const auto back = d_back.host();
     int64_t worst = 0;
     for (size_t i = 0; i < x.size(); ++i) {
@@ -178,8 +221,8 @@ int main() {
     double* fg = nullptr;
     EXPECT(hipMalloc(reinterpret_cast<void**>(&fg), 4 * NF * 8) == hipSuccess);
     Dev d_g(ggsw), d_in(glwe), d_out(out0);
-    tfhe_ntt_amd::fft64::convert_standard_lwe_bootstrap_key_to_fourier(fft, d_g.p, fg, 4);
-    tfhe_ntt_amd::fft64::add_external_product_assign(fft, d_out.p, d_in.p, fg, bl, 1, 1);
+    tfhe_ntt_amd::fft64::convert_standard_lwe_bootstrap_key_to_fourier(fft, d_g.p, fg, 4, st);
+    tfhe_ntt_amd::fft64::add_external_product_assign(fft, d_out.p, d_in.p, fg, bl, 1, 1, st);
     const auto got = d_out.host();
     // exact: decomposition digit (decomposer.rs, level 1) of each GLWE coefficient, negacyclic products mod 2^64
     std::vector<int64_t> dig(2 * NF);
@@ -210,7 +253,8 @@ int main() {
         worst = std::max(worst, d < 0 ? -d : d);
       }
     if (worst >= (int64_t(1) << (NF > 2048 ? 50 : 48)))
-      std::fprintf(stderr, "f64 external product N = %zu: worst |error| 2^%.2f\n", NF, std::log2((double)worst));
+      std::fprintf(stderr, "f64 external product N = %zu (%s stream): worst |error| 2^%.2f\n", NF, st ? "created" : "null",
+                   std::log2((double)worst));
     EXPECT(worst < (int64_t(1) << (NF > 2048 ? 50 : 48)));  // the f64 bound grows with sqrt(N log N)
     {  // the reference's FourierLweBootstrapKey bytes: write, load (a key owning its copy), write again: same bytes
       tfhe_ntt_amd::fft64::FourierBootstrapKey key(fft, fg, 1, bl, 1);
@@ -232,6 +276,7 @@ int main() {
     (void)hipFree(fg);
   }
 
+  EXPECT(hipStreamDestroy(own) == hipSuccess);
   if (g_failures) {
     std::fprintf(stderr, "%d expectation(s) failed\n", g_failures);
     return 1;

@@ -106,3 +106,44 @@ def test_pbs_functional(oracle, bnf):
         out = ctx.pbs(ct, lut, nbsk, k, base_log, level, bnf=bnf)
         got = H.decode(H.lwe_decrypt(out, out_sk, q), delta, msg_mod, q)
         assert got == f(m), (m, got)
+
+
+@pytest.mark.parametrize("q", [0, SOLINAS_P])
+def test_sample_extract_nth_decrypts(oracle, q):
+    """extract_lwe_sample_from_glwe_ciphertext's defining property (glwe_sample_extraction.rs:26-88 doc test): the
+    LWE extracted at MonomialDegree(nth) decrypts, under the flattened GLWE key, to coefficient nth of the GLWE's
+    plaintext — for every nth, native and custom modulus; nth = 0 equals the nth-0 restatement."""
+    n, k = 32, 2
+    g = H.rng(41 + (q != 0))
+    glwe_sk = H.binary_key(g, (k, n))
+    msg = H.uniform_u64(g, n) if not q else g.integers(0, q, n, dtype=np.uint64)
+    ct = H.glwe_encrypt(g, msg, glwe_sk, 0, q)
+    phase = H.glwe_decrypt(ct, glwe_sk, q)  # msg + the (tiny) noise: extraction keeps the phase exactly
+    lwe_sk = H.glwe_sk_as_lwe_sk(glwe_sk)
+    for nth in range(n):
+        lwe = oracle.sample_extract_nth(ct.reshape(-1), n, k, nth, q)
+        assert int(H.lwe_decrypt(lwe, lwe_sk, q)) == int(phase[nth]), nth
+    assert np.array_equal(oracle.sample_extract_nth(ct.reshape(-1), n, k, 0, q),
+                          oracle.sample_extract(ct.reshape(-1), n, k, q))
+
+
+@pytest.mark.parametrize("bnf,ms", [(True, 0), (True, 1), (False, 0)])
+def test_blind_rotate_then_extract_is_pbs(oracle, bnf, ms):
+    """blind_rotate_ntt64[_bnf]_assign + extraction at 0 == the PBS restatement (ntt64_bnf_pbs.rs:469-540 calls exactly
+    these two; ntt64_pbs.rs:482-538 likewise), on the batched oracle entry points the GPU tests compare against."""
+    n, k, n_lwe, base_log, level = 1024, 1, 12, 15, 2
+    q = 0 if bnf else SOLINAS_P
+    g = H.rng(90 + 2 * bnf + ms)
+    ctx = oracle.NttContext(n)
+    bsk = g.integers(0, SOLINAS_P, size=(n_lwe, level, k + 1, k + 1, n), dtype=np.uint64)
+    lut = H.uniform_u64(g, (k + 1, n)) if not q else g.integers(0, q, (k + 1, n), dtype=np.uint64)
+    lwe = H.uniform_u64(g, (4, n_lwe + 1)) if not q else g.integers(0, q, (4, n_lwe + 1), dtype=np.uint64)
+    accs = np.broadcast_to(lut, (4, k + 1, n)).copy()
+    rot = ctx.blind_rotate_batch(accs, lwe, bsk.reshape(-1), k, base_log, level, bnf=bnf, ms_mode=ms)
+    for b in range(4):
+        want = ctx.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), k, base_log, level, bnf=bnf, centered=ms == 1)
+        assert np.array_equal(oracle.sample_extract_nth(rot[b].reshape(-1), n, k, 0, q), want)
+    # pre-switched input == the standard switch done by the caller
+    if bnf and ms == 0:
+        msed = np.vectorize(lambda x: oracle.modulus_switch(int(x), 11), otypes=[np.uint64])(lwe)
+        assert np.array_equal(ctx.blind_rotate_batch(accs, msed, bsk.reshape(-1), k, base_log, level, ms_mode=2), rot)

@@ -59,7 +59,7 @@ const char* mi_last_error_message(void) { return last_error().c_str(); }
 
 const char* mi_build_source_hash(void) { return MI_SOURCE_HASH; }
 
-int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_plan) {
+static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_plan) {
   if (!out_plan) return fail(MI_ERR_INVALID_ARG, "out_plan is NULL");
   *out_plan = nullptr;
   // prime64.rs:769-775 — same order of checks as the reference
@@ -72,7 +72,7 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   // reference's Solinas root exists up to 2N = 2^32 (roots.rs:96-107), other primes need 2N | p - 1 (checked above)
   if (logn > 31) return fail(MI_ERR_UNSUPPORTED, "this build runs N <= 2^31 on device");
 
-  mi_ntt64_plan* plan = new (std::nothrow) mi_ntt64_plan;
+  std::unique_ptr<mi_ntt64_plan> plan(new (std::nothrow) mi_ntt64_plan);
   if (!plan) return fail(MI_ERR_OOM, "host allocation failed");
   plan->n = n;
   plan->logn = logn;
@@ -85,7 +85,7 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   u64 w;
   if (plan->goldilocks) {
     auto r = mi::host::solinas_root(n);
-    if (!r) { delete plan; return fail(MI_ERR_NO_ROOT, "no Solinas root for this size"); }
+    if (!r) { return fail(MI_ERR_NO_ROOT, "no Solinas root for this size"); }
     w = *r;
   } else {
     w = *root;
@@ -123,11 +123,10 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   }
 
   DeviceGuard g(device);
-  if (!g.ok) { delete plan; return fail(MI_ERR_HIP, "hipSetDevice failed"); }
+  if (!g.ok) { return fail(MI_ERR_HIP, "hipSetDevice failed"); }
   if (hipMalloc(&plan->d_twid, n * sizeof(u64)) != hipSuccess ||
       hipMalloc(&plan->d_inv_twid, n * sizeof(u64)) != hipSuccess) {
     if (plan->d_twid) (void)hipFree(plan->d_twid);
-    delete plan;
     return fail(MI_ERR_OOM, "twiddle allocation failed");
   }
   hipError_t e = hipMemcpy(plan->d_twid, dev_tw.data(), n * sizeof(u64), hipMemcpyHostToDevice);
@@ -135,7 +134,6 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
   if (e != hipSuccess) {
     (void)hipFree(plan->d_twid);
     (void)hipFree(plan->d_inv_twid);
-    delete plan;
     return hip_fail(e, "twiddle upload");
   }
   if (plan->goldilocks && n == 2048) {
@@ -194,14 +192,25 @@ int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_p
         plan->d_twist_f = plan->d_twist_i = nullptr;
         (void)hipFree(plan->d_twid);
         (void)hipFree(plan->d_inv_twid);
-        delete plan;
-        return fail(MI_ERR_OOM, "twist table allocation failed");
+            return fail(MI_ERR_OOM, "twist table allocation failed");
       }
     }
   }
   plan->twisted = plan->d_twist_f != nullptr;
-  *out_plan = plan;
+  *out_plan = plan.release();
   return MI_OK;
+}
+
+// the host tables (2 x N u64 plus their device-form copies: ~64 GiB at N = 2^31) are std::vectors: an allocation
+// failure is returned as MI_ERR_OOM instead of unwinding through the C ABI (plan_create holds the plan in a
+// unique_ptr, and every device allocation comes after the large host tables)
+int mi_ntt64_plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_plan) {
+  try {
+    return plan_create(n, p, device, out_plan);
+  } catch (const std::bad_alloc&) {
+    if (out_plan) *out_plan = nullptr;
+    return fail(MI_ERR_OOM, "host allocation of the twiddle tables failed");
+  }
 }
 
 int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
@@ -644,15 +653,19 @@ int mi_pbs_ntt64_key_destroy(mi_pbs_ntt64_key* key) {
   return MI_OK;
 }
 
-int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
-                       size_t batch, int ms_mode, void* stream) {
+}  // extern "C"
+
+// every NTT bootstrap entry point: the accumulator's start and the output form come in `io` (ntt64_launch.hpp PbsIo);
+// lwe_out is ignored when io.glwe_out is set
+static int pbs_common(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, mi::PbsIo io,
+                      size_t batch, int ms_mode, void* stream) {
   if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
   if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED && ms_mode != MI_MS_PRE_SWITCHED)
     return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
   if (ms_mode == MI_MS_CENTERED && key->variant != MI_NTT64_BNF)
     return fail(MI_ERR_INVALID_ARG, "centered modulus switch applies to native-modulus (BNF) inputs");
   if (batch == 0) return MI_OK;
-  if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if ((!lwe_out && !io.glwe_out) || !lwe_in || !io.lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   const mi_ntt64_plan* plan = key->plan;
   const hipStream_t s = (hipStream_t)stream;
@@ -671,7 +684,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
         return hip_fail(e, "modulus switch launch");
       }
     }
-    hipError_t e = mi::launch_pbs_tw_sol(lwe_out, sw ? sw : lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log,
+    hipError_t e = mi::launch_pbs_tw_sol(lwe_out, sw ? sw : lwe_in, io, key->bsk, key->n_lwe, batch, key->base_log,
                                          plan->d_twist_f, s);
     if (sw) (void)mi::scratch_free(sw, s);
     return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
@@ -691,17 +704,79 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
   }
   hipError_t e;
   if (twisted_ext_applies(plan, key->variant, key->k, key->base_log, key->level))
-    e = mi::launch_pbs_tw(lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
+    e = mi::launch_pbs_tw(lwe_out, lwe_in, io, key->bsk, key->n_lwe, batch, key->base_log, plan->d_twist_f,
                           ms_mode == MI_MS_CENTERED, s);
   else if (plan->logn >= LARGE_PATH_MIN_LOGN)
-    e = mi::launch_pbs_large(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut,
+    e = mi::launch_pbs_large(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, io,
                              key->bsk, key->n_lwe, batch, key->base_log, plan->d_twid, plan->d_inv_twid,
                              ms_mode == MI_MS_CENTERED, s);
   else
-    e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, lut, key->bsk, key->n_lwe, batch,
+    e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, io, key->bsk, key->n_lwe, batch,
                        key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);
   if (lifted) (void)mi::scratch_free(lifted, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "pbs launch");
+}
+
+extern "C" {
+
+int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
+                       size_t batch, int ms_mode, void* stream) {
+  mi::PbsIo io;
+  io.lut = lut;
+  if (!lwe_out && batch) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  return pbs_common(key, lwe_out, lwe_in, io, batch, ms_mode, stream);
+}
+
+int mi_pbs_ntt64_batch_lut_indexed(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in,
+                                   const uint64_t* lut_list, const uint32_t* lut_index, size_t n_lut, size_t batch,
+                                   int ms_mode, void* stream) {
+  if (batch && (!lut_index || !lwe_out)) return fail(MI_ERR_INVALID_ARG, "lut_index / lwe_out is NULL");
+  if (n_lut == 0 || n_lut > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "n_lut out of range");
+  mi::PbsIo io;
+  io.lut = lut_list;
+  io.lut_idx = lut_index;
+  io.n_lut = (uint32_t)n_lut;
+  return pbs_common(key, lwe_out, lwe_in, io, batch, ms_mode, stream);
+}
+
+int mi_blind_rotate_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* acc_glwe, const uint64_t* lwe_in, size_t batch,
+                                int ms_mode, void* stream) {
+  if (batch && !acc_glwe) return fail(MI_ERR_INVALID_ARG, "acc_glwe is NULL");
+  mi::PbsIo io;
+  io.lut = acc_glwe;
+  io.per_item = 1;
+  io.glwe_out = acc_glwe;
+  return pbs_common(key, nullptr, lwe_in, io, batch, ms_mode, stream);
+}
+
+int mi_sample_extract_batch(uint64_t* lwe_out, const uint64_t* glwe, size_t polynomial_size, int k, size_t batch,
+                            size_t nth_first, size_t nth_stride, size_t nth_count, uint64_t modulus, int device,
+                            void* stream) {
+  if (polynomial_size < 2 || (polynomial_size & (polynomial_size - 1)) != 0 || polynomial_size > ((size_t)1 << 31))
+    return fail(MI_ERR_INVALID_ARG, "polynomial size must be a power of two in [2, 2^31]");
+  if (k < 1) return fail(MI_ERR_INVALID_ARG, "GLWE dimension must be >= 1");
+  if (batch == 0 || nth_count == 0) return MI_OK;
+  if (!lwe_out || !glwe) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  // glwe_sample_extraction.rs:89-160 takes MonomialDegree < N (opposite_count = N - nth - 1 would underflow)
+  if (nth_first >= polynomial_size || (nth_count > 1 && nth_stride > (polynomial_size - 1 - nth_first) / (nth_count - 1)))
+    return fail(MI_ERR_INVALID_ARG, "a monomial degree is >= the polynomial size");
+  DeviceGuard g(device);
+  if (!g.ok) return fail(MI_ERR_HIP, "hipSetDevice failed");
+  const hipError_t e = mi::launch_sample_extract(lwe_out, glwe, __builtin_ctzll(polynomial_size), k, batch, nth_first,
+                                                 nth_stride, nth_count, modulus, (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "sample extraction launch");
+}
+
+int mi_scratch_trim(int device, size_t* released) {
+  const size_t b = mi::scratch_trim(device);
+  if (released) *released = b;
+  return MI_OK;
+}
+
+int mi_scratch_bytes(int device, size_t* bytes) {
+  if (!bytes) return fail(MI_ERR_INVALID_ARG, "bytes is NULL");
+  *bytes = mi::scratch_bytes(device);
+  return MI_OK;
 }
 
 // ---- prime32 plans (prime32.rs:632-1025) -------------------------------------------------------

@@ -318,12 +318,13 @@ int multi_gpu_pbs(mi_multi_gpu* m, const Key* const* keys, uint64_t* lwe_out, co
       DeviceGuard g(m->devices[i]);
       (void)mi::scratch_free(scratch[i], m->streams[i]);
     }
-  // the producer streams follow the last use of their key / LUT (shard 0's is `stream`, which the gather ordered)
-  for (size_t i = 0; i < G && st == MI_OK; ++i) {
+  // the producer streams follow the last use of their key / LUT (shard 0's is `stream`, which the gather ordered) —
+  // also when a later step failed after some shards were already queued: the first error is still the one returned
+  for (size_t i = 0; i < G; ++i) {
     hipStream_t ps = producer(i);
     if (i == 0 && ps == (hipStream_t)stream) continue;
     hipError_t e = after(ps, i == 0 ? (hipStream_t)stream : m->streams[i], m->events[i], m->devices[i]);
-    if (e != hipSuccess) st = hip_fail(e, "producer-stream ordering");
+    if (e != hipSuccess && st == MI_OK) st = hip_fail(e, "producer-stream ordering");
   }
   return st;
 }

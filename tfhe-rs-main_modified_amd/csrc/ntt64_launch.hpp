@@ -53,6 +53,29 @@ hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint6
 
 namespace mi {
 
+// Where a bootstrap's accumulator starts and what it leaves (every PBS engine: pbs_tw.hip, pbs_kernels.hip,
+// pbs_large.hip).  The accumulator of item b starts as GLWE `lut_for(b)` of the list `lut` (glwe_len u64 each):
+//   lut_idx != NULL : GLWE lut_idx[b]; an index >= n_lut skips the item (nothing read, nothing written)
+//   per_item != 0   : GLWE b (blind_rotate_ntt64[_bnf]_assign: every item rotates its own accumulator)
+//   otherwise       : GLWE 0, shared by the batch (programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext)
+// glwe_out != NULL: the rotated accumulator of item b is stored to glwe_out[b] ((k+1) N u64; it may be the LUT list
+// itself, in place) instead of extracting sample 0 into lwe_out[b].  Item indices are global to the caller's batch.
+struct PbsIo {
+  const uint64_t* lut = nullptr;
+  const uint32_t* lut_idx = nullptr;
+  uint32_t n_lut = 1;
+  uint32_t per_item = 0;
+  uint64_t* glwe_out = nullptr;
+  __host__ __device__ const uint64_t* lut_for(uint64_t b, uint64_t glwe_len) const {
+    uint64_t i = per_item ? b : 0;
+    if (lut_idx) {
+      i = lut_idx[b];
+      if (i >= n_lut) return nullptr;
+    }
+    return lut + i * glwe_len;
+  }
+};
+
 // pbs_kernels.hip — Goldilocks, the shapes of mi::capi::check_pbs_shape up to N = 8192, any level count (callers
 // validate the shape; other shapes return hipErrorInvalidValue).
 hipError_t launch_lift_switched(uint64_t* dst, const uint64_t* src, size_t count, bool bnf, int logn, hipStream_t s);
@@ -66,13 +89,17 @@ hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, u
                               const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
                               const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx = nullptr,
                               uint32_t n_ggsw = 1);
-hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s);
+// extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160) at MonomialDegree(nth_first + j nth_stride)
+// for j < nth_count of every GLWE: out[b nth_count + j] (k N + 1 u64); modulus 0 = native 2^64
+hipError_t launch_sample_extract(uint64_t* out, const uint64_t* glwe, int logn, int k, size_t batch, size_t nth_first,
+                                 size_t nth_stride, size_t nth_count, uint64_t modulus, hipStream_t s);
 // pbs_large.hip — N = 2^14 ... 2^17 (beyond one workgroup): the blind rotation / external product as device-wide
 // passes per CMUX step over chunks of ciphertexts whose accumulators live in HBM; same arguments as above
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
-                            const uint64_t* lut, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
+                            const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
                             const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s);
 hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
                                     const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
@@ -92,9 +119,9 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
 hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_polys, uint64_t c, int scale,
                                  hipStream_t s, bool ext = false);
 hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count, hipStream_t s);
-hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,
+hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const PbsIo& io, const uint64_t* bsk,
                              size_t n_lwe, size_t batch, int base_log, const uint64_t* tab, hipStream_t s);
-hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const uint64_t* bsk, size_t n_lwe,
+hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const uint64_t* bsk, size_t n_lwe,
                          size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s);
 
 }  // namespace mi

@@ -187,7 +187,7 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void ext_product_kernel(u64* _
 // copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
 template <int LOGN, int K, bool BNF>
 __global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
-                                                             const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                             PbsIo io, const u64* __restrict__ bsk,
                                                              uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                              const u64* __restrict__ tw, const u64* __restrict__ itw,
                                                              int centered) {
@@ -198,6 +198,8 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restric
   const int t = threadIdx.x;
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;
+  const u64* lut = io.lut_for(b, (uint64_t)(K + 1) * N);
+  if (!lut) return;  // LUT index out of range: the item is left untouched
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
   const size_t ggsw_len = (size_t)level * (K + 1) * (K + 1) * N;
   const unsigned log_mod = S::LOG_MOD;
@@ -278,6 +280,19 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restric
     full = (int)(body / N) & 1;
     rem = (int)(body % N);
   }
+  if (io.glwe_out) {  // blind_rotate_ntt64[_bnf]_assign: the rotated GLWE itself
+    u64* g = io.glwe_out + (size_t)b * (K + 1) * N;
+#pragma unroll
+    for (int c = 0; c <= K; ++c)
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const int m = elem<G>(t, r, S::LO_COL);
+        u64 v = sh[c * N + ((m + rem) & (N - 1))];
+        if (full ^ (m >= N - rem)) v = neg_q<BNF>(v);
+        g[c * N + m] = v;
+      }
+    return;
+  }
   // rotated[c][m] = sign * acc[c][(m + rem) % N]; glwe_sample_extraction.rs:89-160: mask polynomial c
   // gives out[c N + 0] = A_c[0], out[c N + j] = -A_c[N - j]; the body coefficient 0 gives out[K N]
   u64* out = lwe_out + (size_t)b * (K * N + 1);
@@ -350,7 +365,45 @@ __global__ __launch_bounds__(256) void lift_switched_kernel(u64* __restrict__ ds
   }
 }
 
+// extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160) at nth = nth_first + j nth_stride:
+// mask polynomial c of the output is reverse(A_c), its first N - nth - 1 entries negated, rotated left by that count,
+// i.e. out[c N + i] = A_c[nth - i] for i <= nth and -A_c[N + nth - i] above; the body is B[nth].  Negation is
+// wrapping (native modulus, q = 0) or modulo the custom modulus q (slice_wrapping_opposite_assign_custom_mod).
+__global__ __launch_bounds__(256) void sample_extract_kernel(u64* __restrict__ out, const u64* __restrict__ glwe,
+                                                             uint32_t logn, uint32_t k, uint64_t batch,
+                                                             uint64_t nth_first, uint64_t nth_stride,
+                                                             uint64_t nth_count, u64 q) {
+  const uint64_t n = 1ull << logn, per_out = (uint64_t)k * n + 1, per_in = (uint64_t)(k + 1) * n;
+  const uint64_t total = batch * nth_count * per_out;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t item = i / per_out, o = i % per_out;
+    const uint64_t b = item / nth_count, nth = nth_first + (item % nth_count) * nth_stride;
+    const uint64_t c = o >> logn, j = o & (n - 1);  // o = k N: the body (c = k, j = 0)
+    const u64* a = glwe + b * per_in + c * n;
+    u64 v;
+    if (c == k) v = a[nth];
+    else if (j <= nth) v = a[nth - j];
+    else {
+      v = a[n + nth - j];
+      v = q ? (v == 0 ? 0 : q - v) : (u64)0 - v;
+    }
+    out[i] = v;
+  }
+}
+
 }  // namespace pbs
+
+hipError_t launch_sample_extract(uint64_t* out, const uint64_t* glwe, int logn, int k, size_t batch, size_t nth_first,
+                                 size_t nth_stride, size_t nth_count, uint64_t modulus, hipStream_t s) {
+  const uint64_t total = (uint64_t)batch * nth_count * (((uint64_t)k << logn) + 1);
+  if (total == 0) return hipSuccess;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(pbs::sample_extract_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, glwe, (uint32_t)logn,
+                     (uint32_t)k, (uint64_t)batch, (uint64_t)nth_first, (uint64_t)nth_stride, (uint64_t)nth_count,
+                     (u64)modulus);
+  return hipGetLastError();
+}
 
 // ---- dispatch ------------------------------------------------------------------------------------
 // Shapes compiled (callers validate, c_api.cpp mi::capi::check_pbs_shape): N = 1024 / 2048 / 4096 with K in {1, 2};
@@ -430,7 +483,7 @@ hipError_t launch_ext_product(int logn, int k, bool bnf, bool cmux, int level, u
 }
 
 template <int LOGN, int K>
-static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const PbsIo& lut,
                             const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                             const uint64_t* itw, int centered, hipStream_t s) {
   const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN, K>::T);
@@ -443,7 +496,7 @@ static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut,
+hipError_t launch_pbs(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in, const PbsIo& lut,
                       const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                       const uint64_t* itw, int centered, hipStream_t s) {
   if (batch == 0) return hipSuccess;

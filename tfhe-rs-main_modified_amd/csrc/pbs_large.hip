@@ -64,16 +64,20 @@ __device__ __forceinline__ void decompose_store(u64 x, u64* __restrict__ dst, ui
   }
 }
 
-// acc[b] = the LUT (BNF), or the LUT rotated by -ms(body) (Solinas, ntt64_pbs.rs:237-249)
+// acc[b] = the item's LUT (BNF), or the LUT rotated by -ms(body) (Solinas, ntt64_pbs.rs:237-249); item b of the chunk
+// is item b0 + b of the caller's batch (PbsIo); a skipped item (LUT index out of range) gets a zero accumulator
 template <bool BNF>
-__global__ __launch_bounds__(256) void large_init_acc(u64* __restrict__ acc, const u64* __restrict__ lut,
+__global__ __launch_bounds__(256) void large_init_acc(u64* __restrict__ acc, PbsIo io, uint64_t b0,
                                                       const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t batch,
                                                       LargeShape sh) {
   const uint64_t per = (uint64_t)(sh.k + 1) * sh.n, total = per * batch;
   for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
     const uint64_t b = i / per, ce = i % per;
     const uint32_t c = (uint32_t)(ce >> sh.logn), m = (uint32_t)(ce & (sh.n - 1));
-    if (BNF) {
+    const u64* lut = io.lut_for(b0 + b, per);
+    if (!lut) {
+      acc[i] = 0;
+    } else if (BNF) {
       acc[i] = lut[ce];
     } else {
       const u64 body = ms_non_native(lwe_in[b * (n_lwe + 1) + n_lwe], sh.logn + 1);
@@ -181,14 +185,18 @@ __global__ __launch_bounds__(256) void large_body_correction(u64* __restrict__ c
 // BNF: rotate by -ms(body [+ centered correction]) (ntt64_bnf_pbs.rs:262-270); Solinas: the LUT was pre-rotated;
 // then sample extraction of coefficient 0 (glwe_sample_extraction.rs:89-160): out[c N] = A_c[0],
 // out[c N + j] = -A_c[N - j], out[k N] = B[0]
-template <bool BNF>
+// With io.glwe_out the rotated accumulator itself is stored (blind_rotate_ntt64[_bnf]_assign); skipped items
+// (io.lut_for == NULL) are not written.  lwe_out / glwe_out point at the chunk's first item; b0 is its global index.
+template <bool BNF, bool GLWE>
 __global__ __launch_bounds__(256) void large_extract(u64* __restrict__ lwe_out, const u64* __restrict__ acc,
                                                      const u64* __restrict__ lwe_in, const u64* __restrict__ corr,
-                                                     uint32_t n_lwe, uint32_t batch, LargeShape sh) {
-  const uint64_t per_out = (uint64_t)sh.k * sh.n + 1, total = per_out * batch;
+                                                     uint32_t n_lwe, uint32_t batch, LargeShape sh, PbsIo io,
+                                                     uint64_t b0) {
   const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
+  const uint64_t per_out = GLWE ? per : (uint64_t)sh.k * sh.n + 1, total = per_out * batch;
   for (uint64_t i = grid_stride_start(); i < total; i += grid_stride()) {
     const uint64_t b = i / per_out, o = i % per_out;
+    if ((io.lut_idx || GLWE) && !io.lut_for(b0 + b, per)) continue;
     uint32_t full = 0, rem = 0;
     if (BNF) {
       const u64 body = modulus_switch(lwe_in[b * (n_lwe + 1) + n_lwe] + (corr ? corr[b] : 0), sh.logn + 1);
@@ -196,6 +204,12 @@ __global__ __launch_bounds__(256) void large_extract(u64* __restrict__ lwe_out, 
       rem = (uint32_t)(body & (sh.n - 1));
     }
     const uint32_t c = (uint32_t)(o >> sh.logn), j = (uint32_t)(o & (sh.n - 1));  // o = k N gives c = k, j = 0
+    if (GLWE) {  // new[j] = old[(j + rem) % N], negated for j >= N - rem
+      u64 v = acc[b * per + (uint64_t)c * sh.n + ((j + rem) & (sh.n - 1))];
+      if (full ^ (j >= sh.n - rem)) v = neg_q<BNF>(v);
+      lwe_out[i] = v;
+      continue;
+    }
     const uint32_t m = (j == 0) ? 0 : sh.n - j;
     u64 v = acc[b * per + (uint64_t)c * sh.n + ((m + rem) & (sh.n - 1))];
     if (full ^ (m >= sh.n - rem)) v = neg_q<BNF>(v);
@@ -231,7 +245,7 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 }  // namespace pbs
 
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
-                            const uint64_t* lut, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
+                            const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
                             const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s) {
   using namespace pbs;
   if (batch == 0) return hipSuccess;
@@ -251,11 +265,11 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
     const u64* in = lwe_in + b0 * (n_lwe + 1);
     const uint64_t elems = (uint64_t)nb * per;
     if (bnf)
-      hipLaunchKernelGGL(large_init_acc<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, lut, in, (uint32_t)n_lwe,
-                         nb, sh);
+      hipLaunchKernelGGL(large_init_acc<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, io, (uint64_t)b0, in,
+                         (uint32_t)n_lwe, nb, sh);
     else
-      hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, lut, in, (uint32_t)n_lwe,
-                         nb, sh);
+      hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, io, (uint64_t)b0, in,
+                         (uint32_t)n_lwe, nb, sh);
     for (uint32_t i = 0; i < n_lwe && e == hipSuccess; ++i) {
       if (bnf)
         hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
@@ -282,14 +296,26 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
     if (corr_on)
       hipLaunchKernelGGL(large_body_correction, dim3(nb), dim3(256), 0, s, corr, in, (uint32_t)n_lwe,
                          (unsigned)(logn + 1));
-    const uint64_t outs = (uint64_t)nb * ((uint64_t)k * sh.n + 1);
-    u64* o = out + b0 * ((size_t)k * sh.n + 1);
-    if (bnf)
-      hipLaunchKernelGGL(large_extract<true>, dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in,
-                         corr_on ? corr : (const u64*)nullptr, (uint32_t)n_lwe, nb, sh);
-    else
-      hipLaunchKernelGGL(large_extract<false>, dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in,
-                         (const u64*)nullptr, (uint32_t)n_lwe, nb, sh);
+    const u64* cr = corr_on ? corr : (const u64*)nullptr;
+    if (io.glwe_out) {
+      const uint64_t outs = (uint64_t)nb * per;
+      u64* o = io.glwe_out + b0 * per;
+      if (bnf)
+        hipLaunchKernelGGL((large_extract<true, true>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
+                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+      else
+        hipLaunchKernelGGL((large_extract<false, true>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
+                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+    } else {
+      const uint64_t outs = (uint64_t)nb * ((uint64_t)k * sh.n + 1);
+      u64* o = out + b0 * ((size_t)k * sh.n + 1);
+      if (bnf)
+        hipLaunchKernelGGL((large_extract<true, false>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
+                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+      else
+        hipLaunchKernelGGL((large_extract<false, false>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
+                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+    }
     e = hipGetLastError();
   }
   const hipError_t ef = mi::scratch_free(scratch, s);

@@ -67,10 +67,11 @@ __device__ __forceinline__ void load_lane_pair_tables(u64* lwtab, const u64* __r
   __syncthreads();
 }
 
-// lwe_in: batch x (n+1); lut: 2 x N; bsk: n x 2 x 2 x N (NTT domain, N^-1 folded in);
-// tab: [fwd twist (N) | fwd lane-pair twiddles (32) | inverse twist (N) | inverse lane-pair (32) | ...].
+// lwe_in: batch x (n+1); io: the accumulator's LUT (2 x N per GLWE) and the output form (PbsIo); bsk: n x 2 x 2 x N
+// (NTT domain, N^-1 folded in); tab: [fwd twist (N) | fwd lane-pair twiddles (32) | inverse twist (N) | inverse
+// lane-pair (32) | ...].
 __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
-                                                     const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                     PbsIo io, const u64* __restrict__ bsk,
                                                      uint32_t n_lwe, uint32_t batch, int base_log,
                                                      const u64* __restrict__ tab, int centered) {
   __shared__ u64 buf[2 * NPW];
@@ -80,6 +81,8 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;  // uniform per workgroup
+  const u64* lut = io.lut_for(b, 2 * N);
+  if (!lut) return;  // LUT index out of range: the item is left untouched
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
   load_lane_pair_tables(lwtab, tab, t);  // ends with a workgroup barrier
   u64 body_corr = 0;
@@ -104,6 +107,17 @@ __global__ __launch_bounds__(128) void pbs_tw_kernel(u64* __restrict__ lwe_out, 
   const u64* acc = buf + w * NPW;
   const u64 body = modulus_switch(lwe[n_lwe] + body_corr, LOG_MOD);
   const int full = (int)(body / N) & 1, rem = (int)(body % N);
+  if (io.glwe_out) {  // blind_rotate_ntt64_bnf_assign: the rotated GLWE itself (new[m] = old[(m + rem) % N], signed)
+    u64* g = io.glwe_out + ((size_t)b * 2 + w) * N;
+#pragma unroll 4
+    for (int r = 0; r < 32; ++r) {
+      const int m = 64 * r + (int)lane;
+      u64 v = acc[(m + rem) & (N - 1)];
+      if (full ^ (m >= N - rem)) v = (u64)0 - v;
+      g[m] = v;
+    }
+    return;
+  }
   u64* out = lwe_out + (size_t)b * (N + 1);
   if (w == 0) {
 #pragma unroll 4
@@ -148,7 +162,7 @@ __global__ __launch_bounds__(256) void ms_non_native_kernel(u64* __restrict__ ds
 // (polynomial_wrapping_monic_monomial_div_assign_custom_mod, ntt64_pbs.rs:237-249); the body runs the
 // loop; sample extraction at nth = 0 negates modulo p (glwe_sample_extraction.rs:89-160).
 __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ switched,
-                                                         const u64* __restrict__ lut, const u64* __restrict__ bsk,
+                                                         PbsIo io, const u64* __restrict__ bsk,
                                                          uint32_t n_lwe, uint32_t batch, int base_log,
                                                          const u64* __restrict__ tab) {
   __shared__ u64 buf[2 * NPW];
@@ -158,6 +172,8 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
   const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t b = blockIdx.x;
   if (b >= batch) return;
+  const u64* lut = io.lut_for(b, 2 * N);
+  if (!lut) return;  // LUT index out of range: the item is left untouched
   const u64* msw = switched + (size_t)b * (n_lwe + 1);
   load_lane_pair_tables(lwtab, tab, t);
   {
@@ -184,6 +200,12 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
                      [n] "s"(n_lwe), [tab_lo] "s"(tab_lo), [tab_hi] "s"(tab_hi), [bl] "s"(base_log),
                      [LW] "s"((uint32_t)(uintptr_t)lwtab));
   const u64* acc = buf + w * NPW;
+  if (io.glwe_out) {  // blind_rotate_ntt64_assign: the accumulator (rotated by -ms(b) before the loop)
+    u64* g = io.glwe_out + ((size_t)b * 2 + w) * N;
+#pragma unroll 4
+    for (int r = 0; r < 32; ++r) g[64 * r + lane] = acc[64 * r + lane];
+    return;
+  }
   u64* out = lwe_out + (size_t)b * (N + 1);
   if (w == 0) {
 #pragma unroll 4
@@ -316,20 +338,20 @@ hipError_t launch_ms_non_native(uint64_t* dst, const uint64_t* src, size_t count
   return hipGetLastError();
 }
 
-hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const uint64_t* lut, const uint64_t* bsk,
+hipError_t launch_pbs_tw_sol(uint64_t* out, const uint64_t* switched, const PbsIo& io, const uint64_t* bsk,
                              size_t n_lwe, size_t batch, int base_log, const uint64_t* tab, hipStream_t s) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pbstw::pbs_tw_sol_kernel, dim3((unsigned)batch), dim3(128), 0, s, out, switched, lut, bsk,
+  hipLaunchKernelGGL(pbstw::pbs_tw_sol_kernel, dim3((unsigned)batch), dim3(128), 0, s, out, switched, io, bsk,
                      (uint32_t)n_lwe, (uint32_t)batch, base_log, tab);
   return hipGetLastError();
 }
 
-hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const uint64_t* bsk, size_t n_lwe,
+hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const uint64_t* bsk, size_t n_lwe,
                          size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pbstw::pbs_tw_kernel, dim3((unsigned)batch), dim3(128), 0, s, out, lwe_in, lut, bsk,
+  hipLaunchKernelGGL(pbstw::pbs_tw_kernel, dim3((unsigned)batch), dim3(128), 0, s, out, lwe_in, io, bsk,
                      (uint32_t)n_lwe, (uint32_t)batch, base_log, tab, centered);
   return hipGetLastError();
 }

@@ -1,0 +1,156 @@
+// scratch.cpp — the event-ordered scratch pool (scratch.hpp).
+#include "scratch.hpp"
+
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace mi {
+namespace {
+
+struct Block {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int device = 0;
+  hipEvent_t last_use = nullptr;  // recorded on the stream of the block's last user
+  bool recorded = false;
+};
+
+struct Pool {
+  std::mutex mu;
+  std::vector<Block> idle;
+  std::unordered_map<void*, Block> busy;
+};
+
+Pool& pool() {
+  static Pool* p = new Pool;  // never destroyed: the HIP runtime may be torn down before static destructors run
+  return *p;
+}
+
+constexpr size_t GRAIN = (size_t)1 << 20;  // blocks are whole MiB
+
+// frees blocks that no longer have a pending user (their event has completed)
+void release(std::vector<Block>& blocks) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (Block& b : blocks) {
+    (void)hipSetDevice(b.device);
+    if (b.recorded) (void)hipEventSynchronize(b.last_use);
+    (void)hipEventDestroy(b.last_use);
+    (void)hipFree(b.p);
+  }
+  (void)hipSetDevice(cur);
+}
+
+}  // namespace
+
+hipError_t scratch_alloc(void** out, size_t bytes, hipStream_t s) {
+  *out = nullptr;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (bytes == 0) bytes = 1;
+  Pool& P = pool();
+  Block blk;
+  bool found = false;
+  std::vector<Block> smaller;  // idle blocks a new, larger block supersedes
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto best = P.idle.end();
+    for (auto it = P.idle.begin(); it != P.idle.end(); ++it)
+      if (it->device == dev && it->bytes >= bytes && (best == P.idle.end() || it->bytes < best->bytes)) best = it;
+    if (best != P.idle.end()) {
+      blk = *best;
+      P.idle.erase(best);
+      P.busy[blk.p] = blk;
+      found = true;
+    } else {
+      auto keep = std::partition(P.idle.begin(), P.idle.end(), [&](const Block& b) { return b.device != dev; });
+      smaller.assign(keep, P.idle.end());
+      P.idle.erase(keep, P.idle.end());
+    }
+  }
+  if (found) {
+    if (blk.recorded && (e = hipStreamWaitEvent(s, blk.last_use, 0)) != hipSuccess) {
+      (void)scratch_free(blk.p, nullptr);
+      return e;
+    }
+    *out = blk.p;
+    return hipSuccess;
+  }
+  release(smaller);
+  blk = Block{};
+  blk.device = dev;
+  blk.bytes = (bytes + GRAIN - 1) / GRAIN * GRAIN;
+  if ((e = hipMalloc(&blk.p, blk.bytes)) != hipSuccess) {
+    (void)hipGetLastError();
+    return e;
+  }
+  if ((e = hipEventCreateWithFlags(&blk.last_use, hipEventDisableTiming)) != hipSuccess) {
+    (void)hipFree(blk.p);
+    return e;
+  }
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.busy[blk.p] = blk;
+  }
+  *out = blk.p;
+  return hipSuccess;
+}
+
+hipError_t scratch_free(void* p, hipStream_t s) {
+  if (!p) return hipSuccess;
+  Pool& P = pool();
+  Block blk;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.busy.find(p);
+    if (it == P.busy.end()) return hipErrorInvalidValue;
+    blk = it->second;
+  }
+  // the block is still owned by this caller: record before it becomes visible to others
+  const hipError_t e = hipEventRecord(blk.last_use, s);
+  blk.recorded = e == hipSuccess;
+  if (!blk.recorded) {  // cannot order the next user: retire the block after the device drains
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.busy.erase(p);
+    std::vector<Block> one{blk};
+    release(one);
+    return e;
+  }
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.busy.erase(p);
+  P.idle.push_back(blk);
+  return hipSuccess;
+}
+
+size_t scratch_trim(int device) {
+  Pool& P = pool();
+  std::vector<Block> out;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto keep = std::partition(P.idle.begin(), P.idle.end(),
+                               [&](const Block& b) { return device >= 0 && b.device != device; });
+    out.assign(keep, P.idle.end());
+    P.idle.erase(keep, P.idle.end());
+  }
+  size_t bytes = 0;
+  for (const Block& b : out) bytes += b.bytes;
+  release(out);
+  return bytes;
+}
+
+size_t scratch_bytes(int device) {
+  Pool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  size_t bytes = 0;
+  for (const Block& b : P.idle)
+    if (device < 0 || b.device == device) bytes += b.bytes;
+  for (const auto& kv : P.busy)
+    if (device < 0 || kv.second.device == device) bytes += kv.second.bytes;
+  return bytes;
+}
+
+}  // namespace mi

@@ -1,24 +1,25 @@
-// scratch.hpp — temporary device buffers of the batched entry points.  On a caller's stream they are stream-ordered
-// (hipMallocAsync / hipFreeAsync: no device synchronisation per call).  On the legacy null stream (stream == NULL,
-// the C ABI's default) they are plain allocations freed after the stream drains: with the /opt/rocm 7.2 runtime the
-// C++ mirror suite saw stream-ordered scratch on the null stream come back with stale contents (an in-place Fourier
-// reorder and a generic f64 external product at N = 8192, a few runs in a hundred; tools/fftg_rt_probe.cpp), which the
-// plain allocation does not show.
+// scratch.hpp — temporary device buffers of the batched entry points (the Solinas PBS's switched mask, the PRE_SWITCHED
+// lift, the external product's W1'-ordered GGSW, the generic f64 engine's digit spectra, pbs_large's accumulators, the
+// keyswitch digits, the multi-GPU shard staging).
+//
+// A per-device pool of plain hipMalloc blocks, kept for reuse and grown on demand (scratch.cpp).  Ordering is by event,
+// not by host synchronisation: each block carries the event recorded on the stream of its last user, and the next
+// user's stream waits on it (hipStreamWaitEvent) before its first launch.  So a block is never reissued before the
+// last kernel that read it retired, on any stream, and no call blocks the host — on the legacy null stream or on a
+// caller's stream alike.  The stream-ordered allocator (hipMallocAsync) is not used: DESIGN.md §5 records why.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 
 namespace mi {
 
-inline hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
-  return s ? hipMallocAsync(p, bytes, s) : hipMalloc(p, bytes);
-}
-
-inline hipError_t scratch_free(void* p, hipStream_t s) {
-  if (!p) return hipSuccess;
-  if (s) return hipFreeAsync(p, s);
-  const hipError_t e = hipStreamSynchronize(nullptr);
-  const hipError_t f = hipFree(p);
-  return e != hipSuccess ? e : f;
-}
+// a block of >= bytes on the current device, ordered after the block's previous user; *p = nullptr on failure
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
+// returns the block to the pool once the work already queued on `s` has been enqueued (event recorded on `s`)
+hipError_t scratch_free(void* p, hipStream_t s);
+// frees every idle block of `device` (-1: all devices) after its last user retired; returns the bytes released
+size_t scratch_trim(int device);
+// bytes held by the pool on `device` (idle + in use)
+size_t scratch_bytes(int device);
 
 }  // namespace mi

@@ -67,6 +67,11 @@ _SIGS = {
     "mi_ntt_bsk_write": (_int, [_vp, _vp, _int, _vp, _sz]),
     "mi_pbs_ntt64_key_load": (_int, [_vp, _vp, _sz, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_pbs_ntt64_batch_lut_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _sz, _int, _vp]),
+    "mi_blind_rotate_ntt64_batch": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_sample_extract_batch": (_int, [_vp, _vp, _sz, _int, _sz, _sz, _sz, _sz, _u64, _int, _vp]),
+    "mi_scratch_trim": (_int, [_int, ctypes.POINTER(_sz)]),
+    "mi_scratch_bytes": (_int, [_int, ctypes.POINTER(_sz)]),
     "mi_multi_gpu_create": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
     "mi_multi_gpu_destroy": (_int, [_vp]),
     "mi_multi_gpu_count": (_int, [_vp, ctypes.POINTER(_int)]),

@@ -8,6 +8,8 @@ Function names follow the reference (paths relative to /root/reference/tfhe/src/
 * ``cmux_ntt64_assign`` / ``cmux_ntt64_bnf_assign``   ntt64_pbs.rs:669-680 / ntt64_bnf_pbs.rs:683-705
 * ``programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized``
                                                      ntt64_pbs.rs:482-538 / ntt64_bnf_pbs.rs:469-540
+* ``blind_rotate_ntt64[_bnf]_assign``                 ntt64_pbs.rs:176-286 / ntt64_bnf_pbs.rs:174-266
+* ``extract_lwe_sample_from_glwe_ciphertext``        algorithms/glwe_sample_extraction.rs:89-160
 
 Every operand is a HIP device tensor (uint64 / int64).  The reference works on one ciphertext per
 call; here a leading batch dimension is allowed everywhere (the reference's rayon loop over
@@ -207,36 +209,122 @@ class NttBootstrapKey:
         return cls(plan, bsk, f["decomposition_base_log"], f["decomposition_level_count"], variant)
 
 
-def _pbs(key, lwe_in, lwe_out, accumulator, ms_mode):
+def _lwe_batch(key, lwe_in):
     n_in = key.input_lwe_dimension + 1
     if lwe_in.shape[-1] != n_in:
         raise ValueError(f"assertion failed: input lwe size {lwe_in.shape[-1]} != {n_in}")
-    batch = lwe_in.numel() // n_in
+    return lwe_in.numel() // n_in
+
+
+def _index(idx, count, device, name):
+    import torch
+
+    if (idx.dtype not in (torch.int32, torch.uint32) or idx.numel() != count or not idx.is_cuda
+            or not idx.is_contiguous() or idx.device != device):
+        raise ValueError(f"assertion failed: {name} must be {count} contiguous int32 indices on the LWEs' device")
+    return ctypes.c_void_p(idx.data_ptr())
+
+
+def _pbs(key, lwe_in, lwe_out, accumulator, ms_mode, lut_index=None):
+    batch = _lwe_batch(key, lwe_in)
     if lwe_out.shape[-1] != key.output_lwe_size() or lwe_out.numel() // key.output_lwe_size() != batch:
         raise ValueError(f"assertion failed: output lwe shape {tuple(lwe_out.shape)}")
-    if tuple(accumulator.shape) != (key.glwe_dimension + 1, key.polynomial_size):
-        raise ValueError(f"assertion failed: accumulator shape {tuple(accumulator.shape)}")
-    check(lib().mi_pbs_ntt64_batch(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
-                                   _dev(accumulator, "accumulator"), batch, ms_mode, _stream(lwe_out)))
+    glwe = (key.glwe_dimension + 1, key.polynomial_size)
+    if lut_index is None:
+        if tuple(accumulator.shape) != glwe:
+            raise ValueError(f"assertion failed: accumulator shape {tuple(accumulator.shape)}")
+        check(lib().mi_pbs_ntt64_batch(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                       _dev(accumulator, "accumulator"), batch, ms_mode, _stream(lwe_out)))
+        return
+    if accumulator.dim() != 3 or tuple(accumulator.shape[1:]) != glwe:
+        raise ValueError(f"assertion failed: accumulator list shape {tuple(accumulator.shape)} != (n_lut, *{glwe})")
+    check(lib().mi_pbs_ntt64_batch_lut_indexed(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                               _dev(accumulator, "accumulator"),
+                                               _index(lut_index, batch, lwe_in.device, "lut_index"),
+                                               int(accumulator.shape[0]), batch, ms_mode, _stream(lwe_out)))
 
 
 def programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key,
-                                                                  ms_mode: int = MS_STANDARD) -> None:
-    """Batched BNF PBS of native-modulus LWEs (ntt64_bnf_pbs.rs:469-540)."""
+                                                                  ms_mode: int = MS_STANDARD, lut_index=None) -> None:
+    """Batched BNF PBS of native-modulus LWEs (ntt64_bnf_pbs.rs:469-540).  With ``lut_index`` (int32 device tensor,
+    one entry per item) ``accumulator`` is a list (n_lut, k+1, N) and item b bootstraps through
+    ``accumulator[lut_index[b]]`` (an out-of-range index leaves ``lwe_out[b]`` untouched)."""
     if key.variant != BNF:
         raise ValueError("key was not prepared for the BNF variant")
-    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode)
+    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode, lut_index)
 
 
 def programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe_in, lwe_out, accumulator, key,
-                                                              ms_mode: int = MS_STANDARD) -> None:
+                                                              ms_mode: int = MS_STANDARD, lut_index=None) -> None:
     """Batched PBS of LWEs modulo the Solinas prime (ntt64_pbs.rs:482-538); ms_mode STANDARD or
-    PRE_SWITCHED."""
+    PRE_SWITCHED; ``lut_index`` as for the BNF form."""
     if key.variant != SOLINAS:
         raise ValueError("key was not prepared for the Solinas variant")
     if ms_mode == MS_CENTERED:
         raise ValueError("centered modulus switch applies to native-modulus (BNF) inputs")
-    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode)
+    _pbs(key, lwe_in, lwe_out, accumulator, ms_mode, lut_index)
+
+
+def _blind_rotate(key, lwe_in, lut, ms_mode):
+    batch = _lwe_batch(key, lwe_in)
+    glwe = (key.glwe_dimension + 1, key.polynomial_size)
+    if lut.dim() < 2 or tuple(lut.shape[-2:]) != glwe or lut.numel() != batch * glwe[0] * glwe[1]:
+        raise ValueError(f"assertion failed: lut shape {tuple(lut.shape)} != ({batch}, *{glwe})")
+    check(lib().mi_blind_rotate_ntt64_batch(key._h, _dev(lut, "lut"), _dev(lwe_in, "lwe_in"), batch, ms_mode,
+                                            _stream(lut)))
+
+
+def blind_rotate_ntt64_bnf_assign(msed_input, lut, key, ms_mode: int = MS_PRE_SWITCHED) -> None:
+    """blind_rotate_ntt64_bnf_assign[_mem_optimized] (ntt64_bnf_pbs.rs:174-266), batched and in place: every item's
+    GLWE ``lut[b]`` is rotated by ``msed_input[b]``.  The reference's input is a ModulusSwitchedLweCiphertext:
+    ``MS_PRE_SWITCHED`` (default) takes the switched values (in [0, 2N)); ``MS_STANDARD`` / ``MS_CENTERED`` take the
+    native LWE and switch it on the device (lwe_ciphertext_modulus_switch / the centered binary switch)."""
+    if key.variant != BNF:
+        raise ValueError("key was not prepared for the BNF variant")
+    _blind_rotate(key, msed_input, lut, ms_mode)
+
+
+def blind_rotate_ntt64_assign(lwe_in, lut, key, ms_mode: int = MS_STANDARD) -> None:
+    """blind_rotate_ntt64_assign[_mem_optimized] (ntt64_pbs.rs:176-286), batched and in place: LWEs modulo the Solinas
+    prime (or ``MS_PRE_SWITCHED`` values)."""
+    if key.variant != SOLINAS:
+        raise ValueError("key was not prepared for the Solinas variant")
+    if ms_mode == MS_CENTERED:
+        raise ValueError("centered modulus switch applies to native-modulus (BNF) inputs")
+    _blind_rotate(key, lwe_in, lut, ms_mode)
+
+
+def extract_lwe_sample_from_glwe_ciphertext(glwe, lwe_out, nth: int = 0, nth_stride: int = 0, nth_count: int = 1,
+                                            modulus: int = 0) -> None:
+    """extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160) over a batch of GLWEs
+    (..., k+1, N): lwe_out[b, j] = the LWE of coefficient ``nth + j * nth_stride`` of glwe[b], j < nth_count
+    (lwe_out: (batch, nth_count, k N + 1), or (batch, k N + 1) when nth_count is 1).  ``modulus`` 0 = native 2^64,
+    else the custom modulus (e.g. the Solinas prime)."""
+    if glwe.dim() < 2:
+        raise ValueError(f"assertion failed: glwe shape {tuple(glwe.shape)}")
+    kp1, n = int(glwe.shape[-2]), int(glwe.shape[-1])
+    batch = glwe.numel() // (kp1 * n)
+    out_len = (kp1 - 1) * n + 1
+    if lwe_out.shape[-1] != out_len or lwe_out.numel() != batch * nth_count * out_len:
+        raise ValueError(f"assertion failed: lwe_out shape {tuple(lwe_out.shape)} != ({batch}, {nth_count}, {out_len})")
+    if lwe_out.device != glwe.device:
+        raise ValueError("glwe and lwe_out must be on one device")
+    check(lib().mi_sample_extract_batch(_dev(lwe_out, "lwe_out"), _dev(glwe, "glwe"), n, kp1 - 1, batch, int(nth),
+                                        int(nth_stride), int(nth_count), int(modulus), glwe.device.index,
+                                        _stream(glwe)))
+
+
+def scratch_trim(device: int = -1) -> int:
+    """Frees the idle blocks of the engine's scratch pool (``mi_scratch_trim``); returns the bytes released."""
+    out = ctypes.c_size_t()
+    check(lib().mi_scratch_trim(int(device), ctypes.byref(out)))
+    return out.value
+
+
+def scratch_bytes(device: int = -1) -> int:
+    out = ctypes.c_size_t()
+    check(lib().mi_scratch_bytes(int(device), ctypes.byref(out)))
+    return out.value
 
 
 __all__ = [
@@ -244,5 +332,6 @@ __all__ = [
     "convert_standard_lwe_bootstrap_key_to_ntt64", "add_external_product_ntt64_assign",
     "add_external_product_ntt64_bnf_assign", "cmux_ntt64_assign", "cmux_ntt64_bnf_assign",
     "programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized",
-    "programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized",
+    "programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized", "blind_rotate_ntt64_bnf_assign",
+    "blind_rotate_ntt64_assign", "extract_lwe_sample_from_glwe_ciphertext", "scratch_trim", "scratch_bytes",
 ]
