@@ -544,13 +544,22 @@ def bench_ext_product(args, eng, torch, dev, world, barrier, dist):
     glwe = torch.empty((batch, 2, N), dtype=torch.int64, device=dev)
     eng.fill_uniform(glwe, SEED + 31, 0)
     out = torch.zeros((batch, 2, N), dtype=torch.int64, device=dev)
-    run = lambda: M.add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, PBS_BASE_LOG, 1)
+    # the GGSW is prepared once (mi_ntt64_ggsw_create: permuted into the bodies' read order), as a key is; the raw-pointer
+    # form, which permutes it on every call, is timed beside it (raw_ggsw_per_call)
+    prepared = M.NttGgswList(plan, ggsw, PBS_BASE_LOG, 1, M.BNF)
+    torch.cuda.synchronize()
+    run_raw = lambda: M.add_external_product_ntt64_bnf_assign(plan, out, ggsw, glwe, PBS_BASE_LOG, 1)
+    K_raw, el_raw, kernel_ms_raw = timed_leg(run_raw, torch, barrier, dist, dev)
+    run = lambda: M.add_external_product_ntt64_bnf_assign(plan, out, prepared, glwe, PBS_BASE_LOG, 1)
     K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev)
     hbm = EXT_BYTES * batch / (kernel_ms * 1e-3) / 1e9
     return {"metric": "GGSW x GLWE external products/sec (config 3)", "value": world * batch * K / el,
             "unit": "external products/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms,
-            "config": {"workload": "add_external_product_ntt64_bnf_assign, N=2048, k=1, level 1, base_log 23",
+            "config": {"workload": "add_external_product_ntt64_bnf_assign, N=2048, k=1, level 1, base_log 23, "
+                                   "prepared GGSW (NttGgswList)",
                        "batch_per_gpu": batch},
+            "raw_ggsw_per_call": {"value": world * batch * K_raw / el_raw, "kernel_ms": kernel_ms_raw,
+                                  "note": "the same products through the raw-pointer call (GGSW permuted per call)"},
             "algorithmic_bytes_per_unit": EXT_BYTES,
             "roofline": dict(valu_roofline(2, VALU_CYCLES["ext_bnf"], batch, kernel_ms,
                                            "bound by integer VALU issue (2 waves per product: decomposition, 2 fwd + "

@@ -153,6 +153,24 @@ int mi_cmux_ntt64_batch_indexed(const mi_ntt64_plan *plan, uint64_t *ct0, uint64
                                 const uint32_t *ggsw_index, size_t n_ggsw, int k, int base_log, int level,
                                 size_t batch, int variant, void *stream);
 
+/* A GGSW list made ready for repeated external products / CMUXes (the reference's NttGgswCiphertext[List] kept in the
+ * NTT domain, entities/ntt_ggsw_ciphertext_list.rs): n_ggsw GGSWs back to back (layout above) on the plan's device.
+ * The fused N = 2048, k = 1, level-1 bodies read their GGSW in their own coefficient order (pbs_tw.hip), so for that
+ * shape the list is permuted once into a private copy (on `stream`, synchronised before returning; the caller's
+ * buffer may then be freed); every other shape references the caller's list (keep it alive).  The raw-pointer calls
+ * above permute a twisted-shape GGSW on every call. */
+typedef struct mi_ntt64_ggsw mi_ntt64_ggsw;
+int mi_ntt64_ggsw_create(const mi_ntt64_plan *plan, const uint64_t *ggsw_list, size_t n_ggsw, int k, int base_log,
+                         int level, int variant, void *stream, mi_ntt64_ggsw **out);
+int mi_ntt64_ggsw_destroy(mi_ntt64_ggsw *ggsw);
+int mi_ntt64_ggsw_info(const mi_ntt64_ggsw *ggsw, size_t *n_ggsw, int *k, int *base_log, int *level, int *variant);
+/* mi_ext_product_ntt64_batch / mi_cmux_ntt64_batch on a prepared list: ggsw_index NULL = GGSW 0 for every item, else
+ * item b uses GGSW ggsw_index[b] (an index >= n_ggsw leaves the item untouched, as the _indexed calls). */
+int mi_ext_product_ntt64_prepared_batch(const mi_ntt64_ggsw *ggsw, uint64_t *out_glwe, const uint64_t *in_glwe,
+                                        const uint32_t *ggsw_index, size_t batch, void *stream);
+int mi_cmux_ntt64_prepared_batch(const mi_ntt64_ggsw *ggsw, uint64_t *ct0, uint64_t *ct1, const uint32_t *ggsw_index,
+                                 size_t batch, void *stream);
+
 /* A bootstrap key made ready for mi_pbs_ntt64_batch on the plan's device.  MI_NTT64_BNF keys
  * (converted Raw, as ntt64_bnf_pbs.rs tests do) are copied once with N^{-1} folded in — the
  * reference normalises each product at run time (ntt64_bnf_pbs.rs:670); in exact mod-p arithmetic

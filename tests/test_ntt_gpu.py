@@ -213,3 +213,22 @@ def test_headline_batch_full_parity(engine, oracle):
     back = host(t)
     # size-independent property: inv(fwd(x)) == N x mod p, i.e. normalize(inv(fwd(x))) == x
     assert np.array_equal(ora.normalize(back), x)
+
+
+def test_split_transform_chunked_batch(engine, oracle):
+    """The split transform (N = 4096: one top stage + the twisted 2048 body on 2 blocks per polynomial) on a batch
+    past the top pass's 65,535-polynomial grid.y chunk: the polynomials on both sides of the chunk edge equal the
+    oracle, and normalize(inv(fwd(x))) == x over the whole batch (checked on the device)."""
+    import torch
+    n, batch = 4096, 65535 + 4
+    plan, ora = engine.Plan.try_new(n, SOLINAS_P), oracle.Plan.try_new(n, SOLINAS_P)
+    x = torch.empty((batch, n), dtype=torch.int64, device="cuda")
+    engine.fill_uniform(x, 0x5917, SOLINAS_P)
+    t = x.clone()
+    plan.fwd(t)
+    rows = [0, 1, 65533, 65534, 65535, 65536, batch - 1]
+    xs = host(x[rows])
+    assert np.array_equal(host(t[rows]), ora.fwd(xs, threads=8))
+    plan.inv(t)
+    plan.normalize(t)
+    assert torch.equal(t, x)

@@ -3,6 +3,9 @@
 The reference cannot be compiled here (Rust, no cargo), so these KATs/properties — copied as
 *data* from the reference's test modules — are what make the oracle trustworthy.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
@@ -161,3 +164,12 @@ def test_generator_range(oracle):
         if p:
             assert int(v.max()) < p
     assert len(set(oracle.fill_uniform(5, SOLINAS_P, 4096).tolist())) == 4096
+
+
+@pytest.mark.parametrize("logn", [12, 13, 14, 15, 16, 17])
+def test_split_factorisation(logn):
+    """The split transform's factorisation (ntt64_kernels.hip launch_ntt_split): t = log2 N - 11 reference stages, the
+    block twist alpha_b^j, the 2048-point plan's transform per block == the N-point oracle transform, both directions."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import check_split_factorisation as C
+    assert C.check(logn) == (True, True)

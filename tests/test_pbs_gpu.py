@@ -509,3 +509,44 @@ def test_indexed_ggsw_ext_product_and_cmux(engine, oracle, bnf, n, k, base_log, 
     assert np.array_equal(host(t1), want1)
     with pytest.raises(ValueError):
         fn(pl, t0, t1, dev(ggsw), base_log, level, ggsw_index=tidx[:3])
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+@pytest.mark.parametrize("n,k,base_log,level", [(2048, 1, 23, 1), (2048, 1, 12, 2), (1024, 2, 23, 1), (16384, 1, 23, 1)])
+def test_prepared_ggsw_list(engine, oracle, bnf, n, k, base_log, level):
+    """NttGgswList (mi_ntt64_ggsw_create: the twisted-shape list permuted once into a private copy, other shapes
+    referenced): the external product and CMUX through it equal the raw-pointer calls and the oracle, shared and
+    indexed; the prepared copy survives the caller's tensor being overwritten."""
+    import torch
+    q = 0 if bnf else P
+    g = H.rng(6100 + n + k + level + bnf)
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    n_ggsw, batch = 3, 5
+    ggsw = rand_q(g, (n_ggsw, level, k + 1, k + 1, n), P)
+    idx = np.array([1, 2, 0, 5, 1], np.int32)
+    glwe = rand_q(g, (batch, k + 1, n), q)
+    out0 = rand_q(g, (batch, k + 1, n), q)
+    tg = dev(ggsw)
+    pg = M.NttGgswList(pl, tg, base_log, level, M.BNF if bnf else M.SOLINAS)
+    twisted = (n, k, level) == (2048, 1, 1)
+    if twisted:
+        tg.zero_()  # the prepared copy is private on the fused shape
+    ext = M.add_external_product_ntt64_bnf_assign if bnf else M.add_external_product_ntt64_assign
+    cm = M.cmux_ntt64_bnf_assign if bnf else M.cmux_ntt64_assign
+    out = dev(out0)
+    ext(pl, out, pg, dev(glwe), base_log, level)  # shared: GGSW 0
+    want = np.stack([c.ext_product(out0[b].reshape(-1), ggsw[0].reshape(-1), glwe[b].reshape(-1), k, base_log, level,
+                                   bnf=bnf).reshape(k + 1, n) for b in range(batch)])
+    assert np.array_equal(host(out), want)
+    t0, t1 = dev(out0), dev(glwe)
+    cm(pl, t0, t1, pg, base_log, level, ggsw_index=torch.from_numpy(idx).cuda())
+    want0 = out0.copy()
+    for b in range(batch):
+        if idx[b] < n_ggsw:
+            want0[b] = c.cmux(out0[b].reshape(-1), glwe[b].reshape(-1), ggsw[idx[b]].reshape(-1), k, base_log, level,
+                              bnf=bnf).reshape(k + 1, n)
+    assert np.array_equal(host(t0), want0)
+    with pytest.raises(ValueError):  # the list was made for another decomposition
+        ext(pl, out, pg, dev(glwe), base_log + 1, level)

@@ -197,6 +197,41 @@ static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_pla
     }
   }
   plan->twisted = plan->d_twist_f != nullptr;
+  if (plan->goldilocks && logn >= 12 && logn <= MI_SPLIT_MAX_LOGN) {
+    // the split transform (launch_ntt_split): needs the 2048 plan's twisted body and the root tower
+    // psi_N^(N / 2048) = psi_2048 (prime64.rs:166-177), checked here against the tables both plans were built from
+    const mi_ntt64_plan* sub = nullptr;
+    const u64 psi = plan->twid[mi::host::bit_rev(logn, 1)];
+    if (mi_ntt64_plan_cached(2048, p, device, &sub) == MI_OK && sub->twisted &&
+        mi::host::exp_mod(psi, (u64)(n / 2048), p) == sub->twid[mi::host::bit_rev(11, 1)]) {
+      const int t = logn - 11;
+      std::vector<u64> blk(2 * n);
+      for (size_t b = 0; b < ((size_t)1 << t); ++b) {
+        // alpha_b = psi^(2 bitrev_t(b) + 1 - 2^t mod 2N)
+        const u64 e = (2 * (u64)mi::host::bit_rev(t, (unsigned)b) + 1 + 2 * (u64)n - ((u64)1 << t)) % (2 * (u64)n);
+        const u64 a = mi::host::exp_mod(psi, e, p), ai = mi::host::exp_mod(a, p - 2, p);
+        u64 f = 1, g = 1;
+        for (size_t j = 0; j < 2048; ++j) {
+          blk[b * 2048 + j] = f;
+          blk[n + b * 2048 + j] = g;
+          f = mi::host::mul_mod(f, a, p);
+          g = mi::host::mul_mod(g, ai, p);
+        }
+      }
+      if (hipMalloc(&plan->d_split, 2 * n * sizeof(u64)) != hipSuccess) {
+        (void)hipFree(plan->d_twid);
+        (void)hipFree(plan->d_inv_twid);
+        return fail(MI_ERR_OOM, "split-transform table allocation failed");
+      }
+      if (hipMemcpy(plan->d_split, blk.data(), 2 * n * sizeof(u64), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(plan->d_split);
+        (void)hipFree(plan->d_twid);
+        (void)hipFree(plan->d_inv_twid);
+        return fail(MI_ERR_HIP, "split-transform table upload failed");
+      }
+      plan->sub2048 = sub;
+    }
+  }
   *out_plan = plan.release();
   return MI_OK;
 }
@@ -220,6 +255,7 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
     if (plan->d_twid) (void)hipFree(plan->d_twid);
     if (plan->d_inv_twid) (void)hipFree(plan->d_inv_twid);
     if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);  // d_twist_i points into the same allocation
+    if (plan->d_split) (void)hipFree(plan->d_split);
   }
   delete plan;
   return MI_OK;
@@ -293,12 +329,15 @@ static int check_batch(const mi_ntt64_plan* plan, const void* buf, size_t batch,
   return MI_OK;
 }
 
-// Kernel routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan, else the
-// register-window kernels.  One kernel per plan shape; nothing in the environment changes it.
+// Kernel routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan, the split transform (top passes +
+// that kernel on 2048-blocks) for Solinas 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN, else the register-window kernels.  One kernel per plan shape; nothing in the environment changes it.
 static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride,
                                    hipStream_t s) {
   if (plan->twisted)
     return mi::launch_ntt_tw(fwd, buf, batch, stride, fwd ? plan->d_twist_f : plan->d_twist_i, s);
+  if (plan->d_split)
+    return mi::launch_ntt_split(fwd, plan->logn, buf, batch, stride, fwd ? plan->d_twid : plan->d_inv_twid,
+                                plan->split_tables(), s);
   return mi::launch_ntt(fwd, plan->logn, plan->goldilocks, plan->mp, buf, batch, stride,
                         fwd ? plan->d_twid : plan->d_inv_twid, s);
 }
@@ -500,6 +539,15 @@ int mi::capi::check_pbs_shape(const mi_ntt64_plan* plan, int k, int base_log, in
   return MI_OK;
 }
 
+// the split-transform tables of a plan (launch_ntt_split), or NULL: the large-N passes then run the window kernels.
+// Returns a pointer to thread-local storage, valid until the next call on this thread.
+static const mi::SplitTw* split_of(const mi_ntt64_plan* plan) {
+  thread_local mi::SplitTw t;
+  if (!plan->d_split) return nullptr;
+  t = plan->split_tables();
+  return &t;
+}
+
 // the twisted-transform bodies (pbs_tw.hip) cover level 1, base_log <= 31 (BNF and Solinas) on the
 // Solinas N = 2048 plan; every other shape runs the generic kernels (pbs_kernels.hip)
 bool mi::capi::twisted_ext_applies(const mi_ntt64_plan* plan, int variant, int k, int base_log, int level) {
@@ -526,7 +574,8 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
   }
   hipError_t e = plan->logn > 13  // the fused conversion kernel covers N <= 8192
                      ? mi::launch_bsk_to_ntt_large(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width,
-                                                   normalize ? 1 : 0, plan->n_inv, plan->d_twid, (hipStream_t)stream)
+                                                   normalize ? 1 : 0, plan->n_inv, plan->d_twid, (hipStream_t)stream,
+                                                   split_of(plan))
                      : mi::launch_bsk_to_ntt(plan->logn, bsk_ntt, bsk_std, n_polys, in_modulus_width, normalize ? 1 : 0,
                                              plan->n_inv, plan->d_twid, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "bsk conversion launch");
@@ -534,7 +583,7 @@ int mi_bsk_to_ntt64(const mi_ntt64_plan* plan, const uint64_t* bsk_std, uint64_t
 
 static int ext_common(const mi_ntt64_plan* plan, bool cmux, uint64_t* out, uint64_t* in, const uint64_t* ggsw,
                       const uint32_t* gidx, size_t n_ggsw, int k, int base_log, int level, size_t batch, int variant,
-                      void* stream) {
+                      void* stream, bool prepared = false) {
   int st = check_pbs_shape(plan, k, base_log, level, variant);
   if (st != MI_OK) return st;
   if (batch == 0) return MI_OK;
@@ -545,16 +594,84 @@ static int ext_common(const mi_ntt64_plan* plan, bool cmux, uint64_t* out, uint6
   hipError_t e;
   if (twisted_ext_applies(plan, variant, k, base_log, level))
     e = mi::launch_ext_tw(cmux, variant == MI_NTT64_SOLINAS, out, in, ggsw, batch, base_log, plan->d_twist_f,
-                          (hipStream_t)stream, gidx, (uint32_t)n_ggsw);
+                          (hipStream_t)stream, gidx, (uint32_t)n_ggsw, prepared);
   else if (plan->logn >= LARGE_PATH_MIN_LOGN)
     e = mi::launch_ext_product_large(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch,
                                      base_log, plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
-                                     (uint32_t)n_ggsw);
+                                     (uint32_t)n_ggsw, split_of(plan));
   else
     e = mi::launch_ext_product(plan->logn, k, variant == MI_NTT64_BNF, cmux, level, out, in, ggsw, batch, base_log,
                                plan->d_twid, plan->d_inv_twid, plan->n_inv, (hipStream_t)stream, gidx,
                                (uint32_t)n_ggsw);
   return e == hipSuccess ? MI_OK : hip_fail(e, cmux ? "cmux launch" : "external product launch");
+}
+
+int mi_ntt64_ggsw_create(const mi_ntt64_plan* plan, const uint64_t* ggsw_list, size_t n_ggsw, int k, int base_log,
+                         int level, int variant, void* stream, mi_ntt64_ggsw** out) {
+  if (!out) return fail(MI_ERR_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int st = check_pbs_shape(plan, k, base_log, level, variant);
+  if (st != MI_OK) return st;
+  if (!ggsw_list) return fail(MI_ERR_INVALID_ARG, "ggsw_list is NULL");
+  if (n_ggsw == 0 || n_ggsw > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "GGSW count out of range");
+  std::unique_ptr<mi_ntt64_ggsw> g(new (std::nothrow) mi_ntt64_ggsw);
+  if (!g) return fail(MI_ERR_OOM, "host allocation failed");
+  g->plan = plan;
+  g->n_ggsw = n_ggsw;
+  g->k = k;
+  g->base_log = base_log;
+  g->level = level;
+  g->variant = variant;
+  g->ggsw = ggsw_list;
+  if (twisted_ext_applies(plan, variant, k, base_log, level) && mi::ext_tw_reads_w1p()) {
+    const size_t polys = n_ggsw * 4;  // k = 1, level 1: (k + 1)^2 polynomials per GGSW
+    DeviceGuard dg(plan->device);
+    if (hipMalloc(&g->owned, polys * plan->n * sizeof(u64)) != hipSuccess)
+      return fail(MI_ERR_OOM, "GGSW copy allocation failed");
+    hipError_t e = mi::launch_prepare_tw_key(g->owned, ggsw_list, polys, 0, 0, (hipStream_t)stream, true);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    if (e != hipSuccess) {
+      (void)hipFree(g->owned);
+      return hip_fail(e, "GGSW preparation");
+    }
+    g->ggsw = g->owned;
+  }
+  *out = g.release();
+  return MI_OK;
+}
+
+int mi_ntt64_ggsw_destroy(mi_ntt64_ggsw* g) {
+  if (!g) return MI_OK;
+  if (g->owned) {
+    DeviceGuard dg(g->plan->device);
+    (void)hipFree(g->owned);
+  }
+  delete g;
+  return MI_OK;
+}
+
+int mi_ntt64_ggsw_info(const mi_ntt64_ggsw* g, size_t* n_ggsw, int* k, int* base_log, int* level, int* variant) {
+  if (!g) return fail(MI_ERR_INVALID_ARG, "ggsw is NULL");
+  if (n_ggsw) *n_ggsw = g->n_ggsw;
+  if (k) *k = g->k;
+  if (base_log) *base_log = g->base_log;
+  if (level) *level = g->level;
+  if (variant) *variant = g->variant;
+  return MI_OK;
+}
+
+int mi_ext_product_ntt64_prepared_batch(const mi_ntt64_ggsw* g, uint64_t* out_glwe, const uint64_t* in_glwe,
+                                        const uint32_t* ggsw_index, size_t batch, void* stream) {
+  if (!g) return fail(MI_ERR_INVALID_ARG, "ggsw is NULL");
+  return ext_common(g->plan, false, out_glwe, const_cast<uint64_t*>(in_glwe), g->ggsw, ggsw_index,
+                    ggsw_index ? g->n_ggsw : 1, g->k, g->base_log, g->level, batch, g->variant, stream, g->owned != nullptr);
+}
+
+int mi_cmux_ntt64_prepared_batch(const mi_ntt64_ggsw* g, uint64_t* ct0, uint64_t* ct1, const uint32_t* ggsw_index,
+                                 size_t batch, void* stream) {
+  if (!g) return fail(MI_ERR_INVALID_ARG, "ggsw is NULL");
+  return ext_common(g->plan, true, ct0, ct1, g->ggsw, ggsw_index, ggsw_index ? g->n_ggsw : 1, g->k, g->base_log,
+                    g->level, batch, g->variant, stream, g->owned != nullptr);
 }
 
 int mi_ext_product_ntt64_batch(const mi_ntt64_plan* plan, uint64_t* out_glwe, const uint64_t* in_glwe,
@@ -709,7 +826,7 @@ static int pbs_common(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint
   else if (plan->logn >= LARGE_PATH_MIN_LOGN)
     e = mi::launch_pbs_large(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, io,
                              key->bsk, key->n_lwe, batch, key->base_log, plan->d_twid, plan->d_inv_twid,
-                             ms_mode == MI_MS_CENTERED, s);
+                             ms_mode == MI_MS_CENTERED, s, split_of(plan));
   else
     e = mi::launch_pbs(plan->logn, key->k, key->variant == MI_NTT64_BNF, key->level, lwe_out, lwe_in, io, key->bsk, key->n_lwe, batch,
                        key->base_log, plan->d_twid, plan->d_inv_twid, ms_mode == MI_MS_CENTERED, s);

@@ -14,6 +14,9 @@
 using mi::host::u128;
 using mi::host::u64;
 
+// largest log2 N of the split transform (launch_ntt_split): its block-twist tables hold 2 N u64
+constexpr int MI_SPLIT_MAX_LOGN = 20;
+
 struct mi_ntt64_plan {
   size_t n = 0;
   int logn = 0;
@@ -32,6 +35,18 @@ struct mi_ntt64_plan {
   u64* d_twist_f = nullptr;
   u64* d_twist_i = nullptr;
   u64* d_twist_fn = nullptr;  // forward twist rows x N^-1 + the forward lane-pair twiddles (normalising key conversion)
+  // Solinas 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN: the split transform (ntt64_kernels.hip launch_ntt_split): d_split holds
+  // the block twist alpha_b^j then alpha_b^-j (2 N u64); sub2048 is the cached 2048 plan whose body tables it uses
+  u64* d_split = nullptr;
+  const mi_ntt64_plan* sub2048 = nullptr;
+  mi::SplitTw split_tables() const {
+    mi::SplitTw t;
+    t.blk_fwd = d_split;
+    t.blk_inv = d_split + n;
+    t.body_fwd = sub2048->d_twist_f;
+    t.body_inv = sub2048->d_twist_i;
+    return t;
+  }
 };
 
 struct mi_fft64_plan {
@@ -51,6 +66,17 @@ struct mi_fft64_pbs_key {
   double* owned = nullptr;       // device copy made by mi_fft64_pbs_key_load
   size_t n_lwe = 0;
   int k = 1, base_log = 0, level = 0;
+};
+
+// a GGSW list made ready for the external product / CMUX (mi_ntt64_ggsw_create): the fused N = 2048 level-1 bodies read
+// their GGSW in the W1' order (pbs_tw.hip), so for that shape the list is permuted once into a private copy instead of
+// per call; every other shape references the caller's list
+struct mi_ntt64_ggsw {
+  const mi_ntt64_plan* plan = nullptr;
+  size_t n_ggsw = 0;
+  int k = 1, base_log = 0, level = 0, variant = 0;
+  const u64* ggsw = nullptr;  // what the kernels read
+  u64* owned = nullptr;       // the W1'-ordered private copy (or nullptr)
 };
 
 struct mi_pbs_ntt64_key {

@@ -83,9 +83,13 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__
 // left independent: thread j of block b owns the 2^K elements b 2^(logn - S0) + j + i cols (i < 2^K, cols =
 // 2^(logn - S0 - K), coalesced across j), and its local stage s (m = 2^s local groups) reads the table at
 // (2^S0 + b) 2^s + g, the global stage S0 + s's twiddle of the block's group.
-template <int K, bool FWD, class Mod, class IO>
+// TWIST (the split transform, launch_ntt_split): 1 = the forward's last pass multiplies each output element e (index
+// within the polynomial) by twist[e] after its stages; 2 = the inverse's first pass multiplies each input by twist[e]
+// before them.
+template <int K, bool FWD, class Mod, class IO, int TWIST = 0>
 __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn, uint32_t s0,
-                                                      const u64* __restrict__ tw, Mod mod) {
+                                                      const u64* __restrict__ tw, Mod mod,
+                                                      const u64* __restrict__ twist = nullptr) {
   constexpr int R = 1 << K;
   const uint32_t logc = logn - s0 - K;
   const uint64_t cols = (uint64_t)1 << logc;
@@ -93,10 +97,15 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
   if (jg >= ((uint64_t)1 << (logn - K))) return;
   const uint64_t blk = jg >> logc, j = jg & (cols - 1);
   const uint64_t twc = ((uint64_t)1 << s0) + blk;
-  IO* __restrict__ src = data + (uint64_t)blockIdx.y * stride + (blk << (logn - s0)) + j;
+  const uint64_t e0 = (blk << (logn - s0)) + j;  // element index of register 0 within the polynomial
+  IO* __restrict__ src = data + (uint64_t)blockIdx.y * stride + e0;
   u64 x[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = (u64)src[i * cols];
+  if constexpr (TWIST == 2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = mod.mul(x[i], twist[e0 + i * cols]);
+  }
 #pragma unroll
   for (int st = 0; st < K; ++st) {
     const int s = FWD ? st : K - 1 - st;  // stage s has m = 2^s groups, pair distance 2^(K-1-s) in i
@@ -116,6 +125,10 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
         x[i + d] = mod.mul(mod.sub(a, b), wv);
       }
     }
+  }
+  if constexpr (TWIST == 1) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = mod.mul(x[i], twist[e0 + i * cols]);
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
@@ -210,6 +223,71 @@ static hipError_t dispatch(int logn, IO* data, size_t batch, size_t stride, cons
     case 14: return launch_window<14, 4, FWD>(data, batch, stride, tw, mod, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The split transform (ntt64_launch.hpp SplitTw): t = logn - 11 top stages on strided columns with the block twist
+// fused into the forward's last / the inverse's first pass, and the 2048-blocks through the twisted N = 2048 body.
+// Factorisation (checked against the oracle for N = 2^12 ... 2^17, fwd and inv: tests/test_ntt_gpu.py and
+// tools/check_split_factorisation.py): after the reference's first t stages, block b of 2048 coefficients holds the
+// residue mod X^2048 - zeta_b; with alpha_b = psi_N^(2 bitrev_t(b) + 1 - 2^t) (alpha_b^2048 = -zeta_b) the substitution
+// X = alpha_b Y makes it the negacyclic (mod Y^2048 + 1) transform of the 2048 plan, whose root is psi_N^(N / 2048)
+// (the Solinas root tower), in the same bit-reversed output order.
+template <int K, bool FWD, int TWIST>
+static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn, int s0, const u64* tw,
+                                const u64* twist, hipStream_t s) {
+  const uint64_t threads = (uint64_t)1 << (logn - K);
+  const dim3 grid((unsigned)((threads + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST>), grid, dim3(256), 0, s, data, (uint64_t)stride,
+                     (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist);
+  return hipGetLastError();
+}
+
+template <bool FWD, int TWIST>
+static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int logn, int s0, const u64* tw,
+                         const u64* twist, hipStream_t s) {
+  switch (kk) {
+    case 1: return launch_top_tw<1, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    case 2: return launch_top_tw<2, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    case 3: return launch_top_tw<3, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    case 4: return launch_top_tw<4, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    case 5: return launch_top_tw<5, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,
+                            const SplitTw& st, hipStream_t s) {
+  const int t = logn - 11;
+  if (t < 1 || t > 10) return hipErrorInvalidValue;
+  if (batch == 0) return hipSuccess;
+  // the top passes put polynomials on grid.y (<= 65535 per launch); passes of <= 5 stages, balanced
+  const int passes = (t + 4) / 5;
+  int ks[2] = {(t + passes - 1) / passes, t - (t + passes - 1) / passes};
+  auto tops = [&](u64* d, size_t nb) -> hipError_t {
+    for (int q = 0; q < passes; ++q) {
+      const int pi = fwd ? q : passes - 1 - q;
+      const int s0 = pi == 0 ? 0 : ks[0], kk = ks[pi];
+      const bool twist_here = fwd ? (pi == passes - 1) : (q == 0);
+      hipError_t e;
+      if (!twist_here) e = fwd ? top_tw<true, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s)
+                               : top_tw<false, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s);
+      else e = fwd ? top_tw<true, 1>(kk, d, nb, stride, logn, s0, tw, st.blk_fwd, s)
+                   : top_tw<false, 2>(kk, d, nb, stride, logn, s0, tw, st.blk_inv, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  auto all_tops = [&]() -> hipError_t {
+    for (size_t b0 = 0; b0 < batch; b0 += 65535) {
+      const hipError_t e = tops(data + b0 * stride, std::min<size_t>(65535, batch - b0));
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  hipError_t e = fwd ? all_tops() : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t);
+  if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t) : all_tops();
+  return e;
 }
 
 hipError_t launch_ntt(bool fwd, int logn, bool goldilocks, const MontParams& mp, u64* data, size_t batch,

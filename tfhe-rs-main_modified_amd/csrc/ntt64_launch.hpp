@@ -28,7 +28,21 @@ hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, con
 hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
                               hipStream_t s);
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
-                         hipStream_t s);
+                         hipStream_t s, int sub_log = 0);
+
+// The split transform of a Solinas plan with 2^12 <= N <= 2^17 (ntt64_kernels.hip): the reference's first
+// t = log2 N - 11 stages as passes over strided columns, the block twist (element j of 2048-block b times alpha_b^j,
+// alpha_b = psi_N^(2 bitrev_t(b) + 1 - 2^t)) fused into the last forward / first inverse pass, and every 2048-block
+// through the twisted N = 2048 body (ntt64_tw.hip) of the cached 2048-point Solinas plan.  Device tables:
+struct SplitTw {
+  const uint64_t* blk_fwd = nullptr;   // N: alpha_b^j at b 2048 + j
+  const uint64_t* blk_inv = nullptr;   // N: alpha_b^-j
+  const uint64_t* body_fwd = nullptr;  // the 2048 plan's d_twist_f (forward body tables)
+  const uint64_t* body_inv = nullptr;  // the 2048 plan's d_twist_i (inverse body tables)
+};
+// tw = the N plan's forward (fwd) or inverse (inv) twiddle table; data: batch polynomials `stride` u64 apart
+hipError_t launch_ntt_split(bool fwd, int logn, uint64_t* data, size_t batch, size_t stride, const uint64_t* tw,
+                            const SplitTw& st, hipStream_t s);
 
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
 hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,
@@ -100,19 +114,24 @@ hipError_t launch_sample_extract(uint64_t* out, const uint64_t* glwe, int logn, 
 // passes per CMUX step over chunks of ciphertexts whose accumulators live in HBM; same arguments as above
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
                             const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
-                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s);
+                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s,
+                            const SplitTw* split = nullptr);
 hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
                                     const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
                                     const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx,
-                                    uint32_t n_ggsw);
+                                    uint32_t n_ggsw, const SplitTw* split = nullptr);
 hipError_t launch_bsk_to_ntt_large(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
-                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s);
+                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s,
+                                   const SplitTw* split = nullptr);
 // BNF, level 1, base_log <= 31, on the twisted transform; tab = plan twist tables [fwd | inverse]
 // BNF level-1 external product (cmux=false: out += GGSW . glwe) / CMUX (cmux=true: ct0 = out,
 // ct1 = glwe) on the twisted transform; the GGSW is the Raw NTT key (N^-1 via the third table)
+// prepared: the GGSWs are already in the bodies' read order (ext_tw_reads_w1p(): mi_ntt64_ggsw_create permuted them)
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                          int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx = nullptr,
-                         uint32_t n_ggsw = 1);
+                         uint32_t n_ggsw = 1, bool prepared = false);
+// whether the external-product / CMUX bodies read their GGSW in the W1' order (a prepared list is permuted once)
+bool ext_tw_reads_w1p();
 // Solinas PBS on the twisted engine: switched = pre-switched mask + body values in [0, 2N)
 // the twisted bodies' key order (pbs_tw.hip): per N = 2048 polynomial, positions permuted to the W1' step layout
 // when the blind-rotation (ext: external-product) body reads that order, times c when scale (dst may equal src)

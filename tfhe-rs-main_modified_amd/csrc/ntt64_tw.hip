@@ -49,17 +49,20 @@ static constexpr int WAVE_LDS2 = 1088;  // u64: max(32 x 34, 16 x 66)
 template <bool FWD>
 constexpr uint32_t tw_waves() { return FWD ? 1u : 4u; }
 
+// sub_log > 0 (the split transform of N = 2^(11 + sub_log), ntt64_kernels.hip launch_ntt_split): unit `poly` is block
+// poly & (2^sub_log - 1) of polynomial poly >> sub_log, 2048 contiguous coefficients at that block's offset
 template <bool FWD>
 __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* __restrict__ data, uint32_t batch,
                                                                           uint64_t stride,
-                                                                          const u64* __restrict__ twist) {
+                                                                          const u64* __restrict__ twist,
+                                                                          uint32_t sub_log) {
   constexpr uint32_t W = tw_waves<FWD>();
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t poly = blockIdx.x * W + wv;
   if (poly >= batch) return;
-  u64* p = data + (uint64_t)poly * stride;
+  u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
   const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
@@ -130,20 +133,23 @@ hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys
   return hipGetLastError();
 }
 
-hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist, hipStream_t s) {
+hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist, hipStream_t s,
+                         int sub_log) {
   if (batch == 0) return hipSuccess;
-  constexpr size_t CHUNK = size_t(1) << 30;  // grid.x limit 2^31 - 1 (a whole chunk is 16 TiB of polynomials)
-  for (size_t off = 0; off < batch; off += CHUNK) {
-    const uint32_t n = (uint32_t)std::min(CHUNK, batch - off);
-    uint64_t* d = data + off * stride;
+  // grid.x limit 2^31 - 1 (a whole chunk is 16 TiB of polynomials); a chunk of units holds whole polynomials
+  const size_t CHUNK = (size_t(1) << 30) >> sub_log << sub_log;
+  const size_t units = batch << sub_log;
+  for (size_t off = 0; off < units; off += CHUNK) {
+    const uint32_t n = (uint32_t)std::min(CHUNK, units - off);
+    uint64_t* d = data + (off >> sub_log) * stride;
     if (fwd) {
       constexpr uint32_t W = tw::tw_waves<true>();
       hipLaunchKernelGGL((tw::ntt_tw_body_kernel<true>), dim3((n + W - 1) / W), dim3(64 * W), 0, s, d, n,
-                         (uint64_t)stride, twist);
+                         (uint64_t)stride, twist, (uint32_t)sub_log);
     } else {
       constexpr uint32_t W = tw::tw_waves<false>();
       hipLaunchKernelGGL((tw::ntt_tw_body_kernel<false>), dim3((n + W - 1) / W), dim3(64 * W), 0, s, d, n,
-                         (uint64_t)stride, twist);
+                         (uint64_t)stride, twist, (uint32_t)sub_log);
     }
   }
   return hipGetLastError();

@@ -236,6 +236,13 @@ inline unsigned blocks_for(uint64_t total) {
   return (unsigned)std::min<uint64_t>(b, 65536);
 }
 
+// the plan's transform: the split engine (launch_ntt_split) when the plan has one, else the register-window passes
+inline hipError_t ntt_large(bool fwd, int logn, u64* d, size_t batch, size_t stride, const u64* tw,
+                            const SplitTw* split, hipStream_t s) {
+  if (split) return launch_ntt_split(fwd, logn, d, batch, stride, tw, *split, s);
+  return launch_ntt(fwd, logn, true, MontParams{}, d, batch, stride, tw, s);
+}
+
 // ciphertexts per chunk: the digits, products and accumulators of one chunk stay below ~1 GiB of scratch
 inline size_t chunk_for(const LargeShape& sh, size_t batch) {
   const size_t per_item = ((size_t)sh.level + 2) * (sh.k + 1) * sh.n * sizeof(u64);
@@ -246,7 +253,8 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
                             const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
-                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s) {
+                            const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s,
+                            const SplitTw* split) {
   using namespace pbs;
   if (batch == 0) return hipSuccess;
   const LargeShape sh{(uint32_t)logn, 1u << logn, (uint32_t)k, (uint32_t)level, base_log};
@@ -277,11 +285,11 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
       else
         hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
                            (uint32_t)n_lwe, i, nb, sh);
-      e = launch_ntt(true, logn, true, mp, digits, (size_t)nb * level * (k + 1), sh.n, tw, s);
+      e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
       if (e != hipSuccess) break;
       hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, bsk + (size_t)i * ggsw_len, nb,
                          sh, (u64)0, (const uint32_t*)nullptr, 1u);
-      e = launch_ntt(false, logn, true, mp, y, (size_t)nb * (k + 1), sh.n, itw, s);
+      e = ntt_large(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, split, s);
       if (e != hipSuccess) break;
       if (bnf)
         hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, y, nb, sh,
@@ -325,13 +333,14 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
 // convert_standard_lwe_bootstrap_key_to_ntt64 (lwe_bootstrap_key_conversion.rs:294-365) at large N: modulus switch
 // into dst, the large-N forward transform in place, optional normalisation (NttLweBootstrapKeyOption::Normalize)
 hipError_t launch_bsk_to_ntt_large(int logn, uint64_t* dst, const uint64_t* src, size_t n_polys, unsigned in_width,
-                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s) {
+                                   int normalize, uint64_t n_inv, const uint64_t* tw, hipStream_t s,
+                                   const SplitTw* split) {
   using namespace pbs;
   if (n_polys == 0) return hipSuccess;
   const uint64_t count = (uint64_t)n_polys << logn;
   hipLaunchKernelGGL(large_modswitch_to_prime, dim3(blocks_for(count)), dim3(256), 0, s, dst, src, count, in_width);
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = launch_ntt(true, logn, true, MontParams{}, dst, n_polys, (size_t)1 << logn, tw, s);
+  if (e == hipSuccess) e = ntt_large(true, logn, dst, n_polys, (size_t)1 << logn, tw, split, s);
   if (e == hipSuccess && normalize) e = launch_scale(dst, dst, count, n_inv, s);
   return e;
 }
@@ -339,7 +348,7 @@ hipError_t launch_bsk_to_ntt_large(int logn, uint64_t* dst, const uint64_t* src,
 hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int level, uint64_t* out, uint64_t* glwe,
                                     const uint64_t* ggsw, size_t batch, int base_log, const uint64_t* tw,
                                     const uint64_t* itw, uint64_t n_inv, hipStream_t s, const uint32_t* gidx,
-                                    uint32_t n_ggsw) {
+                                    uint32_t n_ggsw, const SplitTw* split) {
   using namespace pbs;
   if (batch == 0) return hipSuccess;
   const LargeShape sh{(uint32_t)logn, 1u << logn, (uint32_t)k, (uint32_t)level, base_log};
@@ -365,12 +374,12 @@ hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int le
       if (cmux) MI_LARGE_DEC(false, true); else MI_LARGE_DEC(false, false);
     }
 #undef MI_LARGE_DEC
-    e = launch_ntt(true, logn, true, mp, digits, (size_t)nb * level * (k + 1), sh.n, tw, s);
+    e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
     if (e != hipSuccess) break;
     // BNF GGSWs are the reference's Raw NTT keys: the product is normalised here (ntt64_bnf_pbs.rs:670)
     hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, ggsw, nb, sh,
                        bnf ? (u64)n_inv : (u64)0, gi, gi ? n_ggsw : 1u);
-    e = launch_ntt(false, logn, true, mp, y, (size_t)nb * (k + 1), sh.n, itw, s);
+    e = ntt_large(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, split, s);
     if (e != hipSuccess) break;
     if (bnf)
       hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, s, o, y, nb, sh, gi, n_ggsw);

@@ -301,12 +301,15 @@ hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_po
   return hipGetLastError();
 }
 
+bool ext_tw_reads_w1p() { return MI_EXT_W1P != 0; }
+
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
-                         int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw) {
+                         int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw,
+                         bool prepared) {
   if (batch == 0) return hipSuccess;
   if (base_log < 1 || base_log > 31) return hipErrorInvalidValue;
-  u64* perm = nullptr;  // MI_EXT_W1P: the caller's GGSWs in the body's W1' order, stream-ordered scratch
-  if (MI_EXT_W1P) {
+  u64* perm = nullptr;  // MI_EXT_W1P on a raw list: the caller's GGSWs in the body's W1' order, in pooled scratch
+  if (MI_EXT_W1P && !prepared) {
     hipError_t e = mi::scratch_alloc((void**)&perm, (size_t)n_ggsw * 4 * pbstw::N * sizeof(u64), s);
     if (e != hipSuccess) return e;
     e = launch_prepare_tw_key(perm, ggsw, (size_t)n_ggsw * 4, 0, 0, s, true);

@@ -67,6 +67,12 @@ _SIGS = {
     "mi_ntt_bsk_write": (_int, [_vp, _vp, _int, _vp, _sz]),
     "mi_pbs_ntt64_key_load": (_int, [_vp, _vp, _sz, _int, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_pbs_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_ntt64_ggsw_create": (_int, [_vp, _vp, _sz, _int, _int, _int, _int, _vp, ctypes.POINTER(_vp)]),
+    "mi_ntt64_ggsw_destroy": (_int, [_vp]),
+    "mi_ntt64_ggsw_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int),
+                                  ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "mi_ext_product_ntt64_prepared_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+    "mi_cmux_ntt64_prepared_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
     "mi_pbs_ntt64_batch_lut_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _sz, _int, _vp]),
     "mi_blind_rotate_ntt64_batch": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
     "mi_sample_extract_batch": (_int, [_vp, _vp, _sz, _int, _sz, _sz, _sz, _sz, _u64, _int, _vp]),

@@ -75,7 +75,53 @@ def convert_standard_lwe_bootstrap_key_to_ntt64(plan, input_bsk, output_bsk, nor
                                 _stream(output_bsk)))
 
 
+class NttGgswList:
+    """GGSWs made ready for repeated external products / CMUXes (``mi_ntt64_ggsw``): the reference's
+    NttGgswCiphertextList (entities/ntt_ggsw_ciphertext_list.rs) held in the NTT domain.  ``ggsw`` is the device tensor
+    (n_ggsw, level, k+1, k+1, N) (or one GGSW (level, k+1, k+1, N)).  The fused N = 2048, k = 1, level-1 bodies read a
+    private copy permuted once into their order (made on the tensor's current stream); other shapes reference the
+    tensor (keep it alive).  Pass it wherever a ``ggsw`` tensor is accepted below."""
+
+    def __init__(self, plan, ggsw, base_log: int, level: int, variant: int):
+        n = plan.ntt_size()
+        if ggsw.dim() == 4:
+            ggsw = ggsw.unsqueeze(0)
+        k = int(ggsw.shape[2]) - 1 if ggsw.dim() == 5 else 0
+        if ggsw.dim() != 5 or tuple(ggsw.shape[1:]) != (level, k + 1, k + 1, n):
+            raise ValueError(f"assertion failed: ggsw shape {tuple(ggsw.shape)} != (n_ggsw, {level}, k + 1, k + 1, {n})")
+        self.plan, self.ggsw, self.base_log, self.level, self.variant = plan, ggsw, base_log, level, variant
+        self.glwe_dimension, self.n_ggsw = k, int(ggsw.shape[0])
+        h = ctypes.c_void_p()
+        check(lib().mi_ntt64_ggsw_create(plan.handle, _dev(ggsw, "ggsw"), self.n_ggsw, k, base_log, level, variant,
+                                         _stream(ggsw), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().mi_ntt64_ggsw_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+def _ext_prepared(pg, out, glwe, base_log, level, variant, cmux, ggsw_index):
+    n = pg.plan.ntt_size()
+    k = pg.glwe_dimension
+    if (base_log, level, variant) != (pg.base_log, pg.level, pg.variant):
+        raise ValueError("the prepared GGSW list was made for another decomposition / variant")
+    b = _glwe_batch(out, k, n, "out")
+    if glwe.shape != out.shape:
+        raise ValueError(f"assertion failed: glwe shape {tuple(glwe.shape)} != out shape {tuple(out.shape)}")
+    idx = None if ggsw_index is None else _index(ggsw_index, b, out.device, "ggsw_index")
+    fn = lib().mi_cmux_ntt64_prepared_batch if cmux else lib().mi_ext_product_ntt64_prepared_batch
+    check(fn(pg._h, _dev(out, "out"), _dev(glwe, "glwe"), idx, b, _stream(out)))
+
+
 def _ext(plan, out, ggsw, glwe, base_log, level, variant, cmux, ggsw_index=None):
+    if isinstance(ggsw, NttGgswList):
+        return _ext_prepared(ggsw, out, glwe, base_log, level, variant, cmux, ggsw_index)
     n = plan.ntt_size()
     if out.dim() < 2:
         raise ValueError(f"assertion failed: out shape {tuple(out.shape)} != (..., k + 1, {n})")
@@ -328,7 +374,7 @@ def scratch_bytes(device: int = -1) -> int:
 
 
 __all__ = [
-    "SOLINAS", "BNF", "MS_STANDARD", "MS_CENTERED", "MS_PRE_SWITCHED", "MiError", "NttBootstrapKey",
+    "SOLINAS", "BNF", "MS_STANDARD", "MS_CENTERED", "MS_PRE_SWITCHED", "MiError", "NttBootstrapKey", "NttGgswList",
     "convert_standard_lwe_bootstrap_key_to_ntt64", "add_external_product_ntt64_assign",
     "add_external_product_ntt64_bnf_assign", "cmux_ntt64_assign", "cmux_ntt64_bnf_assign",
     "programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized",
