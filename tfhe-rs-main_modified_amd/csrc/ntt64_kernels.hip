@@ -23,6 +23,7 @@
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "ntt64_regs.hpp"
+#include "pbs_device.hpp"
 
 namespace mi {
 
@@ -86,10 +87,14 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__
 // TWIST (the split transform, launch_ntt_split): 1 = the forward's last pass multiplies each output element e (index
 // within the polynomial) by twist[e] after its stages; 2 = the inverse's first pass multiplies each input by twist[e]
 // before them.
-template <int K, bool FWD, class Mod, class IO, int TWIST = 0>
+// ACC (the inverse's last pass inside the large-N blind rotation, pbs_large.hip): instead of storing the output x,
+// acc[e] += modswitch_{p -> 2^64}(x) (1, BNF, ntt64.rs:184-197 + wrapping add) or acc[e] = acc[e] + x mod p (2,
+// Solinas, ntt64.rs:244-266), acc laid out like data (stride apart per polynomial)
+template <int K, bool FWD, class Mod, class IO, int TWIST = 0, int ACC = 0>
 __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn, uint32_t s0,
                                                       const u64* __restrict__ tw, Mod mod,
-                                                      const u64* __restrict__ twist = nullptr) {
+                                                      const u64* __restrict__ twist = nullptr,
+                                                      u64* __restrict__ acc = nullptr) {
   constexpr int R = 1 << K;
   const uint32_t logc = logn - s0 - K;
   const uint64_t cols = (uint64_t)1 << logc;
@@ -129,6 +134,13 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
   if constexpr (TWIST == 1) {
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = mod.mul(x[i], twist[e0 + i * cols]);
+  }
+  if constexpr (ACC != 0) {
+    u64* __restrict__ a = acc + (uint64_t)blockIdx.y * stride + e0;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      a[i * cols] = ACC == 1 ? a[i * cols] + pbs::modswitch_prime_to_native(x[i]) : pbs::add_custom(a[i * cols], x[i]);
+    return;
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
@@ -233,31 +245,32 @@ static hipError_t dispatch(int logn, IO* data, size_t batch, size_t stride, cons
 // residue mod X^2048 - zeta_b; with alpha_b = psi_N^(2 bitrev_t(b) + 1 - 2^t) (alpha_b^2048 = -zeta_b) the substitution
 // X = alpha_b Y makes it the negacyclic (mod Y^2048 + 1) transform of the 2048 plan, whose root is psi_N^(N / 2048)
 // (the Solinas root tower), in the same bit-reversed output order.
-template <int K, bool FWD, int TWIST>
+template <int K, bool FWD, int TWIST, int ACC>
 static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn, int s0, const u64* tw,
-                                const u64* twist, hipStream_t s) {
+                                const u64* twist, u64* acc, hipStream_t s) {
   const uint64_t threads = (uint64_t)1 << (logn - K);
   const dim3 grid((unsigned)((threads + 255) / 256), (unsigned)batch);
-  hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST>), grid, dim3(256), 0, s, data, (uint64_t)stride,
-                     (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist);
+  hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC>), grid, dim3(256), 0, s, data,
+                     (uint64_t)stride, (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist, acc);
   return hipGetLastError();
 }
 
-template <bool FWD, int TWIST>
+template <bool FWD, int TWIST, int ACC = 0>
 static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int logn, int s0, const u64* tw,
-                         const u64* twist, hipStream_t s) {
+                         const u64* twist, hipStream_t s, u64* acc = nullptr) {
   switch (kk) {
-    case 1: return launch_top_tw<1, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
-    case 2: return launch_top_tw<2, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
-    case 3: return launch_top_tw<3, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
-    case 4: return launch_top_tw<4, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
-    case 5: return launch_top_tw<5, FWD, TWIST>(data, batch, stride, logn, s0, tw, twist, s);
+    case 1: return launch_top_tw<1, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
+    case 2: return launch_top_tw<2, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
+    case 3: return launch_top_tw<3, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
+    case 4: return launch_top_tw<4, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
+    case 5: return launch_top_tw<5, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,
-                            const SplitTw& st, hipStream_t s) {
+                            const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first) {
+  if ((acc && fwd) || (skip_first && !fwd)) return hipErrorInvalidValue;  // acc: inverse only; skip_first: forward only
   const int t = logn - 11;
   if (t < 1 || t > 10) return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
@@ -265,13 +278,21 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
   const int passes = (t + 4) / 5;
   int ks[2] = {(t + passes - 1) / passes, t - (t + passes - 1) / passes};
   auto tops = [&](u64* d, size_t nb) -> hipError_t {
-    for (int q = 0; q < passes; ++q) {
+    for (int q = skip_first ? 1 : 0; q < passes; ++q) {
       const int pi = fwd ? q : passes - 1 - q;
       const int s0 = pi == 0 ? 0 : ks[0], kk = ks[pi];
       const bool twist_here = fwd ? (pi == passes - 1) : (q == 0);
+      // the inverse's last pass (q = passes - 1) accumulates into acc instead of storing, when asked
+      u64* a = (!fwd && acc && q == passes - 1) ? acc + (d - data) : nullptr;
       hipError_t e;
-      if (!twist_here) e = fwd ? top_tw<true, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s)
-                               : top_tw<false, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s);
+      if (a && twist_here)
+        e = acc_mode == 1 ? top_tw<false, 2, 1>(kk, d, nb, stride, logn, s0, tw, st.blk_inv, s, a)
+                          : top_tw<false, 2, 2>(kk, d, nb, stride, logn, s0, tw, st.blk_inv, s, a);
+      else if (a)
+        e = acc_mode == 1 ? top_tw<false, 0, 1>(kk, d, nb, stride, logn, s0, tw, nullptr, s, a)
+                          : top_tw<false, 0, 2>(kk, d, nb, stride, logn, s0, tw, nullptr, s, a);
+      else if (!twist_here) e = fwd ? top_tw<true, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s)
+                                    : top_tw<false, 0>(kk, d, nb, stride, logn, s0, tw, nullptr, s);
       else e = fwd ? top_tw<true, 1>(kk, d, nb, stride, logn, s0, tw, st.blk_fwd, s)
                    : top_tw<false, 2>(kk, d, nb, stride, logn, s0, tw, st.blk_inv, s);
       if (e != hipSuccess) return e;

@@ -41,8 +41,18 @@ struct SplitTw {
   const uint64_t* body_inv = nullptr;  // the 2048 plan's d_twist_i (inverse body tables)
 };
 // tw = the N plan's forward (fwd) or inverse (inv) twiddle table; data: batch polynomials `stride` u64 apart
+// acc (inverse only): the last top pass accumulates its output into acc (same layout as data) instead of storing it,
+// acc_mode 1 = BNF (acc += modswitch p -> 2^64), 2 = Solinas (acc = acc + x mod p); data then holds an intermediate
 hipError_t launch_ntt_split(bool fwd, int logn, uint64_t* data, size_t batch, size_t stride, const uint64_t* tw,
-                            const SplitTw& st, hipStream_t s);
+                            const SplitTw& st, hipStream_t s, uint64_t* acc = nullptr, int acc_mode = 0,
+                            bool skip_first = false);
+// how launch_ntt_split cuts the t = log2 N - 11 top stages into passes: the first pass's stage count (the forward's
+// first pass, s0 = 0) and whether it is the only one (then it carries the block twist)
+inline void split_first_pass(int logn, int* k0, bool* only) {
+  const int t = logn - 11, passes = (t + 4) / 5;
+  *k0 = (t + passes - 1) / passes;
+  *only = passes == 1;
+}
 
 // op: 0 normalize (out *= c), 1 mul_assign_normalize (out = out*b*c), 2 mul_accumulate (out += a*b[*c])
 hipError_t launch_pointwise(int op, bool goldilocks, const MontParams& mp, uint64_t* out, const uint64_t* a,

@@ -113,6 +113,107 @@ __global__ __launch_bounds__(256) void large_rotate_decompose(u64* __restrict__ 
   }
 }
 
+// Step i of the blind rotation fused with the forward's first pass of the split transform (launch_ntt_split): thread j
+// of GLWE polynomial (b, c) forms ct1 = X^a acc - acc at the 2^K coefficients e = j + r cols (cols = N / 2^K), decomposes
+// them, and for each level li runs the first K top CT stages of the transform (s0 = 0: twiddle tw[m + g]) on the
+// digits in registers (ONLY: the pass is the last one, so the block twist follows), storing digit polynomial (b, li, c)
+// in the layout of large_rotate_decompose.  Replaces that pass plus the transform's first pass: acc is read once and
+// the digits written once (not written, read and written again).
+template <int K, bool BNF, bool ONLY>
+__global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits, const u64* __restrict__ acc,
+                                                        const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
+                                                        LargeShape sh, const u64* __restrict__ tw,
+                                                        const u64* __restrict__ twist) {
+  constexpr int R = 1 << K;
+  const Goldilocks gl;
+  const uint64_t cols = (uint64_t)sh.n >> K;
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  const uint32_t bc = blockIdx.y, b = bc / (sh.k + 1), c = bc % (sh.k + 1);
+  const unsigned log_mod = sh.logn + 1;
+  const u64 a_raw = lwe_in[(uint64_t)b * (n_lwe + 1) + step];
+  u64 a = 0;
+  if (BNF) a = modulus_switch(a_raw, log_mod);
+  else if (a_raw != 0) a = ms_non_native(a_raw, log_mod);
+  const uint32_t full = (uint32_t)(a >> sh.logn) & 1u, rem = (uint32_t)(a & (sh.n - 1));
+  const u64* ap = acc + (uint64_t)bc * sh.n;
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
+  u64* dp = digits + (uint64_t)b * sh.level * per + (uint64_t)c * sh.n + j;
+  u64 st[R];
+  bool sg[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t e = (uint32_t)(j + r * cols);
+    u64 v = ap[(e - rem) & (sh.n - 1)];  // X^a acc: new[e] = old[(e - rem) % N], negated for e < rem
+    if (full ^ (e < rem)) v = neg_q<BNF>(v);
+    const u64 x = BNF ? v - ap[e] : sub_custom(v, ap[e]);
+    if (BNF) {
+      st[r] = decomp_init_native(x, sh.base_log, (int)sh.level);
+      sg[r] = false;
+    } else {  // iter.rs:623-745, as decompose_store
+      const unsigned shift = 64u - (unsigned)(sh.base_log * (int)sh.level);
+      sg[r] = x >= P / 2 + 1;
+      st[r] = closest_abs_nonnative(sg[r] ? P - x : x, sh.base_log, (int)sh.level) >> shift;
+    }
+  }
+  for (uint32_t li = 0; li < sh.level; ++li) {
+    u64 x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u64 term = decompose_one_level(sh.base_log, st[r]);
+      if (!BNF && sg[r]) term = (u64)0 - term;
+      x[r] = ((int64_t)term < 0) ? term + P : term;
+    }
+#pragma unroll
+    for (int s = 0; s < K; ++s) {  // stage s: m = 2^s groups, pair distance 2^(K-1-s) in r
+      const int m = 1 << s, d = 1 << (K - 1 - s);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r & d) continue;
+        const u64 z = gl.mul(x[r + d], tw[m + (r >> (K - s))]);
+        const u64 u = x[r];
+        x[r] = gl.add(u, z);
+        x[r + d] = gl.sub(u, z);
+      }
+    }
+    u64* o = dp + (uint64_t)li * per;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      u64 v = x[r];
+      if (ONLY) v = gl.mul(v, twist[j + r * cols]);
+      o[r * cols] = v;
+    }
+  }
+}
+
+template <int K, bool BNF>
+static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, const u64* lwe_in, uint32_t n_lwe,
+                                    uint32_t step, uint32_t nb, const LargeShape& sh, const u64* tw, const u64* twist,
+                                    hipStream_t s) {
+  const dim3 grid((unsigned)((((uint64_t)sh.n >> K) + 255) / 256), nb * (sh.k + 1));
+  if (only)
+    hipLaunchKernelGGL((large_rotdec_top<K, BNF, true>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
+                       tw, twist);
+  else
+    hipLaunchKernelGGL((large_rotdec_top<K, BNF, false>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
+                       tw, twist);
+  return hipGetLastError();
+}
+
+template <bool BNF>
+static hipError_t rotdec_top(int k0, bool only, u64* digits, const u64* acc, const u64* lwe_in, uint32_t n_lwe,
+                             uint32_t step, uint32_t nb, const LargeShape& sh, const u64* tw, const u64* twist,
+                             hipStream_t s) {
+  switch (k0) {
+    case 1: return rotdec_top_launch<1, BNF>(only, digits, acc, lwe_in, n_lwe, step, nb, sh, tw, twist, s);
+    case 2: return rotdec_top_launch<2, BNF>(only, digits, acc, lwe_in, n_lwe, step, nb, sh, tw, twist, s);
+    case 3: return rotdec_top_launch<3, BNF>(only, digits, acc, lwe_in, n_lwe, step, nb, sh, tw, twist, s);
+    case 4: return rotdec_top_launch<4, BNF>(only, digits, acc, lwe_in, n_lwe, step, nb, sh, tw, twist, s);
+    case 5: return rotdec_top_launch<5, BNF>(only, digits, acc, lwe_in, n_lwe, step, nb, sh, tw, twist, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // external product / CMUX input: CMUX first writes glwe -= out back (ct1 = ct1 - ct0), then both decompose glwe.
 // gidx: item b is skipped (nothing written anywhere) when gidx[b] >= n_ggsw
 template <bool BNF, bool CMUX>
@@ -278,17 +379,32 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
     else
       hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, io, (uint64_t)b0, in,
                          (uint32_t)n_lwe, nb, sh);
+    int k0 = 0;
+    bool only = false;
+    if (split) split_first_pass(logn, &k0, &only);
     for (uint32_t i = 0; i < n_lwe && e == hipSuccess; ++i) {
-      if (bnf)
-        hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
-                           (uint32_t)n_lwe, i, nb, sh);
-      else
-        hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
-                           (uint32_t)n_lwe, i, nb, sh);
-      e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
-      if (e != hipSuccess) break;
+      if (split) {  // rotation + decomposition + the transform's first pass in one kernel, then the rest of the transform
+        e = bnf ? rotdec_top<true>(k0, only, digits, acc, in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, s)
+                : rotdec_top<false>(k0, only, digits, acc, in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, s);
+        if (e == hipSuccess)
+          e = launch_ntt_split(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, *split, s, nullptr, 0, true);
+        if (e != hipSuccess) break;
+      } else {
+        if (bnf)
+          hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
+                             (uint32_t)n_lwe, i, nb, sh);
+        else
+          hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
+                             (uint32_t)n_lwe, i, nb, sh);
+        e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
+        if (e != hipSuccess) break;
+      }
       hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, bsk + (size_t)i * ggsw_len, nb,
                          sh, (u64)0, (const uint32_t*)nullptr, 1u);
+      if (split) {  // the inverse's last pass accumulates into acc itself (launch_ntt_split acc_mode)
+        e = launch_ntt_split(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, *split, s, acc, bnf ? 1 : 2);
+        continue;
+      }
       e = ntt_large(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, split, s);
       if (e != hipSuccess) break;
       if (bnf)
