@@ -233,7 +233,7 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uin
 /* The same bootstrap with one LUT per item (the CUDA backend's lut_indexes, backends/tfhe-cuda-backend/cuda/include/
  * pbs/programmable_bootstrap.h:41; the shortint many-LUT / per-block LUT batches): lut_list holds n_lut GLWEs
  * ((k+1) N u64 each), item b uses GLWE lut_index[b] (device u32 array of `batch` entries).  An item whose index is
- * >= n_lut is left untouched (lwe_out[b] not written). */
+ * >= n_lut is left untouched (lwe_out[b] not written).  lut_index NULL: item b uses GLWE b (n_lut >= batch). */
 int mi_pbs_ntt64_batch_lut_indexed(const mi_pbs_ntt64_key *key, uint64_t *lwe_out, const uint64_t *lwe_in,
                                    const uint64_t *lut_list, const uint32_t *lut_index, size_t n_lut, size_t batch,
                                    int ms_mode, void *stream);
@@ -376,6 +376,18 @@ int mi_fft64_pbs_key_destroy(mi_fft64_pbs_key *key);
 int mi_fft64_pbs_key_info(const mi_fft64_pbs_key *key, size_t *n_lwe, int *k, int *base_log, int *level);
 int mi_fft64_pbs_batch(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uint64_t *lwe_in, const uint64_t *lut,
                        size_t batch, int ms_mode, void *stream);
+/* One accumulator per item: lut_index NULL = batch_programmable_bootstrap_lwe_ciphertext_mem_optimized
+ * (fft64_pbs.rs:1055-1127: item b bootstraps through GLWE b of lut_list, n_lut >= batch); otherwise item b uses GLWE
+ * lut_index[b] (device u32) and an index >= n_lut leaves lwe_out[b] untouched. */
+int mi_fft64_pbs_batch_lut_indexed(const mi_fft64_pbs_key *key, uint64_t *lwe_out, const uint64_t *lwe_in,
+                                   const uint64_t *lut_list, const uint32_t *lut_index, size_t n_lut, size_t batch,
+                                   int ms_mode, void *stream);
+/* blind_rotate_assign[_mem_optimized] (fft64_pbs.rs:186-250; FourierLweBootstrapKey::blind_rotate_assign,
+ * fft_impl/fft64/crypto/bootstrap.rs:294-381), batched and in place: acc_glwe[b] ((k+1) N u64) is divided by
+ * X^ms(body) and rotated through the CMUX loop over lwe_in[b].  ms_mode as mi_pbs_ntt64_batch (the reference's
+ * ModulusSwitchedLweCiphertext input: MI_MS_PRE_SWITCHED, or the native LWE switched on the device). */
+int mi_fft64_blind_rotate_batch(const mi_fft64_pbs_key *key, uint64_t *acc_glwe, const uint64_t *lwe_in, size_t batch,
+                                int ms_mode, void *stream);
 /* The multi-GPU bootstrap of mi_pbs_ntt64_multi_gpu[_ordered] (same sharding, active-GPU count, scatter / gather and
  * producer-stream ordering) on the f64-FFT path: keys[i] (bound to a plan of devices[i], same shape) and luts[i] on
  * devices[i], lwe_in / lwe_out on devices[0]. */

@@ -847,12 +847,14 @@ int mi_pbs_ntt64_batch(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uin
 int mi_pbs_ntt64_batch_lut_indexed(const mi_pbs_ntt64_key* key, uint64_t* lwe_out, const uint64_t* lwe_in,
                                    const uint64_t* lut_list, const uint32_t* lut_index, size_t n_lut, size_t batch,
                                    int ms_mode, void* stream) {
-  if (batch && (!lut_index || !lwe_out)) return fail(MI_ERR_INVALID_ARG, "lut_index / lwe_out is NULL");
+  if (batch && !lwe_out) return fail(MI_ERR_INVALID_ARG, "lwe_out is NULL");
   if (n_lut == 0 || n_lut > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "n_lut out of range");
+  if (!lut_index && n_lut < batch) return fail(MI_ERR_INVALID_ARG, "per-item LUTs: n_lut < batch");
   mi::PbsIo io;
   io.lut = lut_list;
   io.lut_idx = lut_index;
   io.n_lut = (uint32_t)n_lut;
+  io.per_item = lut_index ? 0 : 1;  // no index array: item b uses GLWE b
   return pbs_common(key, lwe_out, lwe_in, io, batch, ms_mode, stream);
 }
 

@@ -483,21 +483,57 @@ int mi_fft64_pbs_key_info(const mi_fft64_pbs_key* key, size_t* n_lwe, int* k, in
   return MI_OK;
 }
 
-int mi_fft64_pbs_batch(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
-                       size_t batch, int ms_mode, void* stream) {
+}  // extern "C"
+
+static int fft_pbs_common(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const mi::PbsIo& io,
+                          size_t batch, int ms_mode, void* stream) {
   if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
   if (ms_mode < MI_MS_STANDARD || ms_mode > MI_MS_PRE_SWITCHED) return fail(MI_ERR_INVALID_ARG, "unknown ms_mode");
   if (batch == 0) return MI_OK;
-  if (!lwe_out || !lwe_in || !lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if ((!lwe_out && !io.glwe_out) || !lwe_in || !io.lut) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (batch > 0x7FFFFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
   DeviceGuard g(key->plan->device);
   const mi_fft64_plan* plan = key->plan;
   const hipError_t e =
-      plan->generic ? mi::launch_fftg_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
+      plan->generic ? mi::launch_fftg_pbs(key->k, lwe_out, lwe_in, io, key->fbsk, key->n_lwe, batch, key->base_log,
                                           key->level, ms_mode, plan->gtables, (hipStream_t)stream)
-                    : mi::launch_fft64_pbs(key->k, lwe_out, lwe_in, lut, key->fbsk, key->n_lwe, batch, key->base_log,
+                    : mi::launch_fft64_pbs(key->k, lwe_out, lwe_in, io, key->fbsk, key->n_lwe, batch, key->base_log,
                                            key->level, ms_mode, plan->tables, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "fft64 pbs launch");
+}
+
+extern "C" {
+
+int mi_fft64_pbs_batch(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uint64_t* lwe_in, const uint64_t* lut,
+                       size_t batch, int ms_mode, void* stream) {
+  if (batch && !lwe_out) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  mi::PbsIo io;
+  io.lut = lut;
+  return fft_pbs_common(key, lwe_out, lwe_in, io, batch, ms_mode, stream);
+}
+
+int mi_fft64_pbs_batch_lut_indexed(const mi_fft64_pbs_key* key, uint64_t* lwe_out, const uint64_t* lwe_in,
+                                   const uint64_t* lut_list, const uint32_t* lut_index, size_t n_lut, size_t batch,
+                                   int ms_mode, void* stream) {
+  if (batch && !lwe_out) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (n_lut == 0 || n_lut > 0xFFFFFFFFull) return fail(MI_ERR_INVALID_ARG, "n_lut out of range");
+  if (!lut_index && n_lut < batch) return fail(MI_ERR_INVALID_ARG, "per-item LUTs: n_lut < batch");
+  mi::PbsIo io;
+  io.lut = lut_list;
+  io.lut_idx = lut_index;
+  io.n_lut = (uint32_t)n_lut;
+  io.per_item = lut_index ? 0 : 1;
+  return fft_pbs_common(key, lwe_out, lwe_in, io, batch, ms_mode, stream);
+}
+
+int mi_fft64_blind_rotate_batch(const mi_fft64_pbs_key* key, uint64_t* acc_glwe, const uint64_t* lwe_in, size_t batch,
+                                int ms_mode, void* stream) {
+  if (batch && !acc_glwe) return fail(MI_ERR_INVALID_ARG, "acc_glwe is NULL");
+  mi::PbsIo io;
+  io.lut = acc_glwe;
+  io.per_item = 1;
+  io.glwe_out = acc_glwe;
+  return fft_pbs_common(key, nullptr, lwe_in, io, batch, ms_mode, stream);
 }
 
 }  // extern "C"

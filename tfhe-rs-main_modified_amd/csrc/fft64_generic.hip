@@ -430,7 +430,9 @@ __global__ __launch_bounds__(256) void reorder_kernel(cplx* __restrict__ out, co
 
 // ---- blind-rotation bookkeeping ----------------------------------------------------------------------------
 // acc[b] = LUT / X^body (polynomial_wrapping_monic_monomial_div, bootstrap.rs:499-507)
-__global__ __launch_bounds__(256) void init_acc_kernel(u64* __restrict__ acc, const u64* __restrict__ lut,
+// acc[b] = the item's LUT / X^body (io: pbs_io.hpp; item b of the chunk is item b0 + b of the batch; a skipped item,
+// LUT index out of range, gets a zero accumulator and is not written back)
+__global__ __launch_bounds__(256) void init_acc_kernel(u64* __restrict__ acc, PbsIo io, uint64_t b0,
                                                        const u64* __restrict__ lwe, const u64* __restrict__ corr,
                                                        uint32_t n_lwe, uint32_t batch, uint32_t logn, uint32_t kp1,
                                                        int ms_mode) {
@@ -439,6 +441,11 @@ __global__ __launch_bounds__(256) void init_acc_kernel(u64* __restrict__ acc, co
   for (uint64_t i = gs_start(); i < per * batch; i += gs_stride()) {
     const uint64_t b = i / per, ce = i % per;
     const uint32_t c = (uint32_t)(ce >> logn), m = (uint32_t)ce & (nn - 1);
+    const u64* lut = io.lut_for(b0 + b, per);
+    if (!lut) {
+      acc[i] = 0;
+      continue;
+    }
     const u64 bv = lwe[b * (n_lwe + 1) + n_lwe];
     const u64 body = ms_mode == 2 ? (bv & (2 * nn - 1)) : modulus_switch(bv + (corr ? corr[b] : 0), logn + 1);
     const uint32_t full = (uint32_t)(body >> logn) & 1u, rem = (uint32_t)body & (nn - 1);
@@ -457,16 +464,28 @@ __global__ __launch_bounds__(256) void body_correction_kernel(u64* __restrict__ 
   if (threadIdx.x == 0) corr[blockIdx.x] = v;
 }
 
-// extract_lwe_sample_from_glwe_ciphertext, nth = 0: out[c N] = A_c[0], out[c N + j] = -A_c[N - j], out[k N] = B[0]
+// extract_lwe_sample_from_glwe_ciphertext, nth = 0: out[c N] = A_c[0], out[c N + j] = -A_c[N - j], out[k N] = B[0];
+// items whose LUT index is out of range (io.lut_idx) are not written
 __global__ __launch_bounds__(256) void extract_kernel(u64* __restrict__ out, const u64* __restrict__ acc,
-                                                      uint32_t batch, uint32_t logn, uint32_t k) {
+                                                      uint32_t batch, uint32_t logn, uint32_t k, PbsIo io, uint64_t b0) {
   const uint32_t nn = 1u << logn;
   const uint64_t per_out = ((uint64_t)k << logn) + 1, per = (uint64_t)(k + 1) << logn;
   for (uint64_t i = gs_start(); i < per_out * batch; i += gs_stride()) {
     const uint64_t b = i / per_out, o = i % per_out;
+    if (io.lut_idx && !io.lut_for(b0 + b, per)) continue;
     const uint32_t c = (uint32_t)(o >> logn), j = (uint32_t)o & (nn - 1);
     const u64 v = acc[b * per + ((uint64_t)c << logn) + (j ? nn - j : 0u)];
     out[i] = (c == k || j == 0) ? v : (u64)0 - v;
+  }
+}
+
+// blind_rotate_assign (fft64_pbs.rs:186-250): the rotated accumulators of a chunk into io.glwe_out (skipped items kept)
+__global__ __launch_bounds__(256) void store_glwe_kernel(const u64* __restrict__ acc, uint32_t batch, uint64_t per,
+                                                         PbsIo io, uint64_t b0) {
+  for (uint64_t i = gs_start(); i < per * batch; i += gs_stride()) {
+    const uint64_t b = i / per;
+    if (!io.lut_for(b0 + b, per)) continue;
+    io.glwe_out[b0 * per + i] = acc[i];
   }
 }
 
@@ -674,7 +693,7 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
   return e != hipSuccess ? e : ef;
 }
 
-hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftGenTables& t,
                            hipStream_t s) {
   using namespace fft::gen;
@@ -699,8 +718,8 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
     const uint64_t* in = lwe_in + b0 * (n_lwe + 1);
     if (ms_mode == 1)
       hipLaunchKernelGGL(body_correction_kernel, dim3(nb), dim3(256), 0, s, corr, in, (uint32_t)n_lwe, g.logn + 1);
-    hipLaunchKernelGGL(init_acc_kernel, dim3(blocks_for((uint64_t)nb * per)), dim3(256), 0, s, acc, lut, in,
-                       ms_mode == 1 ? (const uint64_t*)corr : nullptr, (uint32_t)n_lwe, nb, g.logn, kp1, ms_mode);
+    hipLaunchKernelGGL(init_acc_kernel, dim3(blocks_for((uint64_t)nb * per)), dim3(256), 0, s, acc, io, (uint64_t)b0,
+                       in, ms_mode == 1 ? (const uint64_t*)corr : nullptr, (uint32_t)n_lwe, nb, g.logn, kp1, ms_mode);
     if ((e = hipGetLastError()) != hipSuccess) break;
     for (uint32_t i = 0; i < (uint32_t)n_lwe && e == hipSuccess; ++i) {
       e = forward(g, RotDigitSrc{acc, in, g.tw, g.logn, kp1, lv, (uint32_t)n_lwe, i, base_log, ms_mode}, d,
@@ -710,9 +729,15 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const u
                   (uint64_t)nb * kp1, s);
     }
     if (e != hipSuccess) break;
-    const uint64_t outs = (uint64_t)nb * (((uint64_t)k << g.logn) + 1);
-    hipLaunchKernelGGL(extract_kernel, dim3(blocks_for(outs)), dim3(256), 0, s, out + b0 * (((size_t)k << g.logn) + 1),
-                       (const uint64_t*)acc, nb, g.logn, (uint32_t)k);
+    if (io.glwe_out) {
+      hipLaunchKernelGGL(store_glwe_kernel, dim3(blocks_for((uint64_t)nb * per)), dim3(256), 0, s,
+                         (const uint64_t*)acc, nb, (uint64_t)per, io, (uint64_t)b0);
+    } else {
+      const uint64_t outs = (uint64_t)nb * (((uint64_t)k << g.logn) + 1);
+      hipLaunchKernelGGL(extract_kernel, dim3(blocks_for(outs)), dim3(256), 0, s,
+                         out + b0 * (((size_t)k << g.logn) + 1), (const uint64_t*)acc, nb, g.logn, (uint32_t)k, io,
+                         (uint64_t)b0);
+    }
     e = hipGetLastError();
   }
   const hipError_t ef = mi::scratch_free(scratch, s);

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "pbs_io.hpp"
+
 namespace mi {
 
 // Device twiddle tables of an N = 2048 plan (complex values as interleaved re, im doubles):
@@ -25,7 +27,7 @@ hipError_t launch_fft64_bwd_torus(uint64_t* std_, const double* fourier, size_t 
                                   hipStream_t s);
 hipError_t launch_fft64_ext_product(int k, bool cmux, uint64_t* out, uint64_t* glwe, const double* ggsw, size_t batch,
                                     int base_log, int level, const FftTables& t, hipStream_t s);
-hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
                             size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftTables& t,
                             hipStream_t s);
 // Fourier order interchange of `polys` polynomials (N / 2 complex each; in place allowed): to_standard = engine
@@ -51,7 +53,7 @@ hipError_t launch_fftg_reorder(double* out, const double* in, size_t polys, bool
                                hipStream_t s);
 hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* glwe, const double* ggsw, size_t batch,
                                    int base_log, int level, const FftGenTables& t, hipStream_t s);
-hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftGenTables& t,
                            hipStream_t s);
 // engine position -> frequency of a generic plan (fft64_generic.hip: k1 C + p holds k1 + R bitrev_C(p))

@@ -569,9 +569,12 @@ constexpr int CT_FAST = 4;
 // With several ciphertexts per workgroup a mask element that switches to 0 is not skipped (the reference
 // skips it, bootstrap.rs:336): its CMUX difference is the zero polynomial, whose digits, transforms and
 // products are exactly 0, so the accumulator is unchanged bit for bit either way.
+// io (pbs_io.hpp): the item's LUT (shared, per item or indexed) and the output form (LWE of sample 0, or the rotated
+// GLWE itself: blind_rotate_assign, fft64_pbs.rs:186-250).  An item whose LUT index is out of range runs on LUT 0 like a
+// padding item and writes nothing.
 template <int K, bool L1, int CT>
-__device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
-                                         const u64* __restrict__ lut, const cplx* __restrict__ fbsk, uint32_t n_lwe,
+__device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in, const PbsIo& io,
+                                         const cplx* __restrict__ fbsk, uint32_t n_lwe,
                                          uint32_t batch, int base_log, int level, int ms_mode, const Tables& tb,
                                          Wg<K, CT>& wg) {
   constexpr int TG = 64 * (K + 1);
@@ -580,8 +583,10 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ct = wave / (K + 1), w = wave % (K + 1);
   const uint32_t b0 = blockIdx.x * CT + ct;
-  const bool valid = b0 < batch;  // every wave takes part in the barriers
-  const uint32_t b = valid ? b0 : batch - 1;
+  const uint32_t b = b0 < batch ? b0 : batch - 1;
+  const u64* lut = io.lut_for(b, (uint64_t)(K + 1) * N);
+  const bool valid = b0 < batch && lut;  // every wave takes part in the barriers
+  if (!lut) lut = io.lut;
   const u64* lwe = lwe_in + (size_t)b * (n_lwe + 1);
   const size_t ggsw_len = (size_t)level * (K + 1) * (K + 1) * M;
   cplx* pair = wg.bufs + ct * (K + 1) * BUF;
@@ -644,6 +649,14 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
                            lane, ps);
   }
 
+  if (io.glwe_out) {  // the rotated accumulator (the LUT was divided by X^body before the loop)
+    if (valid) {
+      u64* g = io.glwe_out + ((size_t)b * (K + 1) + w) * N;
+#pragma unroll
+      for (int r = 0; r < NPL; ++r) g[lane + 64 * r] = acc[r];
+    }
+    return;
+  }
   // extract_lwe_sample_from_glwe_ciphertext (glwe_sample_extraction.rs:89-160), nth = 0
   u64* out = lwe_out + (size_t)b * (K * N + 1);
   if (w < K) {
@@ -666,17 +679,17 @@ __device__ __forceinline__ void pbs_body(u64* __restrict__ lwe_out, const u64* _
 
 template <int K, bool L1>
 __global__ __launch_bounds__(64 * (K + 1)) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
-                                                           const u64* __restrict__ lut, const cplx* __restrict__ fbsk,
+                                                           PbsIo io, const cplx* __restrict__ fbsk,
                                                            uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                            int ms_mode, Tables tb) {
   __shared__ Wg<K, 1> wg;
-  pbs_body<K, L1, 1>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
+  pbs_body<K, L1, 1>(lwe_out, lwe_in, io, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
 }
 __global__ __launch_bounds__(128 * CT_FAST) __attribute__((amdgpu_waves_per_eu(2))) void pbs_kernel_k1l1(
-    u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in, const u64* __restrict__ lut,
+    u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in, PbsIo io,
     const cplx* __restrict__ fbsk, uint32_t n_lwe, uint32_t batch, int base_log, int level, int ms_mode, Tables tb) {
   __shared__ Wg<1, CT_FAST> wg;
-  pbs_body<1, true, CT_FAST>(lwe_out, lwe_in, lut, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
+  pbs_body<1, true, CT_FAST>(lwe_out, lwe_in, io, fbsk, n_lwe, batch, base_log, level, ms_mode, tb, wg);
 }
 
 }  // namespace fft
@@ -742,7 +755,7 @@ hipError_t launch_fft64_ext_product(int k, bool cmux, uint64_t* out, uint64_t* g
 }
 
 template <int K, bool L1>
-static hipError_t pbs_one(uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const fft::cplx* g, size_t n_lwe,
+static hipError_t pbs_one(uint64_t* out, const uint64_t* lwe_in, const PbsIo& lut, const fft::cplx* g, size_t n_lwe,
                           size_t batch, int base_log, int level, int ms_mode, const FftTables& t, hipStream_t s) {
   if (K == 1 && L1)
     hipLaunchKernelGGL(fft::pbs_kernel_k1l1, dim3((unsigned)((batch + fft::CT_FAST - 1) / fft::CT_FAST)),
@@ -754,7 +767,7 @@ static hipError_t pbs_one(uint64_t* out, const uint64_t* lwe_in, const uint64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const uint64_t* lut, const double* fbsk,
+hipError_t launch_fft64_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& lut, const double* fbsk,
                             size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftTables& t,
                             hipStream_t s) {
   if (batch == 0) return hipSuccess;

@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "pbs_io.hpp"
+
 namespace mi {
 
 // Montgomery parameters for a generic odd prime (R = 2^64).
@@ -76,29 +78,6 @@ hipError_t launch_fill_uniform(uint64_t* out, size_t count, uint64_t seed, uint6
 }  // namespace mi
 
 namespace mi {
-
-// Where a bootstrap's accumulator starts and what it leaves (every PBS engine: pbs_tw.hip, pbs_kernels.hip,
-// pbs_large.hip).  The accumulator of item b starts as GLWE `lut_for(b)` of the list `lut` (glwe_len u64 each):
-//   lut_idx != NULL : GLWE lut_idx[b]; an index >= n_lut skips the item (nothing read, nothing written)
-//   per_item != 0   : GLWE b (blind_rotate_ntt64[_bnf]_assign: every item rotates its own accumulator)
-//   otherwise       : GLWE 0, shared by the batch (programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext)
-// glwe_out != NULL: the rotated accumulator of item b is stored to glwe_out[b] ((k+1) N u64; it may be the LUT list
-// itself, in place) instead of extracting sample 0 into lwe_out[b].  Item indices are global to the caller's batch.
-struct PbsIo {
-  const uint64_t* lut = nullptr;
-  const uint32_t* lut_idx = nullptr;
-  uint32_t n_lut = 1;
-  uint32_t per_item = 0;
-  uint64_t* glwe_out = nullptr;
-  __host__ __device__ const uint64_t* lut_for(uint64_t b, uint64_t glwe_len) const {
-    uint64_t i = per_item ? b : 0;
-    if (lut_idx) {
-      i = lut_idx[b];
-      if (i >= n_lut) return nullptr;
-    }
-    return lut + i * glwe_len;
-  }
-};
 
 // pbs_kernels.hip — Goldilocks, the shapes of mi::capi::check_pbs_shape up to N = 8192, any level count (callers
 // validate the shape; other shapes return hipErrorInvalidValue).

@@ -109,6 +109,8 @@ _SIGS = {
     "mi_fft64_pbs_key_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_int), ctypes.POINTER(_int),
                                      ctypes.POINTER(_int)]),
     "mi_fft64_pbs_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _int, _vp]),
+    "mi_fft64_pbs_batch_lut_indexed": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, _sz, _int, _vp]),
+    "mi_fft64_blind_rotate_batch": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
     "mi_fft64_bsk_serialized_size": (_int, [_sz, _sz, _int, _int, _int, ctypes.POINTER(_sz)]),
     "mi_fft64_pbs_key_load": (_int, [_vp, _vp, _sz, _int, _vp, ctypes.POINTER(_vp)]),
     "mi_fft64_pbs_key_write": (_int, [_vp, _int, _vp, _sz, _vp]),

@@ -7,6 +7,8 @@ Names follow the reference (paths relative to /root/reference/tfhe/src/core_cryp
 * ``convert_standard_lwe_bootstrap_key_to_fourier``  algorithms/lwe_bootstrap_key_conversion.rs:20-43
 * ``add_external_product_assign`` / ``cmux_assign``  algorithms/lwe_programmable_bootstrapping/fft64_pbs.rs:270-330, 510-560
 * ``FourierLweBootstrapKey``, ``programmable_bootstrap_lwe_ciphertext``  fft64_pbs.rs:924-1060
+* ``batch_programmable_bootstrap_lwe_ciphertext`` (one accumulator per input), ``blind_rotate_assign``
+                                                     fft64_pbs.rs:1055-1127, 186-250
 * ``Fft.to_standard_order`` / ``from_standard_order``  the serialised (natural) Fourier order of
   tfhe-fft/src/unordered.rs:943-1020; ``FourierLweBootstrapKey.serialize`` / ``deserialize``: the reference's
   bytes of the key (``fourier_bsk_format``)
@@ -224,21 +226,65 @@ class FourierLweBootstrapKey:
         return cls(fbsk, info["decomposition_base_log"], info["decomposition_level_count"], fft)
 
 
-def programmable_bootstrap_lwe_ciphertext(lwe_in, lwe_out, accumulator, key: FourierLweBootstrapKey,
-                                          ms_mode: int = MS_STANDARD) -> None:
-    """Batched f64-FFT PBS of native-modulus LWEs (fft64_pbs.rs:924-1060)."""
+def _lwe_batch(key, lwe_in):
     n_in = key.input_lwe_dimension + 1
     if lwe_in.shape[-1] != n_in:
         raise ValueError(f"assertion failed: input lwe size {lwe_in.shape[-1]} != {n_in}")
-    batch = lwe_in.numel() // n_in
+    return lwe_in.numel() // n_in
+
+
+def programmable_bootstrap_lwe_ciphertext(lwe_in, lwe_out, accumulator, key: FourierLweBootstrapKey,
+                                          ms_mode: int = MS_STANDARD, lut_index=None) -> None:
+    """Batched f64-FFT PBS of native-modulus LWEs (fft64_pbs.rs:924-1060).  ``accumulator`` (k+1, N) is shared; with
+    ``lut_index`` (int32 device tensor, one entry per item) it is a list (n_lut, k+1, N) and item b bootstraps through
+    ``accumulator[lut_index[b]]`` (an out-of-range index leaves ``lwe_out[b]`` untouched)."""
+    from .ntt64_pbs import _index
+    batch = _lwe_batch(key, lwe_in)
     if lwe_out.shape[-1] != key.output_lwe_size() or lwe_out.numel() // key.output_lwe_size() != batch:
         raise ValueError(f"assertion failed: output lwe shape {tuple(lwe_out.shape)}")
-    if tuple(accumulator.shape) != (key.glwe_dimension + 1, key.polynomial_size):
-        raise ValueError(f"assertion failed: accumulator shape {tuple(accumulator.shape)}")
-    check(lib().mi_fft64_pbs_batch(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
-                                   _dev(accumulator, "accumulator"), batch, ms_mode, _stream(lwe_out)))
+    glwe = (key.glwe_dimension + 1, key.polynomial_size)
+    if lut_index is None:
+        if tuple(accumulator.shape) != glwe:
+            raise ValueError(f"assertion failed: accumulator shape {tuple(accumulator.shape)}")
+        check(lib().mi_fft64_pbs_batch(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                       _dev(accumulator, "accumulator"), batch, ms_mode, _stream(lwe_out)))
+        return
+    if accumulator.dim() != 3 or tuple(accumulator.shape[1:]) != glwe:
+        raise ValueError(f"assertion failed: accumulator list shape {tuple(accumulator.shape)} != (n_lut, *{glwe})")
+    check(lib().mi_fft64_pbs_batch_lut_indexed(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                               _dev(accumulator, "accumulator"),
+                                               _index(lut_index, batch, lwe_in.device, "lut_index"),
+                                               int(accumulator.shape[0]), batch, ms_mode, _stream(lwe_out)))
+
+
+def batch_programmable_bootstrap_lwe_ciphertext(lwe_in, lwe_out, accumulators, key: FourierLweBootstrapKey,
+                                                ms_mode: int = MS_STANDARD) -> None:
+    """batch_programmable_bootstrap_lwe_ciphertext_mem_optimized (fft64_pbs.rs:1055-1127): one accumulator per input
+    (``accumulators``: (batch, k+1, N))."""
+    batch = _lwe_batch(key, lwe_in)
+    glwe = (key.glwe_dimension + 1, key.polynomial_size)
+    if lwe_out.shape[-1] != key.output_lwe_size() or lwe_out.numel() // key.output_lwe_size() != batch:
+        raise ValueError(f"assertion failed: output lwe shape {tuple(lwe_out.shape)}")
+    if accumulators.dim() != 3 or tuple(accumulators.shape) != (batch, *glwe):
+        raise ValueError(f"assertion failed: accumulator list shape {tuple(accumulators.shape)} != ({batch}, *{glwe})")
+    check(lib().mi_fft64_pbs_batch_lut_indexed(key._h, _dev(lwe_out, "lwe_out"), _dev(lwe_in, "lwe_in"),
+                                               _dev(accumulators, "accumulators"), None, batch, batch, ms_mode,
+                                               _stream(lwe_out)))
+
+
+def blind_rotate_assign(msed_input, lut, key: FourierLweBootstrapKey, ms_mode: int = MS_PRE_SWITCHED) -> None:
+    """blind_rotate_assign (fft64_pbs.rs:186-250), batched and in place: lut (batch, k+1, N), every item rotated by its
+    own input; ``MS_PRE_SWITCHED`` (default) takes the ModulusSwitchedLweCiphertext values, ``MS_STANDARD`` /
+    ``MS_CENTERED`` the native LWE switched on the device."""
+    batch = _lwe_batch(key, msed_input)
+    glwe = (key.glwe_dimension + 1, key.polynomial_size)
+    if lut.dim() < 2 or tuple(lut.shape[-2:]) != glwe or lut.numel() != batch * glwe[0] * glwe[1]:
+        raise ValueError(f"assertion failed: lut shape {tuple(lut.shape)} != ({batch}, *{glwe})")
+    check(lib().mi_fft64_blind_rotate_batch(key._h, _dev(lut, "lut"), _dev(msed_input, "msed_input"), batch, ms_mode,
+                                            _stream(lut)))
 
 
 __all__ = ["Fft", "FourierLweBootstrapKey", "convert_standard_lwe_bootstrap_key_to_fourier",
            "add_external_product_assign", "cmux_assign", "programmable_bootstrap_lwe_ciphertext",
+           "batch_programmable_bootstrap_lwe_ciphertext", "blind_rotate_assign",
            "MS_STANDARD", "MS_CENTERED", "MS_PRE_SWITCHED"]

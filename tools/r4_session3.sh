@@ -6,3 +6,4 @@ step pytest_split 900 python -u -m pytest tests/test_ntt_gpu.py tests/test_pbs_l
 step split_probe_new 300 python -u tools/split_probe.py 20 || exit 1
 step split_probe_r3 300 python -u tools/split_probe.py --lib ab/oldlib/libtfhe_ntt_amd.so 20 || exit 1
 step shape_probe 600 python -u tools/shape_probe.py message_3_carry_3 message_4_carry_4 || exit 1
+step occupancy 300 tools/occupancy_probe 8192 || exit 1
