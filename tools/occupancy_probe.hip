@@ -28,7 +28,7 @@ static constexpr int WAVE_LDS2 = 1088;
     }                                                                           \
   } while (0)
 
-// W waves per workgroup (the library: forward 1, inverse 4); dynamic LDS pads the workgroup to throttle residency
+// W waves per workgroup; dynamic LDS pads the workgroup to throttle residency
 template <bool FWD, int W>
 __global__ __launch_bounds__(64 * W) void body_kernel(u64* __restrict__ data, uint32_t batch,
                                                       const u64* __restrict__ twist) {
@@ -91,15 +91,16 @@ int main(int argc, char** argv) {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipLaunchKernelGGL(fill, dim3(32), dim3(256), 0, s, twist, (size_t)8192, 11ull);
   hipLaunchKernelGGL(fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, data, n, 7ull);
-  CK(hipFuncSetAttribute((const void*)body_kernel<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-  CK(hipFuncSetAttribute((const void*)body_kernel<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+  // both directions with one-wave workgroups here (the library's inverse uses four: 2.4 % faster at full residency),
+  // so every residency target is reachable under the 64 KiB per-workgroup LDS limit
+  CK(hipFuncSetAttribute((const void*)body_kernel<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 56 * 1024));
+  CK(hipFuncSetAttribute((const void*)body_kernel<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 56 * 1024));
   const int occ[] = {4, 3, 2, 1};
   auto run = [&](bool fwd, int o) {
     if (fwd)
       hipLaunchKernelGGL((body_kernel<true, 1>), dim3(batch), dim3(64), pad_for(o, 1), s, data, batch, twist);
     else
-      hipLaunchKernelGGL((body_kernel<false, 4>), dim3((batch + 3) / 4), dim3(256), pad_for(o, 4), s, data, batch,
-                         twist);
+      hipLaunchKernelGGL((body_kernel<false, 1>), dim3(batch), dim3(64), pad_for(o, 1), s, data, batch, twist);
   };
   for (int it = 0; it < 20000; ++it) run(it & 1, 4);  // the clock settles under load
   CK(hipStreamSynchronize(s));
@@ -127,7 +128,7 @@ int main(int argc, char** argv) {
     std::sort(f.begin(), f.end());
     std::sort(v.begin(), v.end());
     printf("{\"waves_per_simd\": %d, \"pad_fwd_B\": %zu, \"pad_inv_B\": %zu, \"fwd_us_median\": %.2f, "
-           "\"inv_us_median\": %.2f}\n", o, pad_for(o, 1), pad_for(o, 4), f[R / 2], v[R / 2]);
+           "\"inv_us_median\": %.2f}\n", o, pad_for(o, 1), pad_for(o, 1), f[R / 2], v[R / 2]);
   }
   return 0;
 }
