@@ -799,6 +799,71 @@ def cpu_baseline_ks(seconds: float):
                       f"lwe_keyswitch.rs:137-227, OpenMP {threads} threads"}
 
 
+def bench_default_stream(eng, torch, dev, work):
+    """the entry points that take device scratch (the Solinas PBS's modulus-switch pre-pass, the keyswitch
+    digits, the shape-generic f64 engine) called on torch's default stream — the legacy null stream — against the
+    same calls on a created stream.  Small batches, so the per-call host cost shows: `enqueue_us` is the host time
+    per call with the calls back to back (a host-blocking sync inside a call would show here), `us_per_call` the
+    time per call to the final synchronize.  Before r4 every null-stream call synchronised and freed its scratch."""
+    M, KS, F = eng.ntt64_pbs, eng.lwe_keyswitch, eng.fft64
+    batch, n_lwe, R = 4, PBS_N_LWE, 200
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    bsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 90, SOLINAS_P)
+    skey = M.NttBootstrapKey(plan, bsk, PBS_BASE_LOG, PBS_LEVEL, M.SOLINAS)
+    del bsk
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 91, SOLINAS_P)
+    lwe = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lwe, SEED + 92, SOLINAS_P)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+    ksk = torch.empty((KS_IN, KS_LEVEL, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ksk, SEED + 93, 0)
+    kkey = KS.LweKeyswitchKey(ksk, KS_BASE_LOG, KS_LEVEL)
+    del ksk
+    big = torch.empty((batch, KS_IN + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(big, SEED + 94, 0)
+    small = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    n_g, nl_g = 1024, 64  # the shape-generic f64 engine (N != 2048)
+    fft = F.Fft(n_g, dev.index)
+    std = torch.empty((nl_g, 2, 2, 2, n_g), dtype=torch.int64, device=dev)
+    eng.fill_uniform(std, SEED + 95, 0)
+    fbsk = torch.empty((nl_g, 2, 2, 2, n_g // 2, 2), dtype=torch.float64, device=dev)
+    F.convert_standard_lwe_bootstrap_key_to_fourier(std, fbsk, fft)
+    del std
+    fkey = F.FourierLweBootstrapKey(fbsk, 12, 2, fft)
+    flut = torch.empty((2, n_g), dtype=torch.int64, device=dev)
+    eng.fill_uniform(flut, SEED + 96, 0)
+    flwe = torch.empty((batch, nl_g + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(flwe, SEED + 97, 0)
+    fout = torch.empty((batch, n_g + 1), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    cases = {
+        "pbs_solinas_n2048": lambda: M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(lwe, out, lut, skey),
+        "keyswitch_2048_to_918": lambda: KS.keyswitch_lwe_ciphertext(kkey, big, small),
+        "pbs_fft_generic_n1024": lambda: F.programmable_bootstrap_lwe_ciphertext(flwe, fout, flut, fkey),
+    }
+    rows = {}
+    for name, run in cases.items():
+        row = {}
+        for sname, stream in (("default_stream", torch.cuda.default_stream(dev)), ("created_stream", work)):
+            with torch.cuda.stream(stream):
+                for _ in range(5):
+                    run()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(R):
+                    run()
+                t_enq = time.perf_counter() - t0
+                torch.cuda.synchronize()
+                t_all = time.perf_counter() - t0
+            row[sname] = {"enqueue_us": t_enq / R * 1e6, "us_per_call": t_all / R * 1e6}
+        rows[name] = row
+    del skey, kkey, fkey
+    return {"note": f"{R} back-to-back calls at batch {batch} per case and stream (null stream = torch's default)",
+            "cases": rows}
+
+
 def bench_host_path(eng, torch):
     """Config 1 plumbing and VERDICT r2 item 6: the per-polynomial host form of Plan::fwd + Plan::inv
     (`mi_ntt64_fwd_host` / `_inv_host`: copy in, transform, copy out on a pooled private stream, the drop-in for
@@ -1071,6 +1136,8 @@ def main():
     }
     if rank == 0 and world == 1:
         out["host_path"] = bench_host_path(eng, torch)
+        if not args.no_pbs:
+            out["default_stream"] = bench_default_stream(eng, torch, dev, work)
     # the driver keeps only the tail of stdout: the bulky legs first, configs 3 and 4 (external product, PBS) last
     for name in LEG_ORDER:
         if name in legs:

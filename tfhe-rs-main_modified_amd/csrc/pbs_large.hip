@@ -262,6 +262,81 @@ __global__ __launch_bounds__(256) void large_mac(u64* __restrict__ y, const u64*
   }
 }
 
+// The same product with every output column of an item in one thread (k + 1 = KP1 columns): each digit is read once
+// instead of k + 1 times (the digits are (level + 1) / 2 of the step's HBM bytes at k = 1), and the level (k + 1)
+// terms of a column are summed as 128-bit products with one reduction at the end (2^128 = -2^32 mod p).  Grid:
+// x over the coefficient, y over the item.
+template <int KP1>
+__global__ __launch_bounds__(256) void large_mac_cols(u64* __restrict__ y, const u64* __restrict__ digits,
+                                                      const u64* __restrict__ ggsw_list, uint32_t batch,
+                                                      LargeShape sh, u64 n_inv, const uint32_t* __restrict__ gidx,
+                                                      uint32_t n_ggsw) {
+  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t n = sh.n, per = KP1 * n;
+  const uint64_t ggsw_len = (uint64_t)sh.level * KP1 * per;
+  for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {
+    uint32_t g = 0;
+    if (gidx) {
+      g = gidx[b];
+      if (g >= n_ggsw) continue;
+    }
+    const u64* G = ggsw_list + (uint64_t)g * ggsw_len + e;
+    const u64* d = digits + (uint64_t)b * sh.level * per + e;
+    u64 lo[KP1], hi[KP1];
+    uint32_t top[KP1];
+#pragma unroll
+    for (int c = 0; c < KP1; ++c) lo[c] = hi[c] = 0, top[c] = 0;
+    for (uint32_t li = 0; li < sh.level; ++li) {
+#pragma unroll
+      for (int r = 0; r < KP1; ++r) {
+        const u64 x = d[((uint64_t)li * KP1 + r) * n];
+        const u64* Gr = G + ((uint64_t)li * KP1 + r) * KP1 * n;
+#pragma unroll
+        for (int c = 0; c < KP1; ++c) {
+          u64 pl, ph;
+          mul64x64(x, Gr[(uint64_t)c * n], pl, ph);
+          const u64 s = lo[c] + pl;
+          ph += s < pl;  // ph <= 2^64 - 2 for canonical operands: no wrap
+          lo[c] = s;
+          const u64 t = hi[c] + ph;
+          top[c] += t < ph;
+          hi[c] = t;
+        }
+      }
+    }
+    u64* out = y + (uint64_t)b * per + e;
+    const Goldilocks gl;
+#pragma unroll
+    for (int c = 0; c < KP1; ++c) {
+      u64 v = gl.sub(gl.reduce128(lo[c], hi[c]), (u64)top[c] << 32);
+      out[(uint64_t)c * n] = n_inv ? gl.mul(v, n_inv) : v;
+    }
+  }
+}
+
+// large_mac_cols for k + 1 <= 4 (every shortint shape), large_mac otherwise
+inline hipError_t launch_large_mac(u64* y, const u64* digits, const u64* ggsw_list, uint32_t batch,
+                                   const LargeShape& sh, u64 n_inv, const uint32_t* gidx, uint32_t n_ggsw,
+                                   hipStream_t s) {
+  if (sh.k <= 3 && sh.n >= 256) {
+    const dim3 grid(sh.n / 256, std::min<uint32_t>(batch, 65535));
+#define MI_MAC_COLS(KP)                                                                                            \
+  hipLaunchKernelGGL(large_mac_cols<KP>, grid, dim3(256), 0, s, y, digits, ggsw_list, batch, sh, n_inv, gidx, n_ggsw)
+    switch (sh.k) {
+      case 0: MI_MAC_COLS(1); break;
+      case 1: MI_MAC_COLS(2); break;
+      case 2: MI_MAC_COLS(3); break;
+      default: MI_MAC_COLS(4); break;
+    }
+#undef MI_MAC_COLS
+  } else {
+    const uint64_t elems = (uint64_t)batch * (sh.k + 1) * sh.n;
+    hipLaunchKernelGGL(large_mac, dim3((unsigned)std::min<uint64_t>((elems + 255) / 256, 65536)), dim3(256), 0, s, y,
+                       digits, ggsw_list, batch, sh, n_inv, gidx, n_ggsw);
+  }
+  return hipGetLastError();
+}
+
 // acc += modswitch_{p -> 2^64}(y) (ntt64.rs:184-197 + wrapping add) / acc += y mod p (ntt64.rs:244-266)
 template <bool BNF>
 __global__ __launch_bounds__(256) void large_accumulate(u64* __restrict__ acc, const u64* __restrict__ y, uint32_t batch,
@@ -368,7 +443,6 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   u64* y = digits + chunk * level * per;
   u64* acc = y + chunk * per;
   u64* corr = acc + chunk * per;
-  const MontParams mp{};
   for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
     const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
     const u64* in = lwe_in + b0 * (n_lwe + 1);
@@ -399,8 +473,8 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
         e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
         if (e != hipSuccess) break;
       }
-      hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, bsk + (size_t)i * ggsw_len, nb,
-                         sh, (u64)0, (const uint32_t*)nullptr, 1u);
+      e = launch_large_mac(y, digits, bsk + (size_t)i * ggsw_len, nb, sh, (u64)0, nullptr, 1u, s);
+      if (e != hipSuccess) break;
       if (split) {  // the inverse's last pass accumulates into acc itself (launch_ntt_split acc_mode)
         e = launch_ntt_split(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, *split, s, acc, bnf ? 1 : 2);
         continue;
@@ -474,7 +548,6 @@ hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int le
   if (e != hipSuccess) return e;
   u64* digits = scratch;
   u64* y = digits + chunk * level * per;
-  const MontParams mp{};
   for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
     const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
     const uint64_t elems = (uint64_t)nb * per;
@@ -493,8 +566,8 @@ hipError_t launch_ext_product_large(int logn, int k, bool bnf, bool cmux, int le
     e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
     if (e != hipSuccess) break;
     // BNF GGSWs are the reference's Raw NTT keys: the product is normalised here (ntt64_bnf_pbs.rs:670)
-    hipLaunchKernelGGL(large_mac, dim3(blocks_for(elems)), dim3(256), 0, s, y, digits, ggsw, nb, sh,
-                       bnf ? (u64)n_inv : (u64)0, gi, gi ? n_ggsw : 1u);
+    e = launch_large_mac(y, digits, ggsw, nb, sh, bnf ? (u64)n_inv : (u64)0, gi, gi ? n_ggsw : 1u, s);
+    if (e != hipSuccess) break;
     e = ntt_large(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, split, s);
     if (e != hipSuccess) break;
     if (bnf)
