@@ -1136,7 +1136,7 @@ def main():
     }
     if rank == 0 and world == 1:
         out["host_path"] = bench_host_path(eng, torch)
-        if not args.no_pbs:
+        if not args.no_pbs and not args.no_shapes:  # (it runs the shape-generic f64 engine, as the shape legs do)
             out["default_stream"] = bench_default_stream(eng, torch, dev, work)
     # the driver keeps only the tail of stdout: the bulky legs first, configs 3 and 4 (external product, PBS) last
     for name in LEG_ORDER:

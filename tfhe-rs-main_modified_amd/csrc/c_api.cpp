@@ -21,6 +21,7 @@
 #include "scratch.hpp"
 #include "build_info.hpp"  // build/ (Makefile): MI_SOURCE_HASH
 #include "c_api_internal.hpp"
+#include "mi_arith.hpp"
 #include "ntt64_tw_tables.hpp"
 
 namespace mi {
@@ -202,7 +203,16 @@ static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_pla
     // psi_N^(N / 2048) = psi_2048 (prime64.rs:166-177), checked here against the tables both plans were built from
     const mi_ntt64_plan* sub = nullptr;
     const u64 psi = plan->twid[mi::host::bit_rev(logn, 1)];
-    if (mi_ntt64_plan_cached(2048, p, device, &sub) == MI_OK && sub->twisted &&
+    // the top passes at stage 0 multiply by shifts (Goldilocks::mul_pow2): entries 1 .. 31 of both tables must be
+    // the powers of two tower_exp names
+    bool pow2_ok = true;
+    for (int st = 0; st < 5; ++st)
+      for (int g = 0; g < (1 << st); ++g) {
+        const size_t i = ((size_t)1 << st) + g;
+        pow2_ok = pow2_ok && plan->twid[i] == mi::host::exp_mod(2, (u64)mi::tower_exp(true, st, g), p) &&
+                  plan->inv_twid[i] == mi::host::exp_mod(2, (u64)mi::tower_exp(false, st, g), p);
+      }
+    if (pow2_ok && mi_ntt64_plan_cached(2048, p, device, &sub) == MI_OK && sub->twisted &&
         mi::host::exp_mod(psi, (u64)(n / 2048), p) == sub->twid[mi::host::bit_rev(11, 1)]) {
       const int t = logn - 11;
       std::vector<u64> blk(2 * n);

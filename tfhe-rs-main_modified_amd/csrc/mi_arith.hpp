@@ -69,7 +69,29 @@ struct Goldilocks {
     mul64x64(a, b, lo, hi);
     return reduce128(lo, hi);
   }
+  // |x 2^e| mod p for a twiddle 2^e (e < 192; 2^96 = -1), canonical, with the sign in `neg` (x 2^e = neg ? -t : t):
+  // shifts and the 128-bit reduction instead of the four-limb product.  e must fold to a constant (unrolled stage
+  // loops) so the branches disappear.  The friendly twiddles of prime64.rs:162-177.
+  __device__ __forceinline__ static u64 mul_pow2(u64 x, int e, bool& neg) {
+    neg = e >= 96;
+    const int f = neg ? e - 96 : e;
+    if (f == 0) return x >= P ? x - P : x;
+    if (f < 64) return reduce128(x << f, x >> (64 - f));
+    // 64 <= f < 96: with y = x 2^(f - 64) = hi 2^64 + lo (hi < 2^32), x 2^f = lo 2^64 + hi 2^128 = lo 2^64 - hi 2^32
+    const int g = f - 64;
+    const u64 lo = x << g, hi = g ? x >> (64 - g) : 0;
+    return sub(reduce128(0, lo), hi << 32);
+  }
 };
+
+// the power-of-two twiddles of the first five stages of every Goldilocks plan with the Solinas root tower
+// (psi_N^(N / 32) = 8, prime64.rs:166-177): table entry 2^s + g (stage s, group g) is 2^(3 bitrev_5(2^s + g)), its
+// inverse-table twin 2^(192 - that); checked against the plan's tables where a kernel relies on it (c_api.cpp)
+__host__ __device__ constexpr int tower_exp(bool fwd, int s, int g) {
+  int i = (1 << s) + g, r = 0;
+  for (int b = 0; b < 5; ++b) r |= ((i >> b) & 1) << (4 - b);
+  return fwd ? 3 * r : (192 - 3 * r) % 192;
+}
 
 // Generic odd modulus p < 2^64 in Montgomery form (R = 2^64).  `pinv` = -p^{-1} mod 2^64.
 struct Montgomery {

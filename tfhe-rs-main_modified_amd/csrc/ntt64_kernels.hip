@@ -90,7 +90,9 @@ __global__ __launch_bounds__(G::THREADS) void ntt_window_kernel(IO* __restrict__
 // ACC (the inverse's last pass inside the large-N blind rotation, pbs_large.hip): instead of storing the output x,
 // acc[e] += modswitch_{p -> 2^64}(x) (1, BNF, ntt64.rs:184-197 + wrapping add) or acc[e] = acc[e] + x mod p (2,
 // Solinas, ntt64.rs:244-266), acc laid out like data (stride apart per polynomial)
-template <int K, bool FWD, class Mod, class IO, int TWIST = 0, int ACC = 0>
+// P2 (a pass that starts at stage 0 of a Goldilocks plan with the Solinas tower): the twiddles are the powers of two
+// 2^tower_exp(s, g), multiplied by shifts (Goldilocks::mul_pow2) instead of table loads and four-limb products.
+template <int K, bool FWD, class Mod, class IO, int TWIST = 0, int ACC = 0, bool P2 = false>
 __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uint64_t stride, uint32_t logn, uint32_t s0,
                                                       const u64* __restrict__ tw, Mod mod,
                                                       const u64* __restrict__ twist = nullptr,
@@ -118,6 +120,21 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (i & d) continue;
+      if constexpr (P2) {
+        const int g = i >> (K - s), ex = tower_exp(FWD, s, g);
+        bool ng;
+        if (FWD) {
+          const u64 z = Goldilocks::mul_pow2(x[i + d], ex, ng);
+          const u64 a = x[i];
+          x[i] = ng ? Goldilocks::sub(a, z) : Goldilocks::add(a, z);
+          x[i + d] = ng ? Goldilocks::add(a, z) : Goldilocks::sub(a, z);
+        } else {  // (a - b) w = (b - a) |w| for a negative w
+          const u64 a = x[i], b = x[i + d];
+          x[i] = Goldilocks::add(a, b);
+          x[i + d] = Goldilocks::mul_pow2(ex >= 96 ? Goldilocks::sub(b, a) : Goldilocks::sub(a, b), ex, ng);
+        }
+        continue;
+      }
       const u64 wv = tw[twc * m + (uint64_t)(i >> (K - s))];
       if (FWD) {
         const u64 z = mod.mul(x[i + d], wv);
@@ -250,8 +267,14 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
                                 const u64* twist, u64* acc, hipStream_t s) {
   const uint64_t threads = (uint64_t)1 << (logn - K);
   const dim3 grid((unsigned)((threads + 255) / 256), (unsigned)batch);
-  hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC>), grid, dim3(256), 0, s, data,
-                     (uint64_t)stride, (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist, acc);
+  // the pass at stage 0 has the tower's power-of-two twiddles (the split tables are only built when the plan's
+  // tables agree, c_api.cpp)
+  if (s0 == 0)
+    hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true>), grid, dim3(256), 0, s, data,
+                       (uint64_t)stride, (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist, acc);
+  else
+    hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC>), grid, dim3(256), 0, s, data,
+                       (uint64_t)stride, (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist, acc);
   return hipGetLastError();
 }
 

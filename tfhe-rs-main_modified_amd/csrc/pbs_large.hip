@@ -117,6 +117,7 @@ __global__ __launch_bounds__(256) void large_rotate_decompose(u64* __restrict__ 
 // of GLWE polynomial (b, c) forms ct1 = X^a acc - acc at the 2^K coefficients e = j + r cols (cols = N / 2^K), decomposes
 // them, and for each level li runs the first K top CT stages of the transform (s0 = 0: twiddle tw[m + g]) on the
 // digits in registers (ONLY: the pass is the last one, so the block twist follows), storing digit polynomial (b, li, c)
+// (stage 0's twiddles are the tower's powers of two, Goldilocks::mul_pow2; the split tables exist only when they are)
 // in the layout of large_rotate_decompose.  Replaces that pass plus the transform's first pass: acc is read once and
 // the digits written once (not written, read and written again).
 template <int K, bool BNF, bool ONLY>
@@ -165,22 +166,27 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       x[r] = ((int64_t)term < 0) ? term + P : term;
     }
 #pragma unroll
-    for (int s = 0; s < K; ++s) {  // stage s: m = 2^s groups, pair distance 2^(K-1-s) in r
-      const int m = 1 << s, d = 1 << (K - 1 - s);
+    for (int s = 0; s < K; ++s) {  // stage s: m = 2^s groups, pair distance 2^(K-1-s) in r; twiddle tw[m + g] = 2^e
+      const int d = 1 << (K - 1 - s);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (r & d) continue;
-        const u64 z = gl.mul(x[r + d], tw[m + (r >> (K - s))]);
+        bool ng;
+        const u64 z = Goldilocks::mul_pow2(x[r + d], tower_exp(true, s, r >> (K - s)), ng);
         const u64 u = x[r];
-        x[r] = gl.add(u, z);
-        x[r + d] = gl.sub(u, z);
+        x[r] = ng ? gl.sub(u, z) : gl.add(u, z);
+        x[r + d] = ng ? gl.add(u, z) : gl.sub(u, z);
       }
     }
     u64* o = dp + (uint64_t)li * per;
+    // the block twist per level: an opaque base keeps its loads inside the level loop (hoisted, the 2^K values would
+    // stay live across the loop beside the digits and the decomposition state)
+    const u64* tws = twist;
+    if (ONLY) asm volatile("" : "+s"(tws));
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       u64 v = x[r];
-      if (ONLY) v = gl.mul(v, twist[j + r * cols]);
+      if (ONLY) v = gl.mul(v, tws[j + r * cols]);
       o[r * cols] = v;
     }
   }
@@ -264,62 +270,71 @@ __global__ __launch_bounds__(256) void large_mac(u64* __restrict__ y, const u64*
 
 // The same product with every output column of an item in one thread (k + 1 = KP1 columns): each digit is read once
 // instead of k + 1 times (the digits are (level + 1) / 2 of the step's HBM bytes at k = 1), and the level (k + 1)
-// terms of a column are summed as 128-bit products with one reduction at the end (2^128 = -2^32 mod p).  Grid:
-// x over the coefficient, y over the item.
+// terms of a column are summed as 128-bit products with one reduction at the end (2^128 = -2^32 mod p).  A thread
+// takes two adjacent coefficients (16-byte accesses).  Grid: x over coefficient pairs, y over the items.
+struct Acc128 {
+  u64 lo = 0, hi = 0;
+  uint32_t top = 0;
+  __device__ __forceinline__ void mac(u64 x, u64 w) {
+    u64 pl, ph;
+    mul64x64(x, w, pl, ph);
+    const u64 s = lo + pl;
+    ph += s < pl;  // ph <= 2^64 - 2 for canonical operands: no wrap
+    lo = s;
+    const u64 t = hi + ph;
+    top += t < ph;
+    hi = t;
+  }
+  __device__ __forceinline__ u64 value(u64 n_inv) const {
+    const u64 v = Goldilocks::sub(Goldilocks::reduce128(lo, hi), (u64)top << 32);
+    return n_inv ? Goldilocks::mul(v, n_inv) : v;
+  }
+};
+
 template <int KP1>
 __global__ __launch_bounds__(256) void large_mac_cols(u64* __restrict__ y, const u64* __restrict__ digits,
                                                       const u64* __restrict__ ggsw_list, uint32_t batch,
                                                       LargeShape sh, u64 n_inv, const uint32_t* __restrict__ gidx,
                                                       uint32_t n_ggsw) {
-  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t e = (blockIdx.x * 256 + threadIdx.x) * 2;
   const uint64_t n = sh.n, per = KP1 * n;
   const uint64_t ggsw_len = (uint64_t)sh.level * KP1 * per;
   for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {
-    uint32_t g = 0;
+    const u64* G = ggsw_list + e;
     if (gidx) {
-      g = gidx[b];
+      const uint32_t g = gidx[b];
       if (g >= n_ggsw) continue;
+      G += (uint64_t)g * ggsw_len;
     }
-    const u64* G = ggsw_list + (uint64_t)g * ggsw_len + e;
     const u64* d = digits + (uint64_t)b * sh.level * per + e;
-    u64 lo[KP1], hi[KP1];
-    uint32_t top[KP1];
-#pragma unroll
-    for (int c = 0; c < KP1; ++c) lo[c] = hi[c] = 0, top[c] = 0;
+    Acc128 acc[KP1][2];
     for (uint32_t li = 0; li < sh.level; ++li) {
 #pragma unroll
       for (int r = 0; r < KP1; ++r) {
-        const u64 x = d[((uint64_t)li * KP1 + r) * n];
-        const u64* Gr = G + ((uint64_t)li * KP1 + r) * KP1 * n;
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + ((uint64_t)li * KP1 + r) * n);
 #pragma unroll
         for (int c = 0; c < KP1; ++c) {
-          u64 pl, ph;
-          mul64x64(x, Gr[(uint64_t)c * n], pl, ph);
-          const u64 s = lo[c] + pl;
-          ph += s < pl;  // ph <= 2^64 - 2 for canonical operands: no wrap
-          lo[c] = s;
-          const u64 t = hi[c] + ph;
-          top[c] += t < ph;
-          hi[c] = t;
+          const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(G + (((uint64_t)li * KP1 + r) * KP1 + c) * n);
+          acc[c][0].mac(x.x, w.x);
+          acc[c][1].mac(x.y, w.y);
         }
       }
     }
     u64* out = y + (uint64_t)b * per + e;
-    const Goldilocks gl;
 #pragma unroll
-    for (int c = 0; c < KP1; ++c) {
-      u64 v = gl.sub(gl.reduce128(lo[c], hi[c]), (u64)top[c] << 32);
-      out[(uint64_t)c * n] = n_inv ? gl.mul(v, n_inv) : v;
-    }
+    for (int c = 0; c < KP1; ++c)
+      *reinterpret_cast<ulonglong2*>(out + (uint64_t)c * n) =
+          make_ulonglong2(acc[c][0].value(n_inv), acc[c][1].value(n_inv));
   }
 }
 
-// large_mac_cols for k + 1 <= 4 (every shortint shape), large_mac otherwise
+// large_mac_cols for k + 1 <= 4 (every shortint shape) and 16-byte aligned operands, large_mac otherwise
 inline hipError_t launch_large_mac(u64* y, const u64* digits, const u64* ggsw_list, uint32_t batch,
                                    const LargeShape& sh, u64 n_inv, const uint32_t* gidx, uint32_t n_ggsw,
                                    hipStream_t s) {
-  if (sh.k <= 3 && sh.n >= 256) {
-    const dim3 grid(sh.n / 256, std::min<uint32_t>(batch, 65535));
+  const bool aligned = (((uintptr_t)y | (uintptr_t)digits | (uintptr_t)ggsw_list) & 15) == 0;
+  if (sh.k <= 3 && sh.n >= 512 && aligned) {
+    const dim3 grid(sh.n / 512, std::min<uint32_t>(batch, 65535));
 #define MI_MAC_COLS(KP)                                                                                            \
   hipLaunchKernelGGL(large_mac_cols<KP>, grid, dim3(256), 0, s, y, digits, ggsw_list, batch, sh, n_inv, gidx, n_ggsw)
     switch (sh.k) {
