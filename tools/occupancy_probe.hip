@@ -5,7 +5,8 @@
 // its time until too few waves remain to cover the dependency chains.  Times are interleaved in rotated rounds.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I tfhe-rs-main_modified_amd/csrc tools/occupancy_probe.hip \
-//         -o tools/occupancy_probe && tools/occupancy_probe [batch]
+//         -o tools/occupancy_probe && tools/occupancy_probe [batch] [warm-up launches] [launches per round] [rounds]
+// (short settings for a PMC pass: tools/occupancy_probe 8192 200 4 1; the dynamic LDS size tells the residency apart)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -102,12 +103,13 @@ int main(int argc, char** argv) {
     else
       hipLaunchKernelGGL((body_kernel<false, 1>), dim3(batch), dim3(64), pad_for(o, 1), s, data, batch, twist);
   };
-  for (int it = 0; it < 20000; ++it) run(it & 1, 4);  // the clock settles under load
+  const int warm = argc > 2 ? atoi(argv[2]) : 20000;
+  for (int it = 0; it < warm; ++it) run(it & 1, 4);  // the clock settles under load
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int K = 200, R = 9;
+  const int K = argc > 3 ? atoi(argv[3]) : 200, R = argc > 4 ? atoi(argv[4]) : 9;
   std::vector<double> t[2][4];
   for (int r = 0; r < R; ++r)
     for (int oi = 0; oi < 4; ++oi)
