@@ -53,8 +53,10 @@ class Wave:
         m = re.fullmatch(r"s\[(\d+):(\d+)\]", tok)
         return int(m.group(1)) if m else None
 
+    VCC = 106  # vcc_lo / vcc_hi are s106 / s107
+
     def mask(self, tok):
-        b = self.spair(tok)
+        b = self.VCC if tok == "vcc" else self.spair(tok)
         if b is None:
             raise ValueError(tok)
         return _bits(int(self.s[b]) | (int(self.s[b + 1]) << 32))
@@ -234,6 +236,13 @@ class Wave:
     def op_v_subb_co_u32_e64(self, a):
         self._carry_op(a, lambda x, y, c: ((x - y - c) & 0xFFFFFFFF, x - y - c < 0))
 
+    def op_v_cndmask_b32_dpp(self, a):
+        # VOP2 select with a DPP source: D = VCC ? src1 : dpp(src0); a[3] = "vcc quad_perm:[...] ..."
+        src = self.src32(a[1])
+        perm = [int(x) for x in re.search(r"quad_perm:\[(.*?)\]", a[3]).group(1).split(",")]
+        idx = np.array([(l & ~3) + perm[l & 3] for l in range(LANES)])
+        self.wv(self.vreg(a[0]), np.where(self.mask("vcc"), self.src32(a[2]), src[idx]))
+
     def op_v_cndmask_b32_e64(self, a):
         m = self.mask(a[3])
         self.wv(self.vreg(a[0]), np.where(m, self.src32(a[2]), self.src32(a[1])))
@@ -258,7 +267,11 @@ class Wave:
             self.s_set(a[0], val)
 
     def op_s_mov_b64(self, a):
-        if a[1] == "exec":
+        if a[0] == "vcc":
+            v = int(a[1], 0) if not a[1].startswith("s[") else (int(self.s[self.spair(a[1])]) |
+                                                                 (int(self.s[self.spair(a[1]) + 1]) << 32))
+            self.s[self.VCC], self.s[self.VCC + 1] = np.uint64(v & 0xFFFFFFFF), np.uint64((v >> 32) & 0xFFFFFFFF)
+        elif a[1] == "exec":
             word = _word(self.exec)
             b = self.spair(a[0])
             self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
@@ -266,6 +279,12 @@ class Wave:
             self.exec = self.mask(a[1])
         else:
             raise NotImplementedError(a)
+
+    def op_s_not_b64(self, a):
+        word = _word(~self.mask(a[1]))
+        b = self.VCC if a[0] == "vcc" else self.spair(a[0])
+        self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
+        self.scc = int(word != 0)
 
     def op_s_or_b64(self, a):
         word = _word(self.mask(a[1]) | self.mask(a[2]))

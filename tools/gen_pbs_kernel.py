@@ -463,6 +463,9 @@ def add_acc_sol(B, dmap):
 # The key the body reads is then the private copy in that order (row R, lane L of polynomial position 64 R + L holds
 # NTT-domain coefficient tw_key_index(64 R + L); pbs_tw.hip prepare_tw_key builds it).
 PBS_W1P = True
+# the blind-rotation loop keeps one register map across its steps, which the renaming of the DPP-select regroup would
+# break: its bodies keep the DPP-move regroup
+T.REGROUP_DPP_SELECT = False
 
 
 def tw_key_index(pos):
@@ -617,7 +620,8 @@ def gen_ext(tabs, cmux, sol=False):
 
 
 def emit(name, body, sgprs=SGPR_CLOBBER):
-    clob = [f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in sgprs] + ['"scc"', '"memory"']
+    clob = ([f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in sgprs] + ['"scc"', '"memory"'] +
+            (['"vcc"'] if T.REGROUP_DPP_SELECT else []))
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
             f"#define MI_PBS_BODY_{name.upper()}(...) asm volatile(\\\n" +
             "\\\n".join(f'      "{l}\\n"' for l in body.lines) +

@@ -660,7 +660,13 @@ def t1(body, dmap, ybase, newhi, ad=NTT_ADDR, row_waits=None):
 
 
 def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
-    """W1 (pairs=False) or W1' (pairs=True) -> W0, halves split by i (row stride 66)."""
+    """W1 (pairs=False) or W1' (pairs=True) -> W0, halves split by i (row stride 66).  The first half's 16 rows land
+    in registers no data occupies (ybase.. when free; the renamed pairs of REGROUP_DPP_SELECT may sit there)."""
+    ydst = [ybase + 2 * r for r in range(16)]
+    if any(d + o in range(ybase, ybase + 32) for d in dmap for o in (0, 1)):
+        free = [b + 2 * j for b in free_blocks_except(dmap) for j in range(4) if not newhi <= b < newhi + 32]
+        assert len(free) >= 16, free
+        ydst = free[:16]
     L = []
     for h in range(2):
         L += ([f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"] if h == 0 else
@@ -676,24 +682,45 @@ def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
         L += EXEC_ALL
         if h == 1:
             L.append("s_waitcnt lgkmcnt(0)")
-        dst = ybase if h == 0 else newhi
+        dst = ydst if h == 0 else [newhi + 2 * r for r in range(16)]
         rb = ad.t2r if pairs else ad.t4r
         for r in range(16):
-            L.append(f"ds_read_b64 {pv(dst + 2 * r)}, {rb} offset:{r * 66 * 8}")
+            L.append(f"ds_read_b64 {pv(dst[r])}, {rb} offset:{r * 66 * 8}")
     L.append("s_waitcnt lgkmcnt(0)")
     body.raw(*L)
-    return [ybase + 2 * r for r in range(16)] + [newhi + 2 * r for r in range(16)]
+    return ydst + [newhi + 2 * r for r in range(16)]
+
+
+# The lane-pair regroup as two VOP2 selects per 32-bit word with a DPP partner-lane source (v_cndmask_b32_dpp, VCC set
+# by the SALU) instead of two DPP moves and two selects; the second slot's new value goes to a fresh register pair
+# (renamed in dmap) so neither select overwrites a value the partner lane still has to read.
+REGROUP_DPP_SELECT = False
 
 
 def regroup(sg, dmap, k, tmp, to_pairs, k2=None):
     """W1 <-> W1' for register pair (k, k2 = k+16) of this lane and its partner (lane ^ 1).
     to_pairs: even lane ends with (a_k, b_k), odd lane with (a_{k2}, b_{k2}).
-    back:     even lane ends with (a_k, a_{k2}), odd lane with (b_k, b_{k2})."""
+    back:     even lane ends with (a_k, a_{k2}), odd lane with (b_k, b_{k2}).
+    With REGROUP_DPP_SELECT the k2 slot moves to the pair tmp[0:2] (dmap updated) and the returned register base is
+    the one it left, free for the caller's next temporary; otherwise returns None."""
+    kk2 = k + 16 if k2 is None else k2
     lo0, hi0, p0 = X(dmap, k)
-    lo1, hi1, p1 = X(dmap, k + 16 if k2 is None else k2)
+    lo1, hi1, p1 = X(dmap, kk2)
     T0, T1, U0, U1 = tmp
     par = f"s[{S_PAR}:{S_PAR + 1}]"
     dpp = "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+    if REGROUP_DPP_SELECT:
+        # both directions move the same values: the k2 slot of an even lane takes its partner's k slot, the k slot of an
+        # odd lane its partner's k2 slot (VOP2 select: D = VCC ? src1 : dpp(src0))
+        old = dmap[kk2]
+        sg.add(f"s_mov_b64 vcc, {par}", [par], ["vcc"], "salu")
+        sg.add(f"v_cndmask_b32_dpp {T0}, {lo0}, {lo1}, vcc {dpp}", [lo0, lo1, "vcc"], [T0], "dpp")
+        sg.add(f"v_cndmask_b32_dpp {T1}, {hi0}, {hi1}, vcc {dpp}", [hi0, hi1, "vcc"], [T1], "dpp")
+        sg.add(f"s_not_b64 vcc, {par}", [par], ["vcc", "scc"], "salu")
+        sg.add(f"v_cndmask_b32_dpp {lo0}, {lo1}, {lo0}, vcc {dpp}", [lo1, lo0, "vcc"], [lo0], "dpp")
+        sg.add(f"v_cndmask_b32_dpp {hi0}, {hi1}, {hi0}, vcc {dpp}", [hi1, hi0, "vcc"], [hi0], "dpp")
+        dmap[kk2] = int(T0[1:])
+        return old
     if to_pairs:
         # T = partner x[k], U = partner x[k+16]; even: x[k+16] <- T ; odd: x[k] <- U
         sg.add(f"v_mov_b32_dpp {T0}, {lo0} {dpp}", [lo0], [T0], "dpp")
@@ -848,7 +875,9 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
             wlo, whi = f"v{wb[2 * i]}", f"v{wb[2 * i] + 1}"
             if pre and k in pre:  # twiddle loaded earlier, latency hidden behind the previous stages
                 wlo, whi = f"v{pre[k]}", f"v{pre[k] + 1}"
-            regroup(sg, dmap, k, tmp, True)
+            freed = regroup(sg, dmap, k, tmp, True)
+            if freed is not None:
+                tmps[i % 2][0:2] = [freed, freed + 1]
             a, b = X(dmap, k), X(dmap, k + 16)
             if fwd:
                 # last stage: canonical outputs from a canonical a (3 VALU) and a canonicalising add /
@@ -880,7 +909,9 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
                     tmul_lane(sg, E[k], E[k + 16], b, sl, b[0], b[1], par3, (wlo, whi))
                 else:
                     gmul(sg, m, b, wlo, whi, b[0], b[1])
-                regroup(sg, dmap, k, tmp, False)
+                freed = regroup(sg, dmap, k, [f"v{r}" for r in tmps[i % 2]], False)
+                if freed is not None:
+                    tmps[i % 2][0:2] = [freed, freed + 1]
         for j, op in enumerate(sg.ops):
             op.idx = j
         B.out(sg.schedule())
@@ -1173,7 +1204,9 @@ def pair_stage_dit(B, dmap, ad, pre, busy, after_half=None):
             mm = msl[i % 2]
             sl = slot_view(mm, c23[i % 2])
             Se, So = inv_last_exp(2 * m), inv_last_exp(2 * m + 1)
-            regroup(sg, dmap, 2 * m, tmp, True, k2=2 * m + 1)
+            freed = regroup(sg, dmap, 2 * m, tmp, True, k2=2 * m + 1)
+            if freed is not None:
+                tmps[i % 2][0:2] = [freed, freed + 1]
             a, b = X(dmap, 2 * m), X(dmap, 2 * m + 1)
             if lane_tmul_applies(Se, So):
                 neg = tmul_lane(sg, Se, So, b, sl, sl.v[2], sl.v[3], par3, tuple(f"v{r}" for r in amts[i % 2]))
@@ -1307,7 +1340,7 @@ def gen_inv(tabs, stop=None):
 
 def emit(name, body, ops_in, sgpr_extra=()):
     clob = ([f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in list(SGPR_CLOBBER) + list(sgpr_extra)] +
-            ['"scc"', '"memory"'])
+            ['"scc"', '"memory"'] + (['"vcc"'] if REGROUP_DPP_SELECT else []))
     text = "\n".join(f'      "{l}\\n"' for l in body.lines)
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
             f"#define MI_TW_BODY_{name.upper()}(...) asm volatile(\\\n" +

@@ -35,7 +35,8 @@ def counters(path):
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "trace", "run_kernel_stats.csv")):  # (PMC-only sessions have no trace)
+        shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     merged = defaultdict(dict)
     grids = {}
     for sub in ("pmc_sq", "pmc_lds", "pmc_fetch", "pmc_write"):
@@ -65,6 +66,18 @@ def main():
                 d["algorithmic_bytes_per_launch"] = ALG_BYTES
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             d["valu_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
+            for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in d:
+                    d[c.lower() + "_per_wave_cycle"] = d[c] / d["SQ_WAVE_CYCLES"]
+        if "SQ_INSTS_VALU" in d and d.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE sums the 8 XCDs' cycles; SQ_ACTIVE_INST_VALU counts instructions on gfx950 (it equals
+            # SQ_INSTS_VALU), so VALU issue-busy is instructions x the measured issue cost per instruction
+            # (tools/valu_probe.hip; the bodies' mix averages 4.20 cycles) over the SIMD cycles
+            simd_cycles = d["GRBM_GUI_ACTIVE"] / 8 * 1024
+            d["valu_instr_per_simd_cycle"] = d["SQ_INSTS_VALU"] / simd_cycles
+            if "ntt_tw" in k:
+                d["valu_issue_busy"] = d["valu_instr_per_simd_cycle"] * 4.20
         summary[k] = d
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)

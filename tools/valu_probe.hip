@@ -144,6 +144,32 @@ KERNEL(k_dppq, uint32_t, I_DPPQ)
 KERNEL(k_lshl64, uint64_t, I_LSHL64)
 KERNEL(k_madi64, uint64_t, I_MADI64)
 
+// VCC written by the SALU once before the loop (s_mov_b64 vcc, exec): the VOP2 select, and the same select with a DPP
+// partner-lane source (quad_perm [1,0,3,2]: one instruction for the lane-pair regroup's move + select)
+#define KERNEL_SVCC(NAME, T, INS)                                                              \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t s0, uint32_t s1, uint64_t* clk) { \
+    T a0 = s0 + threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7; \
+    uint32_t b = s1 ^ threadIdx.x;                                                           \
+    uint64_t m0;                                                                             \
+    asm volatile("s_mov_b64 %0, exec" : "=s"(m0));                                           \
+    asm volatile("s_mov_b64 vcc, %0\n\ts_nop 7\n\ts_nop 7" :: "s"(m0) : "memory", "vcc");    \
+    uint64_t t0 = __builtin_amdgcn_s_memtime();                                              \
+    uint64_t r0 = __builtin_amdgcn_s_memrealtime();                                          \
+    for (int i = 0; i < ITERS; ++i) { BODY8(INS) }                                           \
+    uint64_t t1 = __builtin_amdgcn_s_memtime();                                              \
+    uint64_t r1 = __builtin_amdgcn_s_memrealtime();                                          \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+    if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t1 - t0; clk[2 * blockIdx.x + 1] = r1 - r0; } \
+  }
+#define I_CND32S(x, k) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(b));
+#define I_CNDDPP(x, k) asm volatile("v_cndmask_b32_dpp %0, %1, %0, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" \
+                                    : "+v"(x) : "v"(b));
+#define I_ADDDPP(x, k) asm volatile("v_add_u32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" \
+                                    : "+v"(x) : "v"(b));
+KERNEL_SVCC(k_cnd32s, uint32_t, I_CND32S)
+KERNEL_SVCC(k_cnddpp, uint32_t, I_CNDDPP)
+KERNEL_SVCC(k_adddpp, uint32_t, I_ADDDPP)
+
 typedef void (*kfn)(uint64_t*, uint32_t, uint32_t, uint64_t*);
 
 int main(int argc, char** argv) {
@@ -164,6 +190,8 @@ int main(int argc, char** argv) {
       {"v_rndne_f64", k_frnd}, {"v_cvt_f64_i32", k_fcvt}, {"v_pk_fma_f32", k_fpkfma},
       {"v_permlane32_swap_b32", k_pl32}, {"v_permlane16_swap_b32", k_pl16}, {"v_mov_b32_dpp quad_perm", k_dppq},
       {"v_lshlrev_b64", k_lshl64}, {"v_mad_i64_i32", k_madi64},
+      {"v_cndmask_e32(vcc salu-set)", k_cnd32s}, {"v_cndmask_b32_dpp(vcc salu-set)", k_cnddpp},
+      {"v_add_u32_dpp quad_perm", k_adddpp},
   };
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
