@@ -587,10 +587,10 @@ hipError_t inverse(const Geo& g, Src src, Sink sink, cplx* tmp, uint64_t polys, 
 }
 
 // items per chunk: digits (level (k + 1) M complex), products (R > 1: (k + 1) M complex) and accumulators stay
-// below ~1 GiB of scratch
+// below ~4 GiB of scratch (of 288 GB)
 inline size_t chunk_for(const Geo& g, uint32_t kp1, uint32_t level, size_t batch) {
   const size_t per_item = ((size_t)level + 2) * kp1 * ((size_t)8 << g.logn);
-  return std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per_item));
+  return std::max<size_t>(1, std::min(batch, ((size_t)4 << 30) / per_item));
 }
 
 }  // namespace gen

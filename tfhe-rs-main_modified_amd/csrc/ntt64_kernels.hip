@@ -23,6 +23,7 @@
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "ntt64_regs.hpp"
+#include "ntt64_tile.hpp"
 #include "pbs_device.hpp"
 
 namespace mi {
@@ -163,6 +164,61 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
   for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
 }
 
+// The stage-0 pass of the split transform at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): the same function as
+// ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true> at s0 = 0.  Grid: x = column tiles of 64, y = polynomials.
+template <int K, bool FWD, int TWIST, int ACC, int W>
+__device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t cols, uint64_t col, uint32_t c,
+                                              const u64* __restrict__ twist, u64* __restrict__ accp, u64* lds) {
+  using Rw = tile::Rows<K>;
+  constexpr int RPT = Rw::RPT;
+  u64 x[RPT];
+  if constexpr (FWD) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) x[k] = poly[Rw::a(W, k) * cols + col];
+    tile::phase_a<K, true, W>(x);
+    tile::exchange<K, W, true>(x, lds, c);
+    tile::phase_b<K, true, W>(x);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint64_t e = Rw::b(W, k) * cols + col;
+      poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : x[k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint64_t e = Rw::b(W, k) * cols + col;
+      x[k] = TWIST == 2 ? Goldilocks::mul(poly[e], twist[e]) : poly[e];
+    }
+    tile::phase_b<K, false, W>(x);
+    tile::exchange<K, W, false>(x, lds, c);
+    tile::phase_a<K, false, W>(x);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint64_t e = Rw::a(W, k) * cols + col;
+      if constexpr (ACC == 1) accp[e] = accp[e] + pbs::modswitch_prime_to_native(x[k]);
+      else if constexpr (ACC == 2) accp[e] = pbs::add_custom(accp[e], x[k]);
+      else poly[e] = x[k];
+    }
+  }
+}
+
+template <int K, bool FWD, int TWIST, int ACC>
+__global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ data, uint64_t stride, uint32_t logn,
+                                                           const u64* __restrict__ twist, u64* __restrict__ acc) {
+  __shared__ u64 lds[(1 << K) * 64];
+  const uint64_t cols = (uint64_t)1 << (logn - K);
+  const uint32_t c = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t col = (uint64_t)blockIdx.x * 64 + c;
+  u64* poly = data + (uint64_t)blockIdx.y * stride;
+  u64* accp = ACC ? acc + (uint64_t)blockIdx.y * stride : nullptr;
+  switch (w) {
+    case 0: top_tile_body<K, FWD, TWIST, ACC, 0>(poly, cols, col, c, twist, accp, lds); break;
+    case 1: top_tile_body<K, FWD, TWIST, ACC, 1>(poly, cols, col, c, twist, accp, lds); break;
+    case 2: top_tile_body<K, FWD, TWIST, ACC, 2>(poly, cols, col, c, twist, accp, lds); break;
+    default: top_tile_body<K, FWD, TWIST, ACC, 3>(poly, cols, col, c, twist, accp, lds); break;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // launch dispatch
 
@@ -268,7 +324,15 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
   const uint64_t threads = (uint64_t)1 << (logn - K);
   const dim3 grid((unsigned)((threads + 255) / 256), (unsigned)batch);
   // the pass at stage 0 has the tower's power-of-two twiddles (the split tables are only built when the plan's
-  // tables agree, c_api.cpp)
+  // tables agree, c_api.cpp); at K = 4 / 5 it runs as the cooperative tile (>= 64 columns: logn >= K + 6)
+  if constexpr (K >= 4) {
+    if (s0 == 0 && logn >= K + 6) {
+      const dim3 tgrid((unsigned)(((uint64_t)1 << (logn - K)) / 64), (unsigned)batch);
+      hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
+                         (uint32_t)logn, twist, acc);
+      return hipGetLastError();
+    }
+  }
   if (s0 == 0)
     hipLaunchKernelGGL((ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true>), grid, dim3(256), 0, s, data,
                        (uint64_t)stride, (uint32_t)logn, (uint32_t)s0, tw, Goldilocks{}, twist, acc);

@@ -29,6 +29,7 @@
 #include "scratch.hpp"
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
+#include "ntt64_tile.hpp"
 #include "pbs_device.hpp"
 
 namespace mi {
@@ -192,10 +193,97 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
   }
 }
 
+// The same step at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): lane (wave W, column c) forms ct1 and the
+// decomposition state of its phase-A rows, then per level runs the phase-A stages, the LDS exchange and the phase-B
+// stages and stores the digit polynomial from its phase-B rows.  Grid: x = column tiles of 64, y = GLWE polynomials.
+template <int K, bool BNF, bool ONLY, int W>
+__device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64* __restrict__ ap, uint32_t full,
+                                                 uint32_t rem, uint64_t cols, uint64_t col, uint32_t c, uint64_t per,
+                                                 const LargeShape& sh, const u64* __restrict__ twist, u64* lds) {
+  using Rw = tile::Rows<K>;
+  constexpr int RPT = Rw::RPT;
+  u64 st[RPT];
+  bool sg[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const uint32_t e = (uint32_t)(Rw::a(W, k) * cols + col);
+    u64 v = ap[(e - rem) & (sh.n - 1)];  // X^a acc: new[e] = old[(e - rem) % N], negated for e < rem
+    if (full ^ (e < rem)) v = neg_q<BNF>(v);
+    const u64 x = BNF ? v - ap[e] : sub_custom(v, ap[e]);
+    if (BNF) {
+      st[k] = decomp_init_native(x, sh.base_log, (int)sh.level);
+      sg[k] = false;
+    } else {
+      const unsigned shift = 64u - (unsigned)(sh.base_log * (int)sh.level);
+      sg[k] = x >= P / 2 + 1;
+      st[k] = closest_abs_nonnative(sg[k] ? P - x : x, sh.base_log, (int)sh.level) >> shift;
+    }
+  }
+#pragma unroll 1
+  for (uint32_t li = 0; li < sh.level; ++li) {
+    u64 x[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      u64 term = decompose_one_level(sh.base_log, st[k]);
+      if (!BNF && sg[k]) term = (u64)0 - term;
+      x[k] = ((int64_t)term < 0) ? term + P : term;
+    }
+    tile::phase_a<K, true, W>(x);
+    tile::exchange<K, W, true>(x, lds, c);
+    tile::phase_b<K, true, W>(x);
+    u64* o = dp + (uint64_t)li * per;
+    const u64* tws = twist;  // opaque per level: the twist loads stay in the loop (not 2^K / 4 live values across it)
+    if (ONLY) asm volatile("" : "+s"(tws));
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint64_t e = Rw::b(W, k) * cols + col;
+      o[e] = ONLY ? Goldilocks::mul(x[k], tws[e]) : x[k];
+    }
+  }
+}
+
+template <int K, bool BNF, bool ONLY>
+__global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digits, const u64* __restrict__ acc,
+                                                         const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
+                                                         LargeShape sh, const u64* __restrict__ twist) {
+  __shared__ u64 lds[(1 << K) * 64];
+  const uint64_t cols = (uint64_t)sh.n >> K;
+  const uint32_t c = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t col = (uint64_t)blockIdx.x * 64 + c;
+  const uint32_t bc = blockIdx.y, b = bc / (sh.k + 1), cc = bc % (sh.k + 1);
+  const unsigned log_mod = sh.logn + 1;
+  const u64 a_raw = lwe_in[(uint64_t)b * (n_lwe + 1) + step];
+  u64 a = 0;
+  if (BNF) a = modulus_switch(a_raw, log_mod);
+  else if (a_raw != 0) a = ms_non_native(a_raw, log_mod);
+  const uint32_t full = (uint32_t)(a >> sh.logn) & 1u, rem = (uint32_t)(a & (sh.n - 1));
+  const u64* ap = acc + (uint64_t)bc * sh.n;
+  const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
+  u64* dp = digits + (uint64_t)b * sh.level * per + (uint64_t)cc * sh.n;
+  switch (w) {
+    case 0: rotdec_tile_body<K, BNF, ONLY, 0>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 1: rotdec_tile_body<K, BNF, ONLY, 1>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 2: rotdec_tile_body<K, BNF, ONLY, 2>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    default: rotdec_tile_body<K, BNF, ONLY, 3>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+  }
+}
+
 template <int K, bool BNF>
 static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, const u64* lwe_in, uint32_t n_lwe,
                                     uint32_t step, uint32_t nb, const LargeShape& sh, const u64* tw, const u64* twist,
                                     hipStream_t s) {
+  if constexpr (K >= 4) {
+    if ((sh.n >> K) >= 64) {  // the cooperative tile (>= one 64-column tile)
+      const dim3 tgrid((unsigned)(((uint64_t)sh.n >> K) / 64), nb * (sh.k + 1));
+      if (only)
+        hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
+                           sh, twist);
+      else
+        hipLaunchKernelGGL((large_rotdec_tile<K, BNF, false>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
+                           sh, twist);
+      return hipGetLastError();
+    }
+  }
   const dim3 grid((unsigned)((((uint64_t)sh.n >> K) + 255) / 256), nb * (sh.k + 1));
   if (only)
     hipLaunchKernelGGL((large_rotdec_top<K, BNF, true>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
@@ -434,10 +522,10 @@ inline hipError_t ntt_large(bool fwd, int logn, u64* d, size_t batch, size_t str
   return launch_ntt(fwd, logn, true, MontParams{}, d, batch, stride, tw, s);
 }
 
-// ciphertexts per chunk: the digits, products and accumulators of one chunk stay below ~1 GiB of scratch
+// ciphertexts per chunk: the digits, products and accumulators of one chunk stay below ~4 GiB of scratch (of 288 GB)
 inline size_t chunk_for(const LargeShape& sh, size_t batch) {
   const size_t per_item = ((size_t)sh.level + 2) * (sh.k + 1) * sh.n * sizeof(u64);
-  return std::max<size_t>(1, std::min(batch, ((size_t)1 << 30) / per_item));
+  return std::max<size_t>(1, std::min(batch, ((size_t)4 << 30) / per_item));
 }
 
 }  // namespace pbs
