@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mi_arith.hpp"
 
 namespace mi {
@@ -52,6 +54,10 @@ __host__ __device__ __forceinline__ constexpr int win_lo(int w) {
 // `twc` (SUB only): the transform is block b of 2^k blocks left by k top stages of a larger one
 // (large-N plans): its stage with m groups reads the big table at m * twc + g, twc = 2^k + b, because
 // the big stage has m 2^k groups and block b owns groups [b m, (b + 1) m).
+// Solinas prime (Mod = Goldilocks): the reference's stages with m < 32 groups use the tower's power-of-two twiddles
+// (entry m + g = 2^tower_exp(log2 m, g), every Goldilocks plan, prime64.rs:166-177); where the window also leaves the
+// group index compile-time (the lanes' bits lie below the window: lo >= LOGT, the first forward / last inverse
+// window) the multiply is a shift (Goldilocks::mul_pow2) instead of a table load and a four-limb product.
 template <class G, bool FWD, class Mod, bool SUB = false>
 __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w, const u64* __restrict__ tw,
                                                    const Mod& mod, uint32_t twc = 1) {
@@ -73,6 +79,21 @@ __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w,
     for (int r0 = 0; r0 < G::E; ++r0) {
       if (r0 & half) continue;
       const int r1 = r0 | half;
+      if (std::is_same<Mod, Goldilocks>::value && !SUB && m < 32 && lo >= G::LOGT) {
+        const int s_ref = G::LOGN - 1 - b, ex = tower_exp(FWD, s_ref, r0 >> (rb + 1));  // (t >> lo) == 0 here
+        bool ng;
+        if (FWD) {
+          const u64 z = Goldilocks::mul_pow2(x[r1], ex, ng);
+          const u64 a = x[r0];
+          x[r0] = ng ? Goldilocks::sub(a, z) : Goldilocks::add(a, z);
+          x[r1] = ng ? Goldilocks::add(a, z) : Goldilocks::sub(a, z);
+        } else {  // (a - b) w = (b - a) |w| for a negative w
+          const u64 a = x[r0], bb = x[r1];
+          x[r0] = Goldilocks::add(a, bb);
+          x[r1] = Goldilocks::mul_pow2(ex >= 96 ? Goldilocks::sub(bb, a) : Goldilocks::sub(a, bb), ex, ng);
+        }
+        continue;
+      }
       const u64 wv = tw[(SUB ? m * twc : m) + (tpart | (r0 >> (rb + 1)))];
       if (FWD) {
         const u64 z1w = mod.mul(x[r1], wv);

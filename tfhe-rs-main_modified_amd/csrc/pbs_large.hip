@@ -219,6 +219,11 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
       st[k] = closest_abs_nonnative(sg[k] ? P - x : x, sh.base_log, (int)sh.level) >> shift;
     }
   }
+  u64 tv[ONLY ? RPT : 1];  // the block twist of the lane's phase-B rows: the same for every level
+  if constexpr (ONLY) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) tv[k] = twist[Rw::b(W, k) * cols + col];
+  }
 #pragma unroll 1
   for (uint32_t li = 0; li < sh.level; ++li) {
     u64 x[RPT];
@@ -232,12 +237,11 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
     tile::exchange<K, W, true>(x, lds, c);
     tile::phase_b<K, true, W>(x);
     u64* o = dp + (uint64_t)li * per;
-    const u64* tws = twist;  // opaque per level: the twist loads stay in the loop (not 2^K / 4 live values across it)
-    if (ONLY) asm volatile("" : "+s"(tws));
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::b(W, k) * cols + col;
-      o[e] = ONLY ? Goldilocks::mul(x[k], tws[e]) : x[k];
+      if constexpr (ONLY) o[e] = Goldilocks::mul(x[k], tv[k]);
+      else o[e] = x[k];
     }
   }
 }
