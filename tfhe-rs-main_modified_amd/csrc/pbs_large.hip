@@ -374,8 +374,9 @@ struct Acc128 {
   __device__ __forceinline__ void mac(u64 x, u64 w) {
     const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
     uint64_t c0, c1, c2, c3, junk;
-    // every carry is read >= 3 instructions after the mad that wrote it (VALU-written SGPR -> VALU read)
-    asm volatile(
+    // every carry is read >= 3 instructions after the mad that wrote it (VALU-written SGPR -> VALU read); not volatile:
+    // the block has no side effect beyond its outputs, so the compiler may schedule the loads around it
+    asm(
         "v_mad_u64_u32 %[a0], %[c0], %[x0], %[w0], %[a0]\n\t"
         "v_mad_u64_u32 %[a32], %[c1], %[x0], %[w1], %[a32]\n\t"
         "v_mad_u64_u32 %[a64], %[c3], %[x1], %[w1], %[a64]\n\t"
@@ -404,14 +405,17 @@ struct Acc128 {
   }
 };
 
-template <int KP1>
+// LEVEL > 0: the level count is compile-time (the shortint shapes' 1 - 3), so the level loop unrolls and every load of
+// the item is issued before the first product; LEVEL = 0 reads it from sh
+template <int KP1, int LEVEL>
 __global__ __launch_bounds__(256) void large_mac_cols(u64* __restrict__ y, const u64* __restrict__ digits,
                                                       const u64* __restrict__ ggsw_list, uint32_t batch,
                                                       LargeShape sh, u64 n_inv, const uint32_t* __restrict__ gidx,
                                                       uint32_t n_ggsw) {
   const uint32_t e = (blockIdx.x * 256 + threadIdx.x) * 2;
+  const uint32_t level = LEVEL ? (uint32_t)LEVEL : sh.level;
   const uint64_t n = sh.n, per = KP1 * n;
-  const uint64_t ggsw_len = (uint64_t)sh.level * KP1 * per;
+  const uint64_t ggsw_len = (uint64_t)level * KP1 * per;
   for (uint32_t b = blockIdx.y; b < batch; b += gridDim.y) {
     const u64* G = ggsw_list + e;
     if (gidx) {
@@ -419,9 +423,10 @@ __global__ __launch_bounds__(256) void large_mac_cols(u64* __restrict__ y, const
       if (g >= n_ggsw) continue;
       G += (uint64_t)g * ggsw_len;
     }
-    const u64* d = digits + (uint64_t)b * sh.level * per + e;
+    const u64* d = digits + (uint64_t)b * level * per + e;
     Acc128 acc[KP1][2];
-    for (uint32_t li = 0; li < sh.level; ++li) {
+#pragma unroll
+    for (uint32_t li = 0; li < level; ++li) {
 #pragma unroll
       for (int r = 0; r < KP1; ++r) {
         const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + ((uint64_t)li * KP1 + r) * n);
@@ -448,14 +453,22 @@ inline hipError_t launch_large_mac(u64* y, const u64* digits, const u64* ggsw_li
   const bool aligned = (((uintptr_t)y | (uintptr_t)digits | (uintptr_t)ggsw_list) & 15) == 0;
   if (sh.k <= 3 && sh.n >= 512 && aligned) {
     const dim3 grid(sh.n / 512, std::min<uint32_t>(batch, 65535));
-#define MI_MAC_COLS(KP)                                                                                            \
-  hipLaunchKernelGGL(large_mac_cols<KP>, grid, dim3(256), 0, s, y, digits, ggsw_list, batch, sh, n_inv, gidx, n_ggsw)
+#define MI_MAC_COLS(KP, L) \
+  hipLaunchKernelGGL((large_mac_cols<KP, L>), grid, dim3(256), 0, s, y, digits, ggsw_list, batch, sh, n_inv, gidx, n_ggsw)
+#define MI_MAC_K(KP)                                  \
+  switch (sh.level) {                                 \
+    case 1: MI_MAC_COLS(KP, 1); break;                \
+    case 2: MI_MAC_COLS(KP, 2); break;                \
+    case 3: MI_MAC_COLS(KP, 3); break;                \
+    default: MI_MAC_COLS(KP, 0); break;               \
+  }
     switch (sh.k) {
-      case 0: MI_MAC_COLS(1); break;
-      case 1: MI_MAC_COLS(2); break;
-      case 2: MI_MAC_COLS(3); break;
-      default: MI_MAC_COLS(4); break;
+      case 0: MI_MAC_K(1); break;
+      case 1: MI_MAC_K(2); break;
+      case 2: MI_MAC_K(3); break;
+      default: MI_MAC_K(4); break;
     }
+#undef MI_MAC_K
 #undef MI_MAC_COLS
   } else {
     const uint64_t elems = (uint64_t)batch * (sh.k + 1) * sh.n;
