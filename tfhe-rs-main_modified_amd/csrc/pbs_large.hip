@@ -364,6 +364,8 @@ __global__ __launch_bounds__(256) void large_mac(u64* __restrict__ y, const u64*
 // instead of k + 1 times (the digits are (level + 1) / 2 of the step's HBM bytes at k = 1), and the level (k + 1)
 // terms of a column are summed as 128-bit products with one reduction at the end (2^128 = -2^32 mod p).  A thread
 // takes two adjacent coefficients (16-byte accesses).  Grid: x over coefficient pairs, y over the items.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 // The sum of a column's level (k + 1) products without a carry chain per product: each term's four 32 x 32 partial
 // products go straight into three 64-bit column accumulators (bits 0, 32 and 64 up) through v_mad_u64_u32's own
 // addend, their carries out of the accumulator counted apart: 8 VALU per term instead of a 128-bit product (4 mads plus
@@ -425,24 +427,46 @@ __global__ __launch_bounds__(256) void large_mac_cols(u64* __restrict__ y, const
     }
     const u64* d = digits + (uint64_t)b * level * per + e;
     Acc128 acc[KP1][2];
+    if constexpr (LEVEL > 0) {
+      // all of the item's digit pairs first (the HBM loads in flight together), then the products with the GGSW
+      // rows (L2)
+      u64x2 x[LEVEL][KP1];
 #pragma unroll
-    for (uint32_t li = 0; li < level; ++li) {
+      for (int li = 0; li < LEVEL; ++li)
 #pragma unroll
-      for (int r = 0; r < KP1; ++r) {
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + ((uint64_t)li * KP1 + r) * n);
+        for (int r = 0; r < KP1; ++r)
+          // digits are read once: non-temporal, so the stream does not evict the GGSW rows every item re-reads
+          x[li][r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(d + ((uint64_t)li * KP1 + r) * n));
 #pragma unroll
-        for (int c = 0; c < KP1; ++c) {
-          const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(G + (((uint64_t)li * KP1 + r) * KP1 + c) * n);
-          acc[c][0].mac(x.x, w.x);
-          acc[c][1].mac(x.y, w.y);
+      for (int li = 0; li < LEVEL; ++li)
+#pragma unroll
+        for (int r = 0; r < KP1; ++r)
+#pragma unroll
+          for (int c = 0; c < KP1; ++c) {
+            const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(G + (((uint64_t)li * KP1 + r) * KP1 + c) * n);
+            acc[c][0].mac(x[li][r].x, w.x);
+            acc[c][1].mac(x[li][r].y, w.y);
+          }
+    } else {
+      for (uint32_t li = 0; li < level; ++li) {
+#pragma unroll
+        for (int r = 0; r < KP1; ++r) {
+          const u64x2 x = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(d + ((uint64_t)li * KP1 + r) * n));
+#pragma unroll
+          for (int c = 0; c < KP1; ++c) {
+            const ulonglong2 w = *reinterpret_cast<const ulonglong2*>(G + (((uint64_t)li * KP1 + r) * KP1 + c) * n);
+            acc[c][0].mac(x.x, w.x);
+            acc[c][1].mac(x.y, w.y);
+          }
         }
       }
     }
     u64* out = y + (uint64_t)b * per + e;
 #pragma unroll
-    for (int c = 0; c < KP1; ++c)
-      *reinterpret_cast<ulonglong2*>(out + (uint64_t)c * n) =
-          make_ulonglong2(acc[c][0].value(n_inv), acc[c][1].value(n_inv));
+    for (int c = 0; c < KP1; ++c) {
+      const u64x2 v = {acc[c][0].value(n_inv), acc[c][1].value(n_inv)};
+      __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(out + (uint64_t)c * n));
+    }
   }
 }
 
