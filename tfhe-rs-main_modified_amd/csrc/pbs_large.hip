@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
     for (int r = 0; r < R; ++r) {
       u64 v = x[r];
       if (ONLY) v = gl.mul(v, tws[j + r * cols]);
-      o[r * cols] = v;
+      __builtin_nontemporal_store(v, o + r * cols);  // the digits are read once, by the next pass
     }
   }
 }
@@ -240,8 +240,9 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::b(W, k) * cols + col;
-      if constexpr (ONLY) o[e] = Goldilocks::mul(x[k], tv[k]);
-      else o[e] = x[k];
+      // the digits are read once, by the next pass: non-temporal
+      if constexpr (ONLY) __builtin_nontemporal_store(Goldilocks::mul(x[k], tv[k]), o + e);
+      else __builtin_nontemporal_store(x[k], o + e);
     }
   }
 }
