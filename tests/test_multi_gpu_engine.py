@@ -65,6 +65,30 @@ def _host(t):
 
 
 @pytest.mark.gpu
+def test_device_set_gather_waits_for_the_caller_stream(engine):
+    """mi_multi_gpu_gather's copies are ordered after the work already queued on the caller's stream (the header's
+    contract): a zero-fill of the destination queued behind a long transform loop on that stream must land before
+    the gathered shards, not over them (r4: the gather used to start its copies at once, and a zero-fill still queued
+    on the caller stream could overwrite them; seen once in test_device_set_pbs_scatter_gather)."""
+    import torch
+    ds = engine.multi_gpu.DeviceSet([0, 0, 0])
+    g = H.rng(4242)
+    total, width = 7, 33
+    shards_h = [H.uniform_u64(g, (b - a, width)) for a, b in (ds.shard(total, i) for i in range(3))]
+    shards = [_dev(x) for x in shards_h]
+    torch.cuda.synchronize()
+    plan = engine.Plan.try_new(N, P)
+    busy = torch.zeros((8192, N), dtype=torch.int64, device="cuda")
+    dst = torch.full((total, width), 7, dtype=torch.int64, device="cuda")
+    for _ in range(20):  # ~2 ms of work queued on the caller (current) stream ahead of the zero-fill
+        plan.fwd(busy)
+    dst.zero_()
+    ds.gather(dst, shards)
+    torch.cuda.synchronize()
+    assert np.array_equal(_host(dst), np.concatenate(shards_h))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("entries,batch", [(2, 9), (3, 10), (3, 2)])
 def test_device_set_pbs_scatter_gather(engine, oracle, entries, batch):
     import torch

@@ -203,7 +203,11 @@ int mi_multi_gpu_gather(mi_multi_gpu* m, void* dst, const void* const* srcs, siz
     char* to = (char*)dst + off * unit_bytes;
     DeviceGuard g(m->devices[i]);
     hipError_t e = hipSuccess;
-    if (srcs[i] != to) e = hipMemcpyPeerAsync(to, m->devices[0], srcs[i], m->devices[i], n * unit_bytes, m->streams[i]);
+    // the copy into dst waits for the work already queued on `stream` (whatever produced or cleared dst there: without
+    // this a zero-fill of dst queued on `stream` could land after the copy, GPU test test_device_set_pbs_scatter_gather)
+    if (srcs[i] != to) e = after(m->streams[i], (hipStream_t)stream, m->events[0], m->devices[0]);
+    if (srcs[i] != to && e == hipSuccess)
+      e = hipMemcpyPeerAsync(to, m->devices[0], srcs[i], m->devices[i], n * unit_bytes, m->streams[i]);
     if (e == hipSuccess) e = after((hipStream_t)stream, m->streams[i], m->events[i], m->devices[i]);
     if (e != hipSuccess) return hip_fail(e, "gather copy");
   }
