@@ -361,6 +361,12 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
   const int t = logn - 11;
   if (t < 1 || t > 10) return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
+  // t <= 3, the whole transform, no accumulation: top stages and bodies in one launch, one workgroup per polynomial.
+  // Not inside the blind rotation (skip_first / acc): at its batch (one or two generations of workgroups) the fused
+  // form's memory phase and body phase do not overlap across workgroups and measured slower.
+  if (t <= 3 && !skip_first && !acc && split_fused_enabled())
+    return launch_ntt_split_fused(fwd, t, data, batch, stride, fwd ? st.blk_fwd : st.blk_inv,
+                                  fwd ? st.body_fwd : st.body_inv, s);
   // the top passes put polynomials on grid.y (<= 65535 per launch); passes of <= 5 stages, balanced
   const int passes = (t + 4) / 5;
   int ks[2] = {(t + passes - 1) / passes, t - (t + passes - 1) / passes};

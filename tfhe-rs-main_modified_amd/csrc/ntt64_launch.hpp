@@ -45,6 +45,11 @@ struct SplitTw {
 // tw = the N plan's forward (fwd) or inverse (inv) twiddle table; data: batch polynomials `stride` u64 apart
 // acc (inverse only): the last top pass accumulates its output into acc (same layout as data) instead of storing it,
 // acc_mode 1 = BNF (acc += modswitch p -> 2^64), 2 = Solinas (acc = acc + x mod p); data then holds an intermediate
+// the split transform of N = 2^(11 + t), t <= 3, as one launch (ntt64_tw.hip ntt_tw_fused_kernel): blk = the block
+// twist (SplitTw blk_fwd / blk_inv), body_tab = the 2048 body's table (body_fwd / body_inv)
+hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch, size_t stride, const uint64_t* blk,
+                                  const uint64_t* body_tab, hipStream_t s);
+bool split_fused_enabled();  // MI_SPLIT_FUSED=0 in the environment: the two-launch form (A/B)
 hipError_t launch_ntt_split(bool fwd, int logn, uint64_t* data, size_t batch, size_t stride, const uint64_t* tw,
                             const SplitTw& st, hipStream_t s, uint64_t* acc = nullptr, int acc_mode = 0,
                             bool skip_first = false);

@@ -28,19 +28,19 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "ntt64_tw_tables.hpp"
-#include "ntt64_tw_body.hpp"
+#include "ntt64_tw_device.hpp"
 
 namespace mi {
 namespace tw {
 
 // ---- whole-body asm kernel (tools/gen_tw_kernel.py) ----------------------------------------------
-// The generated body owns v8..v127 / s20..s99 and performs load -> all stages -> store itself; this
-// wrapper only derives the wave's polynomial and the per-lane LDS / global addresses.
-static constexpr int WAVE_LDS2 = 1088;  // u64: max(32 x 34, 16 x 66)
+// The generated body owns v8..v127 / s20..s99 and performs load -> all stages -> store itself; the wrappers
+// (ntt64_tw_device.hpp tw_body) only derive the wave's polynomial and the per-lane LDS / global addresses.
 
 // Waves per workgroup, measured (tools/variant_probe.hip: same process, rotated order, identical-body controls):
 // the forward runs best with one wave per group (a finished wave frees its slot and its 8.5 KiB of LDS at once:
@@ -63,30 +63,80 @@ __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* 
   const uint32_t poly = blockIdx.x * W + wv;
   if (poly >= batch) return;
   u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
+  tw_body<FWD>(p, twist, (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2), lane);
+}
+
+// ---- the split transform of N = 2^(11 + T), T <= 3, in one launch ------------------------------------------------
+// One workgroup of 2^T waves per polynomial.  Forward: the T top stages (stage 0 on: the Solinas tower's powers of
+// two, Goldilocks::mul_pow2) on the 2048 columns of 2^T rows and the block twist (element e times blk[e]), stored;
+// a workgroup barrier; then wave w runs the 2048 body on block w.  Inverse: the bodies, a barrier, then the block
+// untwist and the T stages (GS, reverse order) on the columns, stored.  The same arithmetic as
+// ntt_top_kernel<T, FWD, Goldilocks, u64, TWIST, 0, true> at s0 = 0 followed / preceded by ntt_tw_body_kernel with
+// sub_log = T (bit-exact), but the polynomial crosses HBM once: the intermediate is written and re-read by the same
+// workgroup, from L2 / the memory-side cache.  A lane holds 32 / 2^T columns x 2^T rows = 32 values (T = 3: two
+// calls of 2 columns, within 128 VGPRs).
+template <int T, bool FWD>
+__device__ __forceinline__ void fused_columns(u64* __restrict__ poly, const u64* __restrict__ blk, uint32_t tid,
+                                              int c0) {
+  constexpr int R = 1 << T, CPL = T == 3 ? 2 : 32 >> T, THREADS = 64 << T;  // CPL: columns of this call
+  u64 x[CPL][R];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t e = (uint32_t)(i * 2048 + (c0 + c) * THREADS) + tid;
+      x[c][i] = FWD ? poly[e] : Goldilocks::mul(poly[e], blk[e]);
+    }
+#pragma unroll
+  for (int st = 0; st < T; ++st) {
+    const int s = FWD ? st : T - 1 - st;  // stage s: 2^s groups, pair distance 2^(T-1-s) in i
+    const int d = 1 << (T - 1 - s);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if (i & d) continue;
+        const int ex = tower_exp(FWD, s, i >> (T - s));
+        bool ng;
+        if (FWD) {
+          const u64 z = Goldilocks::mul_pow2(x[c][i + d], ex, ng);
+          const u64 a = x[c][i];
+          x[c][i] = ng ? Goldilocks::sub(a, z) : Goldilocks::add(a, z);
+          x[c][i + d] = ng ? Goldilocks::add(a, z) : Goldilocks::sub(a, z);
+        } else {  // (a - b) w = (b - a) |w| for a negative w
+          const u64 a = x[c][i], b = x[c][i + d];
+          x[c][i] = Goldilocks::add(a, b);
+          x[c][i + d] = Goldilocks::mul_pow2(ex >= 96 ? Goldilocks::sub(b, a) : Goldilocks::sub(a, b), ex, ng);
+        }
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t e = (uint32_t)(i * 2048 + (c0 + c) * THREADS) + tid;
+      poly[e] = FWD ? Goldilocks::mul(x[c][i], blk[e]) : x[c][i];
+    }
+}
+
+template <int T, bool FWD>
+__global__ __launch_bounds__(64 << T) __attribute__((amdgpu_waves_per_eu(4))) void ntt_tw_fused_kernel(
+    u64* __restrict__ data, uint64_t stride, const u64* __restrict__ blk, const u64* __restrict__ body_tab) {
+  __shared__ u64 lds[(1 << T) * WAVE_LDS2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  u64* poly = data + (uint64_t)blockIdx.x * stride;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
-  const uint32_t par = lane & 1, i = lane >> 1;
-  const uint32_t l8 = lane * 8;
-  const uint32_t t1w = S + (lane & 31) * 8;
-  const uint32_t t1r = S + (i * 34 + par) * 8;
-  const uint32_t lwo = par * 128;
-  const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
-  const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
-  // forward: the lane-pair twiddles follow the twist rows; inverse: the last-DIT-stage table, two regions on
-  // (the plan's allocation: [fwd + 32 | inverse + 32 | inverse N^-1 + 32 | 32], `twist` = the inverse region)
-  const u64* lw = FWD ? twist + 2048 : twist + 2 * (2048 + 32);
   if constexpr (FWD) {
-    const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
-    const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
-    const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
-    MI_TW_BODY_FWD([g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw),
-                   [l8] "v"(l8), [t1w] "v"(t1w), [t1r] "v"(t1r), [t2wl] "v"(t2wl), [t2wh] "v"(t2wh),
-                   [t2r] "v"(t2r), [lwo] "v"(lwo));
+    fused_columns<T, true>(poly, blk, tid, 0);
+    if constexpr (T == 3) fused_columns<T, true>(poly, blk, tid, 2);  // two calls: 2 x 16 values (VGPRs)
+    __syncthreads();  // the workgroup's stores are visible to its waves (one CU, one L1)
+    tw_body<true>(poly + wv * 2048, body_tab, S, lane);
   } else {
-    const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
-    const uint32_t t1x = S + (lane + (lane >> 5)) * 8;        // W0 side of the W1'' transposes
-    const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;  // W1'' side
-    MI_TW_BODY_INV([g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw),
-                   [l8] "v"(l8), [t4w] "v"(t4w), [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo));
+    tw_body<false>(poly + wv * 2048, body_tab, S, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the body's stores (inline asm: not tracked by the compiler)
+    __syncthreads();
+    fused_columns<T, false>(poly, blk, tid, 0);
+    if constexpr (T == 3) fused_columns<T, false>(poly, blk, tid, 2);
   }
 }
 
@@ -129,6 +179,41 @@ hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys
   for (size_t off = 0; off < n_polys; off += CHUNK) {
     const uint32_t n = (uint32_t)std::min(CHUNK, n_polys - off);
     hipLaunchKernelGGL(tw::ntt_tw_ms64_kernel, dim3(n), dim3(64), 0, s, dst + off * 2048, src + off * 2048, n, twist);
+  }
+  return hipGetLastError();
+}
+
+template <int T>
+static void fused_launch(bool fwd, uint64_t* d, uint32_t n, size_t stride, const uint64_t* blk, const uint64_t* body_tab,
+                         hipStream_t s) {
+  if (fwd)
+    hipLaunchKernelGGL((tw::ntt_tw_fused_kernel<T, true>), dim3(n), dim3(64 << T), 0, s, d, (uint64_t)stride, blk,
+                       body_tab);
+  else
+    hipLaunchKernelGGL((tw::ntt_tw_fused_kernel<T, false>), dim3(n), dim3(64 << T), 0, s, d, (uint64_t)stride, blk,
+                       body_tab);
+}
+
+bool split_fused_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("MI_SPLIT_FUSED");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch, size_t stride, const uint64_t* blk,
+                                  const uint64_t* body_tab, hipStream_t s) {
+  if (t < 1 || t > 3) return hipErrorInvalidValue;
+  constexpr size_t CHUNK = size_t(1) << 30;
+  for (size_t off = 0; off < batch; off += CHUNK) {
+    const uint32_t n = (uint32_t)std::min(CHUNK, batch - off);
+    uint64_t* d = data + off * stride;
+    switch (t) {
+      case 1: fused_launch<1>(fwd, d, n, stride, blk, body_tab, s); break;
+      case 2: fused_launch<2>(fwd, d, n, stride, blk, body_tab, s); break;
+      default: fused_launch<3>(fwd, d, n, stride, blk, body_tab, s); break;
+    }
   }
   return hipGetLastError();
 }
