@@ -4,7 +4,8 @@ shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/ks_pbs.rs:71-90), b
 (ntt64_bnf_pbs.rs:208-726, ntt64_pbs.rs:213-702):
 
 * key conversion, external product, CMUX (shared and per-item indexed GGSW) and PBS on random keys vs the oracle, bit
-  for bit (N = 65536 and N = 16384, small n);
+  for bit (N = 65536, 16384 and 8192 — the last two through the one-launch rotation + forward and inverse +
+  accumulate kernels of the split transform —, small n);
 * real keys at the full shape: every one of the 256 messages of the padded 4+4-bit space decrypts to f(m) after the
   PBS (lwe_programmable_bootstrapping.rs:708-865, 1002-1163) — BNF with the centered modulus switch the shortint
   parameters use, Solinas with its own switch; and, on the same real key cut to its first 24 GGSWs (the oracle PBS
@@ -33,7 +34,7 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-@pytest.mark.parametrize("n", [16384, 65536])
+@pytest.mark.parametrize("n", [8192, 16384, 65536])
 @pytest.mark.parametrize("bnf", [True, False])
 def test_large_random_keys(engine, oracle, n, bnf):
     q = 0 if bnf else P
@@ -76,6 +77,35 @@ def test_large_random_keys(engine, oracle, n, bnf):
         (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf else
          M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)(dev(lwe), o, dev(lut), key)
         assert np.array_equal(host(o), want), ("pbs", base_log, level)
+
+
+@pytest.mark.parametrize("bnf", [True, False])
+def test_large_pbs_two_lanes(engine, oracle, bnf):
+    """A chunk of >= 64 ciphertexts runs as two lanes (halves on the caller's stream and a pooled side stream, their
+    launches interleaved per CMUX step; pbs_large.hip PBS_LANE_MIN): every output of an odd-split batch of 70 equals
+    the one-lane run (batch 8 < 64) of the same items, and an item of each half equals the oracle bit for bit."""
+    n, k, base_log, level, n_lwe, batch = 8192, 1, 15, 2, 3, 70
+    q = 0 if bnf else P
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    g = H.rng(777 + bnf)
+    bsk = rand_q(g, (n_lwe, level, k + 1, k + 1, n), P)
+    lut = rand_q(g, (k + 1, n), q)
+    lwe = rand_q(g, (batch, n_lwe + 1), q)
+    key = M.NttBootstrapKey(pl, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
+    fn = (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf else
+          M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)
+    o = dev(np.zeros((batch, k * n + 1), np.uint64))
+    fn(dev(lwe), o, dev(lut), key)
+    got = host(o)
+    for lo in (0, 31, 62):  # one lane each, covering the first half, the split point (35) and the second half
+        o8 = dev(np.zeros((8, k * n + 1), np.uint64))
+        fn(dev(lwe[lo:lo + 8]), o8, dev(lut), key)
+        assert np.array_equal(host(o8), got[lo:lo + 8]), lo
+    for b in (0, batch - 1):
+        want = c.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), k, base_log, level, bnf=bnf)
+        assert np.array_equal(got[b], want), b
 
 
 @pytest.mark.parametrize("bnf", [True, False])

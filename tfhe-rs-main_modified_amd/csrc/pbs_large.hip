@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "scratch.hpp"
 #include "mi_arith.hpp"
@@ -593,6 +594,21 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 }  // namespace pbs
 
+// Two lanes: a chunk of >= PBS_LANE_MIN ciphertexts is split in halves, one on the caller's stream and one on a pooled
+// side stream (mi::StreamFork), their launches interleaved step by step.  Each ciphertext's blind rotation is
+// independent, so the halves share nothing but the key, and the GPU overlaps one half's memory-bound launches (the
+// rotation + decomposition pass, the MAC, the accumulating inverse pass) with the other's issue-bound transform bodies.
+// MI_PBS_LANES=1 in the environment: one lane (A/B).
+static constexpr uint32_t PBS_LANE_MIN = 64;
+
+static bool pbs_lanes_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("MI_PBS_LANES");
+    return !(v && v[0] == '1');
+  }();
+  return on;
+}
+
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
                             const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
                             const uint64_t* tw, const uint64_t* itw, int centered, hipStream_t s,
@@ -605,82 +621,107 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   u64 *scratch = nullptr;
   hipError_t e = mi::scratch_alloc((void**)&scratch, (chunk * ((size_t)level + 2) * per + chunk) * sizeof(u64), s);
   if (e != hipSuccess) return e;
-  u64* digits = scratch;
-  u64* y = digits + chunk * level * per;
-  u64* acc = y + chunk * per;
-  u64* corr = acc + chunk * per;
-  for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
-    const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
-    const u64* in = lwe_in + b0 * (n_lwe + 1);
-    const uint64_t elems = (uint64_t)nb * per;
+  int k0 = 0;
+  bool only = false;
+  if (split) split_first_pass(logn, &k0, &only);
+  // one lane's share of a chunk: ciphertexts [b0, b0 + nb) of the batch, its scratch slices, its stream
+  struct Lane {
+    size_t b0;
+    uint32_t nb;
+    hipStream_t st;
+    const u64* in;
+    u64 *digits, *y, *acc, *corr;
+  };
+  auto init = [&](const Lane& L) -> hipError_t {
+    const uint64_t elems = (uint64_t)L.nb * per;
     if (bnf)
-      hipLaunchKernelGGL(large_init_acc<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, io, (uint64_t)b0, in,
-                         (uint32_t)n_lwe, nb, sh);
+      hipLaunchKernelGGL(large_init_acc<true>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.acc, io,
+                         (uint64_t)L.b0, L.in, (uint32_t)n_lwe, L.nb, sh);
     else
-      hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, io, (uint64_t)b0, in,
-                         (uint32_t)n_lwe, nb, sh);
-    int k0 = 0;
-    bool only = false;
-    if (split) split_first_pass(logn, &k0, &only);
-    for (uint32_t i = 0; i < n_lwe && e == hipSuccess; ++i) {
-      if (split) {  // rotation + decomposition + the transform's first pass in one kernel, then the rest of the transform
-        e = bnf ? rotdec_top<true>(k0, only, digits, acc, in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, s)
-                : rotdec_top<false>(k0, only, digits, acc, in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, s);
-        if (e == hipSuccess)
-          e = launch_ntt_split(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, *split, s, nullptr, 0, true);
-        if (e != hipSuccess) break;
-      } else {
-        if (bnf)
-          hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
-                             (uint32_t)n_lwe, i, nb, sh);
-        else
-          hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, s, digits, acc, in,
-                             (uint32_t)n_lwe, i, nb, sh);
-        e = ntt_large(true, logn, digits, (size_t)nb * level * (k + 1), sh.n, tw, split, s);
-        if (e != hipSuccess) break;
-      }
-      e = launch_large_mac(y, digits, bsk + (size_t)i * ggsw_len, nb, sh, (u64)0, nullptr, 1u, s);
-      if (e != hipSuccess) break;
-      if (split) {  // the inverse's last pass accumulates into acc itself (launch_ntt_split acc_mode)
-        e = launch_ntt_split(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, *split, s, acc, bnf ? 1 : 2);
-        continue;
-      }
-      e = ntt_large(false, logn, y, (size_t)nb * (k + 1), sh.n, itw, split, s);
-      if (e != hipSuccess) break;
+      hipLaunchKernelGGL(large_init_acc<false>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.acc, io,
+                         (uint64_t)L.b0, L.in, (uint32_t)n_lwe, L.nb, sh);
+    return hipGetLastError();
+  };
+  auto step = [&](const Lane& L, uint32_t i) -> hipError_t {  // CMUX step i of the lane's blind rotations
+    const uint32_t nb = L.nb;
+    const uint64_t elems = (uint64_t)nb * per;
+    hipError_t e;
+    if (split) {  // rotation + decomposition + the transform's first pass in one kernel, then the rest of the transform
+      e = bnf ? rotdec_top<true>(k0, only, L.digits, L.acc, L.in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, L.st)
+              : rotdec_top<false>(k0, only, L.digits, L.acc, L.in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, L.st);
+      if (e == hipSuccess)
+        e = launch_ntt_split(true, logn, L.digits, (size_t)nb * level * (k + 1), sh.n, tw, *split, L.st, nullptr, 0,
+                             true);
+    } else {
       if (bnf)
-        hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, y, nb, sh,
-                           (const uint32_t*)nullptr, 1u);
+        hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.digits, L.acc,
+                           L.in, (uint32_t)n_lwe, i, nb, sh);
       else
-        hipLaunchKernelGGL(large_accumulate<false>, dim3(blocks_for(elems)), dim3(256), 0, s, acc, y, nb, sh,
-                           (const uint32_t*)nullptr, 1u);
-      e = hipGetLastError();
+        hipLaunchKernelGGL(large_rotate_decompose<false>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.digits, L.acc,
+                           L.in, (uint32_t)n_lwe, i, nb, sh);
+      e = ntt_large(true, logn, L.digits, (size_t)nb * level * (k + 1), sh.n, tw, split, L.st);
     }
-    if (e != hipSuccess) break;
+    if (e == hipSuccess) e = launch_large_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, sh, (u64)0, nullptr, 1u, L.st);
+    if (e != hipSuccess) return e;
+    if (split)  // the inverse's last pass accumulates into acc itself (launch_ntt_split acc_mode)
+      return launch_ntt_split(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, *split, L.st, L.acc, bnf ? 1 : 2);
+    e = ntt_large(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, split, L.st);
+    if (e != hipSuccess) return e;
+    if (bnf)
+      hipLaunchKernelGGL(large_accumulate<true>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.acc, L.y, nb, sh,
+                         (const uint32_t*)nullptr, 1u);
+    else
+      hipLaunchKernelGGL(large_accumulate<false>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.acc, L.y, nb, sh,
+                         (const uint32_t*)nullptr, 1u);
+    return hipGetLastError();
+  };
+  auto finish = [&](const Lane& L) -> hipError_t {  // body correction, final rotation + extraction
+    const uint32_t nb = L.nb;
     const bool corr_on = bnf && centered;
     if (corr_on)
-      hipLaunchKernelGGL(large_body_correction, dim3(nb), dim3(256), 0, s, corr, in, (uint32_t)n_lwe,
+      hipLaunchKernelGGL(large_body_correction, dim3(nb), dim3(256), 0, L.st, L.corr, L.in, (uint32_t)n_lwe,
                          (unsigned)(logn + 1));
-    const u64* cr = corr_on ? corr : (const u64*)nullptr;
+    const u64* cr = corr_on ? L.corr : (const u64*)nullptr;
     if (io.glwe_out) {
       const uint64_t outs = (uint64_t)nb * per;
-      u64* o = io.glwe_out + b0 * per;
+      u64* o = io.glwe_out + L.b0 * per;
       if (bnf)
-        hipLaunchKernelGGL((large_extract<true, true>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
-                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+        hipLaunchKernelGGL((large_extract<true, true>), dim3(blocks_for(outs)), dim3(256), 0, L.st, o, L.acc, L.in, cr,
+                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)L.b0);
       else
-        hipLaunchKernelGGL((large_extract<false, true>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
-                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+        hipLaunchKernelGGL((large_extract<false, true>), dim3(blocks_for(outs)), dim3(256), 0, L.st, o, L.acc, L.in,
+                           cr, (uint32_t)n_lwe, nb, sh, io, (uint64_t)L.b0);
     } else {
       const uint64_t outs = (uint64_t)nb * ((uint64_t)k * sh.n + 1);
-      u64* o = out + b0 * ((size_t)k * sh.n + 1);
+      u64* o = out + L.b0 * ((size_t)k * sh.n + 1);
       if (bnf)
-        hipLaunchKernelGGL((large_extract<true, false>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
-                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+        hipLaunchKernelGGL((large_extract<true, false>), dim3(blocks_for(outs)), dim3(256), 0, L.st, o, L.acc, L.in,
+                           cr, (uint32_t)n_lwe, nb, sh, io, (uint64_t)L.b0);
       else
-        hipLaunchKernelGGL((large_extract<false, false>), dim3(blocks_for(outs)), dim3(256), 0, s, o, acc, in, cr,
-                           (uint32_t)n_lwe, nb, sh, io, (uint64_t)b0);
+        hipLaunchKernelGGL((large_extract<false, false>), dim3(blocks_for(outs)), dim3(256), 0, L.st, o, L.acc, L.in,
+                           cr, (uint32_t)n_lwe, nb, sh, io, (uint64_t)L.b0);
     }
-    e = hipGetLastError();
+    return hipGetLastError();
+  };
+  for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
+    const uint32_t nb = (uint32_t)std::min(chunk, batch - c0);
+    mi::StreamFork fork;
+    int lanes = 1;
+    if (nb >= PBS_LANE_MIN && pbs_lanes_enabled() && fork.fork(s) == hipSuccess) lanes = 2;
+    Lane L[2];
+    for (int j = 0, off = 0; j < lanes; ++j) {
+      const uint32_t n = lanes == 1 ? nb : (j == 0 ? (nb + 1) / 2 : nb / 2);
+      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(), lwe_in + (c0 + off) * (n_lwe + 1),
+                  scratch + (size_t)off * level * per, scratch + chunk * level * per + (size_t)off * per,
+                  scratch + chunk * (level + 1) * per + (size_t)off * per, scratch + chunk * (level + 2) * per + off};
+      off += (int)n;
+    }
+    for (int j = 0; j < lanes && e == hipSuccess; ++j) e = init(L[j]);
+    for (uint32_t i = 0; i < n_lwe && e == hipSuccess; ++i)
+      for (int j = 0; j < lanes && e == hipSuccess; ++j) e = step(L[j], i);
+    for (int j = 0; j < lanes && e == hipSuccess; ++j) e = finish(L[j]);
+    const hipError_t ej = fork.join();  // the caller's stream after the side lane (also on error: scratch ordering)
+    if (e == hipSuccess) e = ej;
   }
   const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;

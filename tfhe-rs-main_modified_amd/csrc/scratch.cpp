@@ -28,6 +28,48 @@ Pool& pool() {
   return *p;
 }
 
+struct SidePool {
+  std::mutex mu;
+  std::vector<std::pair<int, hipStream_t>> idle;  // (device, stream)
+};
+
+SidePool& side_pool() {
+  static SidePool* p = new SidePool;  // never destroyed, as pool()
+  return *p;
+}
+
+// an idle side stream of `dev`, or a new non-blocking one
+hipError_t side_acquire(int dev, hipStream_t* out) {
+  SidePool& P = side_pool();
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.idle.begin(); it != P.idle.end(); ++it)
+      if (it->first == dev) {
+        *out = it->second;
+        P.idle.erase(it);
+        return hipSuccess;
+      }
+  }
+  return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+}
+
+void side_release(int dev, hipStream_t st) {
+  SidePool& P = side_pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.idle.emplace_back(dev, st);
+}
+
+// one event recorded on `from` and waited on by `to` (the event may be destroyed at once: the wait holds it)
+hipError_t order_after(hipStream_t to, hipStream_t from) {
+  hipEvent_t ev;
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(ev, from);
+  if (e == hipSuccess) e = hipStreamWaitEvent(to, ev, 0);
+  (void)hipEventDestroy(ev);
+  return e;
+}
+
 constexpr size_t GRAIN = (size_t)1 << 20;  // blocks are whole MiB
 
 // frees blocks that no longer have a pending user (their event has completed)
@@ -140,6 +182,31 @@ size_t scratch_trim(int device) {
   for (const Block& b : out) bytes += b.bytes;
   release(out);
   return bytes;
+}
+
+hipError_t StreamFork::fork(hipStream_t s) {
+  if (forked_) return hipErrorInvalidValue;
+  hipError_t e = hipGetDevice(&device_);
+  if (e == hipSuccess) e = side_acquire(device_, &side_);
+  if (e != hipSuccess) return e;
+  if ((e = order_after(side_, s)) != hipSuccess) {
+    side_release(device_, side_);
+    side_ = nullptr;
+    return e;
+  }
+  caller_ = s;
+  forked_ = true;
+  return hipSuccess;
+}
+
+hipError_t StreamFork::join() {
+  if (!forked_) return hipSuccess;
+  hipError_t e = order_after(caller_, side_);
+  if (e != hipSuccess) (void)hipStreamSynchronize(side_);  // cannot order by event: drain the side stream instead
+  side_release(device_, side_);
+  side_ = nullptr;
+  forked_ = false;
+  return e;
 }
 
 size_t scratch_bytes(int device) {

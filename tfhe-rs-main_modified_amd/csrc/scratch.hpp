@@ -22,4 +22,24 @@ size_t scratch_trim(int device);
 // bytes held by the pool on `device` (idle + in use)
 size_t scratch_bytes(int device);
 
+// A pooled non-blocking side stream of the current device, for an entry point that splits its batch over the
+// caller's stream and one more (pbs_large.hip): fork() orders the side stream after the work already queued on the
+// caller's stream, join() orders the caller's stream after everything queued on the side stream and returns the side
+// stream to the pool.  No host synchronisation either way (events only).
+class StreamFork {
+ public:
+  StreamFork() = default;
+  StreamFork(const StreamFork&) = delete;
+  StreamFork& operator=(const StreamFork&) = delete;
+  ~StreamFork() { (void)join(); }
+  hipError_t fork(hipStream_t s);
+  hipError_t join();
+  hipStream_t side() const { return side_; }
+
+ private:
+  hipStream_t caller_ = nullptr, side_ = nullptr;
+  int device_ = 0;
+  bool forked_ = false;
+};
+
 }  // namespace mi
