@@ -257,6 +257,30 @@ def test_generic_pbs_shortint_shapes_real_keys(engine, oracle, name):
         assert key3.serialize(True) == buf
 
 
+@pytest.mark.parametrize("n", [4096, 8192])
+def test_generic_pbs_two_lanes(engine, n):
+    """A chunk of >= 64 ciphertexts runs as two lanes (halves on the caller's stream and a pooled side stream,
+    fft64_generic.hip FFTG_LANE_MIN): every output of an odd-split batch of 70 equals, bit for bit, the one-lane run
+    (batch 8 < 64) of the same items — each item's f64 arithmetic is independent of where the batch is cut."""
+    import torch
+    k, level, base_log, n_lwe, batch = 1, 2, 12, 3, 70
+    fft = engine.fft64.Fft(n)
+    g = H.rng(8100 + n)
+    bsk = H.uniform_u64(g, (n_lwe, level, k + 1, k + 1, n))
+    fbsk = torch.zeros((n_lwe, level, k + 1, k + 1, n // 2, 2), dtype=torch.float64, device="cuda")
+    engine.fft64.convert_standard_lwe_bootstrap_key_to_fourier(dev(bsk), fbsk, fft)
+    key = engine.fft64.FourierLweBootstrapKey(fbsk, base_log, level, fft)
+    lut = H.uniform_u64(g, (k + 1, n))
+    lwe = H.uniform_u64(g, (batch, n_lwe + 1))
+    out = dev(np.zeros((batch, k * n + 1), np.uint64))
+    engine.fft64.programmable_bootstrap_lwe_ciphertext(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    for lo in (0, 31, 62):  # the first half, across the split point (35), the second half
+        o8 = dev(np.zeros((8, k * n + 1), np.uint64))
+        engine.fft64.programmable_bootstrap_lwe_ciphertext(dev(lwe[lo:lo + 8]), o8, dev(lut), key)
+        assert np.array_equal(host(o8), got[lo:lo + 8]), lo
+
+
 def test_generic_errors(engine):
     M_ = engine.fft64
     for bad in (16, 1 << 19):

@@ -34,6 +34,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "scratch.hpp"
 #include "fft64_device.hpp"
@@ -693,6 +694,19 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
   return e != hipSuccess ? e : ef;
 }
 
+// Two lanes, as launch_pbs_large (pbs_large.hip): a chunk of >= FFTG_LANE_MIN ciphertexts is split in halves on the
+// caller's stream and a pooled side stream (mi::StreamFork), launches interleaved step by step, so one half's
+// memory-bound passes overlap the other's transform rows.  MI_PBS_LANES=1 in the environment: one lane.
+static constexpr uint32_t FFTG_LANE_MIN = 64;
+
+static bool fftg_lanes_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("MI_PBS_LANES");
+    return !(v && v[0] == '1');
+  }();
+  return on;
+}
+
 hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftGenTables& t,
                            hipStream_t s) {
@@ -707,38 +721,67 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const P
   cplx* scratch = nullptr;
   hipError_t e = mi::scratch_alloc((void**)&scratch, (dig + prod) * sizeof(cplx) + (acc_u64 + chunk) * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
-  cplx* d = scratch;
-  cplx* y = g.logr ? scratch + dig : nullptr;
-  uint64_t* acc = reinterpret_cast<uint64_t*>(scratch + dig + prod);
-  uint64_t* corr = acc + acc_u64;
+  cplx* d_all = scratch;
+  cplx* y_all = g.logr ? scratch + dig : nullptr;
+  uint64_t* acc_all = reinterpret_cast<uint64_t*>(scratch + dig + prod);
+  uint64_t* corr_all = acc_all + acc_u64;
   const cplx* key = reinterpret_cast<const cplx*>(fbsk);
   const size_t ggsw_len = ((size_t)lv * kp1 * kp1) << g.logm;  // complex per GGSW
-  for (size_t b0 = 0; b0 < batch && e == hipSuccess; b0 += chunk) {
-    const uint32_t nb = (uint32_t)std::min(chunk, batch - b0);
-    const uint64_t* in = lwe_in + b0 * (n_lwe + 1);
-    if (ms_mode == 1)
-      hipLaunchKernelGGL(body_correction_kernel, dim3(nb), dim3(256), 0, s, corr, in, (uint32_t)n_lwe, g.logn + 1);
-    hipLaunchKernelGGL(init_acc_kernel, dim3(blocks_for((uint64_t)nb * per)), dim3(256), 0, s, acc, io, (uint64_t)b0,
-                       in, ms_mode == 1 ? (const uint64_t*)corr : nullptr, (uint32_t)n_lwe, nb, g.logn, kp1, ms_mode);
-    if ((e = hipGetLastError()) != hipSuccess) break;
-    for (uint32_t i = 0; i < (uint32_t)n_lwe && e == hipSuccess; ++i) {
-      e = forward(g, RotDigitSrc{acc, in, g.tw, g.logn, kp1, lv, (uint32_t)n_lwe, i, base_log, ms_mode}, d,
-                  (uint64_t)nb * lv * kp1, s);
-      if (e != hipSuccess) break;
-      e = inverse(g, MacSrc{d, key + i * ggsw_len, g.logm, g.logc, g.logr, kp1, lv}, AccSink{acc, g.untw, g.logn}, y,
-                  (uint64_t)nb * kp1, s);
+  struct Lane {  // ciphertexts [b0, b0 + nb) of the batch, their scratch slices, their stream
+    size_t b0;
+    uint32_t nb;
+    hipStream_t st;
+    const uint64_t* in;
+    cplx *d, *y;
+    uint64_t *acc, *corr;
+  };
+  for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
+    const uint32_t nb_all = (uint32_t)std::min(chunk, batch - c0);
+    mi::StreamFork fork;
+    int lanes = 1;
+    if (nb_all >= FFTG_LANE_MIN && fftg_lanes_enabled() && fork.fork(s) == hipSuccess) lanes = 2;
+    Lane L[2];
+    for (int j = 0, off = 0; j < lanes; ++j) {
+      const uint32_t n = lanes == 1 ? nb_all : (j == 0 ? (nb_all + 1) / 2 : nb_all / 2);
+      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(), lwe_in + (c0 + off) * (n_lwe + 1),
+                  d_all + (((size_t)off * lv * kp1) << g.logm), y_all ? y_all + (((size_t)off * kp1) << g.logm) : nullptr,
+                  acc_all + (size_t)off * per, corr_all + off};
+      off += (int)n;
     }
-    if (e != hipSuccess) break;
-    if (io.glwe_out) {
-      hipLaunchKernelGGL(store_glwe_kernel, dim3(blocks_for((uint64_t)nb * per)), dim3(256), 0, s,
-                         (const uint64_t*)acc, nb, (uint64_t)per, io, (uint64_t)b0);
-    } else {
-      const uint64_t outs = (uint64_t)nb * (((uint64_t)k << g.logn) + 1);
-      hipLaunchKernelGGL(extract_kernel, dim3(blocks_for(outs)), dim3(256), 0, s,
-                         out + b0 * (((size_t)k << g.logn) + 1), (const uint64_t*)acc, nb, g.logn, (uint32_t)k, io,
-                         (uint64_t)b0);
+    for (int j = 0; j < lanes && e == hipSuccess; ++j) {
+      const Lane& l = L[j];
+      if (ms_mode == 1)
+        hipLaunchKernelGGL(body_correction_kernel, dim3(l.nb), dim3(256), 0, l.st, l.corr, l.in, (uint32_t)n_lwe,
+                           g.logn + 1);
+      hipLaunchKernelGGL(init_acc_kernel, dim3(blocks_for((uint64_t)l.nb * per)), dim3(256), 0, l.st, l.acc, io,
+                         (uint64_t)l.b0, l.in, ms_mode == 1 ? (const uint64_t*)l.corr : nullptr, (uint32_t)n_lwe, l.nb,
+                         g.logn, kp1, ms_mode);
+      e = hipGetLastError();
     }
-    e = hipGetLastError();
+    for (uint32_t i = 0; i < (uint32_t)n_lwe && e == hipSuccess; ++i)
+      for (int j = 0; j < lanes && e == hipSuccess; ++j) {
+        const Lane& l = L[j];
+        e = forward(g, RotDigitSrc{l.acc, l.in, g.tw, g.logn, kp1, lv, (uint32_t)n_lwe, i, base_log, ms_mode}, l.d,
+                    (uint64_t)l.nb * lv * kp1, l.st);
+        if (e == hipSuccess)
+          e = inverse(g, MacSrc{l.d, key + i * ggsw_len, g.logm, g.logc, g.logr, kp1, lv},
+                      AccSink{l.acc, g.untw, g.logn}, l.y, (uint64_t)l.nb * kp1, l.st);
+      }
+    for (int j = 0; j < lanes && e == hipSuccess; ++j) {
+      const Lane& l = L[j];
+      if (io.glwe_out) {
+        hipLaunchKernelGGL(store_glwe_kernel, dim3(blocks_for((uint64_t)l.nb * per)), dim3(256), 0, l.st,
+                           (const uint64_t*)l.acc, l.nb, (uint64_t)per, io, (uint64_t)l.b0);
+      } else {
+        const uint64_t outs = (uint64_t)l.nb * (((uint64_t)k << g.logn) + 1);
+        hipLaunchKernelGGL(extract_kernel, dim3(blocks_for(outs)), dim3(256), 0, l.st,
+                           out + l.b0 * (((size_t)k << g.logn) + 1), (const uint64_t*)l.acc, l.nb, g.logn,
+                           (uint32_t)k, io, (uint64_t)l.b0);
+      }
+      e = hipGetLastError();
+    }
+    const hipError_t ej = fork.join();  // the caller's stream after the side lane (also on error: scratch ordering)
+    if (e == hipSuccess) e = ej;
   }
   const hipError_t ef = mi::scratch_free(scratch, s);
   return e != hipSuccess ? e : ef;
