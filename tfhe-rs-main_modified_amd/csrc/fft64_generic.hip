@@ -694,18 +694,11 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
   return e != hipSuccess ? e : ef;
 }
 
-// Two lanes, as launch_pbs_large (pbs_large.hip): a chunk of >= FFTG_LANE_MIN ciphertexts is split in halves on the
-// caller's stream and a pooled side stream (mi::StreamFork), launches interleaved step by step, so one half's
-// memory-bound passes overlap the other's transform rows.  MI_PBS_LANES=1 in the environment: one lane.
+// Lanes, as launch_pbs_large (pbs_large.hip): a chunk of >= FFTG_LANE_MIN ciphertexts is split into
+// mi::pbs_lane_count() parts on the caller's stream and pooled side streams (mi::StreamFork), launches interleaved step
+// by step, so one part's memory-bound passes overlap another's transform rows.  MI_PBS_LANES=<n> (1: one lane, A/B).
 static constexpr uint32_t FFTG_LANE_MIN = 64;
 
-static bool fftg_lanes_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("MI_PBS_LANES");
-    return !(v && v[0] == '1');
-  }();
-  return on;
-}
 
 hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
                            size_t n_lwe, size_t batch, int base_log, int level, int ms_mode, const FftGenTables& t,
@@ -738,12 +731,13 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const P
   for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
     const uint32_t nb_all = (uint32_t)std::min(chunk, batch - c0);
     mi::StreamFork fork;
-    int lanes = 1;
-    if (nb_all >= FFTG_LANE_MIN && fftg_lanes_enabled() && fork.fork(s) == hipSuccess) lanes = 2;
-    Lane L[2];
+    const int want = nb_all >= FFTG_LANE_MIN ? std::min<int>(mi::pbs_lane_count(), (int)(nb_all / 16)) : 1;
+    if (want > 1) (void)fork.fork(s, want - 1);  // fewer lanes when a side stream cannot be had
+    const int lanes = 1 + fork.sides();
+    Lane L[1 + mi::StreamFork::MAX_SIDE];
     for (int j = 0, off = 0; j < lanes; ++j) {
-      const uint32_t n = lanes == 1 ? nb_all : (j == 0 ? (nb_all + 1) / 2 : nb_all / 2);
-      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(), lwe_in + (c0 + off) * (n_lwe + 1),
+      const uint32_t n = nb_all / lanes + ((uint32_t)j < nb_all % lanes ? 1u : 0u);
+      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(j - 1), lwe_in + (c0 + off) * (n_lwe + 1),
                   d_all + (((size_t)off * lv * kp1) << g.logm), y_all ? y_all + (((size_t)off * kp1) << g.logm) : nullptr,
                   acc_all + (size_t)off * per, corr_all + off};
       off += (int)n;

@@ -594,20 +594,13 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 }  // namespace pbs
 
-// Two lanes: a chunk of >= PBS_LANE_MIN ciphertexts is split in halves, one on the caller's stream and one on a pooled
-// side stream (mi::StreamFork), their launches interleaved step by step.  Each ciphertext's blind rotation is
-// independent, so the halves share nothing but the key, and the GPU overlaps one half's memory-bound launches (the
-// rotation + decomposition pass, the MAC, the accumulating inverse pass) with the other's issue-bound transform bodies.
-// MI_PBS_LANES=1 in the environment: one lane (A/B).
+// Lanes: a chunk of >= PBS_LANE_MIN ciphertexts is split into mi::pbs_lane_count() parts (default 2, >= 16 ciphertexts
+// each), the first on the caller's stream and the others on pooled side streams (mi::StreamFork), their launches
+// interleaved step by step.  Each ciphertext's blind rotation is independent, so the parts share nothing but the key,
+// and the GPU overlaps one part's memory-bound launches (the rotation + decomposition pass, the MAC, the accumulating
+// inverse pass) with another's issue-bound transform bodies.  MI_PBS_LANES=<n> in the environment (1: one lane, A/B).
 static constexpr uint32_t PBS_LANE_MIN = 64;
 
-static bool pbs_lanes_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("MI_PBS_LANES");
-    return !(v && v[0] == '1');
-  }();
-  return on;
-}
 
 hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out, const uint64_t* lwe_in,
                             const PbsIo& io, const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log,
@@ -706,12 +699,13 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
     const uint32_t nb = (uint32_t)std::min(chunk, batch - c0);
     mi::StreamFork fork;
-    int lanes = 1;
-    if (nb >= PBS_LANE_MIN && pbs_lanes_enabled() && fork.fork(s) == hipSuccess) lanes = 2;
-    Lane L[2];
+    const int want = nb >= PBS_LANE_MIN ? std::min<int>(mi::pbs_lane_count(), (int)(nb / 16)) : 1;
+    if (want > 1) (void)fork.fork(s, want - 1);  // fewer lanes when a side stream cannot be had
+    const int lanes = 1 + fork.sides();
+    Lane L[1 + mi::StreamFork::MAX_SIDE];
     for (int j = 0, off = 0; j < lanes; ++j) {
-      const uint32_t n = lanes == 1 ? nb : (j == 0 ? (nb + 1) / 2 : nb / 2);
-      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(), lwe_in + (c0 + off) * (n_lwe + 1),
+      const uint32_t n = nb / lanes + ((uint32_t)j < nb % lanes ? 1u : 0u);
+      L[j] = Lane{c0 + off, n, j == 0 ? s : fork.side(j - 1), lwe_in + (c0 + off) * (n_lwe + 1),
                   scratch + (size_t)off * level * per, scratch + chunk * level * per + (size_t)off * per,
                   scratch + chunk * (level + 1) * per + (size_t)off * per, scratch + chunk * (level + 2) * per + off};
       off += (int)n;

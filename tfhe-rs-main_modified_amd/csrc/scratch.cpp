@@ -2,6 +2,7 @@
 #include "scratch.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -184,29 +185,46 @@ size_t scratch_trim(int device) {
   return bytes;
 }
 
-hipError_t StreamFork::fork(hipStream_t s) {
-  if (forked_) return hipErrorInvalidValue;
+hipError_t StreamFork::fork(hipStream_t s, int n) {
+  if (n_ > 0) return hipErrorInvalidValue;
   hipError_t e = hipGetDevice(&device_);
-  if (e == hipSuccess) e = side_acquire(device_, &side_);
   if (e != hipSuccess) return e;
-  if ((e = order_after(side_, s)) != hipSuccess) {
-    side_release(device_, side_);
-    side_ = nullptr;
-    return e;
-  }
   caller_ = s;
-  forked_ = true;
-  return hipSuccess;
+  n = std::max(0, std::min(n, MAX_SIDE));
+  while (n_ < n) {
+    hipStream_t st = nullptr;
+    if ((e = side_acquire(device_, &st)) != hipSuccess) break;
+    if ((e = order_after(st, s)) != hipSuccess) {
+      side_release(device_, st);
+      break;
+    }
+    side_[n_++] = st;
+  }
+  return n_ == n ? hipSuccess : e;
 }
 
 hipError_t StreamFork::join() {
-  if (!forked_) return hipSuccess;
-  hipError_t e = order_after(caller_, side_);
-  if (e != hipSuccess) (void)hipStreamSynchronize(side_);  // cannot order by event: drain the side stream instead
-  side_release(device_, side_);
-  side_ = nullptr;
-  forked_ = false;
-  return e;
+  hipError_t first = hipSuccess;
+  for (int i = 0; i < n_; ++i) {
+    const hipError_t e = order_after(caller_, side_[i]);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(side_[i]);  // cannot order by event: drain the side stream instead
+      if (first == hipSuccess) first = e;
+    }
+    side_release(device_, side_[i]);
+    side_[i] = nullptr;
+  }
+  n_ = 0;
+  return first;
+}
+
+int pbs_lane_count() {
+  static const int n = [] {
+    const char* v = getenv("MI_PBS_LANES");
+    const int k = v ? atoi(v) : 2;
+    return std::max(1, std::min(k, 1 + StreamFork::MAX_SIDE));
+  }();
+  return n;
 }
 
 size_t scratch_bytes(int device) {

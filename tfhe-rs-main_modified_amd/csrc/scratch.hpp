@@ -22,24 +22,29 @@ size_t scratch_trim(int device);
 // bytes held by the pool on `device` (idle + in use)
 size_t scratch_bytes(int device);
 
-// A pooled non-blocking side stream of the current device, for an entry point that splits its batch over the
-// caller's stream and one more (pbs_large.hip): fork() orders the side stream after the work already queued on the
-// caller's stream, join() orders the caller's stream after everything queued on the side stream and returns the side
-// stream to the pool.  No host synchronisation either way (events only).
+// Pooled non-blocking side streams of the current device, for an entry point that splits its batch over the caller's
+// stream and up to MAX_SIDE more (pbs_large.hip, fft64_generic.hip): fork() orders each side stream after the work
+// already queued on the caller's stream, join() orders the caller's stream after everything queued on the side
+// streams and returns them to the pool.  No host synchronisation either way (events only).
 class StreamFork {
  public:
+  static constexpr int MAX_SIDE = 3;
   StreamFork() = default;
   StreamFork(const StreamFork&) = delete;
   StreamFork& operator=(const StreamFork&) = delete;
   ~StreamFork() { (void)join(); }
-  hipError_t fork(hipStream_t s);
+  // acquires up to n side streams (fewer on failure: sides() tells how many)
+  hipError_t fork(hipStream_t s, int n = 1);
   hipError_t join();
-  hipStream_t side() const { return side_; }
+  int sides() const { return n_; }
+  hipStream_t side(int i = 0) const { return side_[i]; }
 
  private:
-  hipStream_t caller_ = nullptr, side_ = nullptr;
-  int device_ = 0;
-  bool forked_ = false;
+  hipStream_t caller_ = nullptr, side_[MAX_SIDE] = {};
+  int device_ = 0, n_ = 0;
 };
+
+// lanes a batched blind rotation splits a chunk into (MI_PBS_LANES in the environment, 1 ... 1 + MAX_SIDE; default 2)
+int pbs_lane_count();
 
 }  // namespace mi
