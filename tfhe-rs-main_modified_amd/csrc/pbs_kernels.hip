@@ -36,6 +36,10 @@ namespace pbs {
 template <int K>
 constexpr int loge_for() { return K >= 3 ? 2 : 3; }
 
+// The level-1 kernels fit 2 waves per SIMD without spilling (254 VGPRs at N = 512, k = 4; the runtime-level ones do
+// not: they keep the decomposition state live and stay at the compiler's choice, 1 wave per SIMD)
+#define MI_SHAPE_WAVES __attribute__((amdgpu_waves_per_eu(L1 ? 2 : 1)))
+
 template <int LOGN, int K>
 struct Shape {
   static constexpr int LOGE = loge_for<K>();
@@ -52,8 +56,10 @@ struct Shape {
 // in: ct1[K+1][E] (column layout, the GLWE to decompose); out: y[K+1][E] (column layout, the GLWE
 // contribution out += GGSW (.) ct1 in the ciphertext domain).  `ggsw` = level x (K+1) x (K+1) x N (NTT
 // domain, highest level first; row r = the decomposition of GLWE polynomial r); BNF keys are expected
-// pre-normalised unless `normalize`.  The decomposition levels are a runtime loop.
-template <int LOGN, int K, bool BNF>
+// pre-normalised unless `normalize`.  L1: the level count is 1 at compile time (the shortint shapes' 1_1 / 2_2),
+// so no decomposition state stays live beside the digits (the register budget of 2 waves per SIMD); else the levels
+// are a runtime loop.
+template <int LOGN, int K, bool BNF, bool L1>
 __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<LOGN, K>::E],
                                                  u64 (&y)[K + 1][Shape<LOGN, K>::E], const u64* __restrict__ ggsw,
                                                  int base_log, int level, int t, u64* sh,
@@ -63,29 +69,31 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
   using G = typename S::G;
   constexpr int E = S::E, N = S::N;
   const Goldilocks gl;
-  u64 state[K + 1][E];
-  bool sign[K + 1][E];
-  if (BNF) {
+  if constexpr (L1) level = 1;
+  // digit li of every coefficient: decomposer.rs:156-185 + iter.rs:131-151 (BNF) / iter.rs:623-745 (Solinas), mapped
+  // into [0, p) as ntt64.rs:231-238; the state arrays exist only for the runtime-level form
+  u64 state[L1 ? 1 : K + 1][L1 ? 1 : E];
+  bool sign[L1 ? 1 : K + 1][L1 ? 1 : E];
+  auto init = [&](u64 v, u64& st, bool& sg) {
+    if (BNF) {
+      st = decomp_init_native(v, base_log, level);
+      sg = false;
+    } else {
+      const unsigned shift = 64u - (unsigned)(base_log * level);
+      sg = v >= P / 2 + 1;  // div_ceil(2)
+      st = closest_abs_nonnative(sg ? P - v : v, base_log, level) >> shift;
+    }
+  };
+  auto digit = [&](u64& st, bool sg) -> u64 {
+    u64 term = decompose_one_level(base_log, st);
+    if (!BNF && sg) term = (u64)0 - term;  // iter.rs:722-731
+    return ((int64_t)term < 0) ? term + P : term;  // ntt64.rs:231-238 / iter.rs:724-730
+  };
+  if constexpr (!L1) {
 #pragma unroll
     for (int c = 0; c <= K; ++c)
 #pragma unroll
-      for (int r = 0; r < E; ++r) {
-        state[c][r] = decomp_init_native(ct1[c][r], base_log, level);
-        sign[c][r] = false;
-      }
-  } else {
-    // iter.rs:623-670 TensorSignedDecompositionLendingIterNonNative::new (q = p: ceil_log2 = 64)
-    const unsigned shift = 64u - (unsigned)(base_log * level);
-    const u64 half = P / 2 + 1;  // div_ceil(2)
-#pragma unroll
-    for (int c = 0; c <= K; ++c)
-#pragma unroll
-      for (int r = 0; r < E; ++r) {
-        const u64 x = ct1[c][r];
-        const bool s = x >= half;
-        state[c][r] = closest_abs_nonnative(s ? P - x : x, base_log, level) >> shift;
-        sign[c][r] = s;
-      }
+      for (int r = 0; r < E; ++r) init(ct1[c][r], state[c][r], sign[c][r]);
   }
 #pragma unroll
   for (int c = 0; c <= K; ++c)
@@ -99,9 +107,14 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
     for (int c = 0; c <= K; ++c)
 #pragma unroll
       for (int r = 0; r < E; ++r) {
-        u64 term = decompose_one_level(base_log, state[c][r]);
-        if (!BNF && sign[c][r]) term = (u64)0 - term;  // iter.rs:722-731
-        x[c][r] = ((int64_t)term < 0) ? term + P : term;  // ntt64.rs:231-238 / iter.rs:724-730
+        if constexpr (L1) {
+          u64 st;
+          bool sg;
+          init(ct1[c][r], st, sg);
+          x[c][r] = digit(st, sg);
+        } else {
+          x[c][r] = digit(state[c][r], sign[c][r]);
+        }
       }
     ntt_regs<G, true, K + 1>(x, t, sh, tw, gl);
     // the iterator yields DecompositionLevel(level_count) first (the least significant digit), the
@@ -138,8 +151,8 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
 // ---- external product / CMUX batch (config 3) ----------------------------------------------------
 // EXT : out[b] += GGSW (.) glwe[b]                          (add_external_product_ntt64[_bnf]_assign)
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
-template <int LOGN, int K, bool BNF, bool CMUX>
-__global__ __launch_bounds__((Shape<LOGN, K>::T)) void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+template <int LOGN, int K, bool BNF, bool CMUX, bool L1>
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) MI_SHAPE_WAVES void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                                      const u64* __restrict__ ggsw_list, uint32_t batch,
                                                                      int base_log, int level,
                                                                      const u64* __restrict__ tw,
@@ -172,7 +185,7 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void ext_product_kernel(u64* _
         in[e] = ct[c][r];
       }
     }
-  ext_product_regs<LOGN, K, BNF>(ct, y, ggsw, base_log, level, t, sh, tw, itw, true, n_inv);
+  ext_product_regs<LOGN, K, BNF, L1>(ct, y, ggsw, base_log, level, t, sh, tw, itw, true, n_inv);
 #pragma unroll
   for (int c = 0; c <= K; ++c)
 #pragma unroll
@@ -185,8 +198,8 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void ext_product_kernel(u64* _
 // ---- programmable bootstrap batch (configs 4/5) -----------------------------------------------
 // lwe_in: batch x (n+1); lut: (K+1) x N shared; bsk: n x level x (K+1) x (K+1) x N (BNF: pre-normalised
 // copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
-template <int LOGN, int K, bool BNF>
-__global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+template <int LOGN, int K, bool BNF, bool L1>
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) MI_SHAPE_WAVES void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                                              PbsIo io, const u64* __restrict__ bsk,
                                                              uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                              const u64* __restrict__ tw, const u64* __restrict__ itw,
@@ -261,7 +274,7 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) void pbs_kernel(u64* __restric
         ct1[c][r] = BNF ? v - acc[c][r] : sub_custom(v, acc[c][r]);  // cmux: ct1 - ct0
       }
     __syncthreads();
-    ext_product_regs<LOGN, K, BNF>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, level, t, sh, tw, itw, false, 0);
+    ext_product_regs<LOGN, K, BNF, L1>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, level, t, sh, tw, itw, false, 0);
 #pragma unroll
     for (int c = 0; c <= K; ++c)
 #pragma unroll
@@ -452,8 +465,14 @@ template <int LOGN, int K, bool BNF, bool CMUX>
 static hipError_t ext_launch(int level, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                              int base_log, const uint64_t* tw, const uint64_t* itw, uint64_t n_inv, hipStream_t s,
                              const uint32_t* gidx, uint32_t n_ggsw) {
-  hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX>), dim3((unsigned)batch), dim3(pbs::Shape<LOGN, K>::T), 0,
-                     s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw, n_inv, gidx, n_ggsw);
+  if (level == 1)
+    hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX, true>), dim3((unsigned)batch),
+                       dim3(pbs::Shape<LOGN, K>::T), 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw,
+                       n_inv, gidx, n_ggsw);
+  else
+    hipLaunchKernelGGL((pbs::ext_product_kernel<LOGN, K, BNF, CMUX, false>), dim3((unsigned)batch),
+                       dim3(pbs::Shape<LOGN, K>::T), 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, level, tw, itw,
+                       n_inv, gidx, n_ggsw);
   return hipGetLastError();
 }
 
@@ -487,12 +506,17 @@ static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* 
                             const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                             const uint64_t* itw, int centered, hipStream_t s) {
   const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN, K>::T);
-  if (bnf)
-    hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, true>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe,
-                       (uint32_t)batch, base_log, level, tw, itw, centered);
-  else
-    hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, false>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe,
-                       (uint32_t)batch, base_log, level, tw, itw, centered);
+#define MI_PBS_K(B, L)                                                                                             \
+  hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, B, L>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, \
+                     (uint32_t)batch, base_log, level, tw, itw, centered)
+  if (bnf) {
+    if (level == 1) MI_PBS_K(true, true);
+    else MI_PBS_K(true, false);
+  } else {
+    if (level == 1) MI_PBS_K(false, true);
+    else MI_PBS_K(false, false);
+  }
+#undef MI_PBS_K
   return hipGetLastError();
 }
 
