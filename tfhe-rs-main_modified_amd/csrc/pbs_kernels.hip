@@ -36,9 +36,16 @@ namespace pbs {
 template <int K>
 constexpr int loge_for() { return K >= 3 ? 2 : 3; }
 
-// The level-1 kernels fit 2 waves per SIMD without spilling (254 VGPRs at N = 512, k = 4; the runtime-level ones do
-// not: they keep the decomposition state live and stay at the compiler's choice, 1 wave per SIMD)
-#define MI_SHAPE_WAVES __attribute__((amdgpu_waves_per_eu(L1 ? 2 : 1)))
+// Waves per SIMD the level-1 kernels are compiled for (amdgpu_waves_per_eu): 2 fits N = 512, k = 4 in 254 VGPRs
+// without spilling; the k = 1 shapes that fit 168 VGPRs without spilling get 3 (hipcc -Rpass-analysis=
+// kernel-resource-usage).  The runtime-level kernels keep the decomposition state live and stay at the compiler's
+// choice (1 wave per SIMD).
+template <int LOGN, int K, bool L1, bool PBS>
+constexpr int shape_waves() {
+  if (!L1) return 1;
+  if (K == 1 && (PBS ? LOGN == 9 : LOGN <= 11)) return 3;
+  return 2;
+}
 
 template <int LOGN, int K>
 struct Shape {
@@ -152,7 +159,8 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
 // EXT : out[b] += GGSW (.) glwe[b]                          (add_external_product_ntt64[_bnf]_assign)
 // CMUX: glwe[b] -= out[b]; out[b] += GGSW (.) glwe[b]       (cmux_ntt64[_bnf]_assign, ct0 = out, ct1 = glwe)
 template <int LOGN, int K, bool BNF, bool CMUX, bool L1>
-__global__ __launch_bounds__((Shape<LOGN, K>::T)) MI_SHAPE_WAVES void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) __attribute__((amdgpu_waves_per_eu(shape_waves<LOGN, K, L1, false>())))
+void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
                                                                      const u64* __restrict__ ggsw_list, uint32_t batch,
                                                                      int base_log, int level,
                                                                      const u64* __restrict__ tw,
@@ -199,7 +207,8 @@ __global__ __launch_bounds__((Shape<LOGN, K>::T)) MI_SHAPE_WAVES void ext_produc
 // lwe_in: batch x (n+1); lut: (K+1) x N shared; bsk: n x level x (K+1) x (K+1) x N (BNF: pre-normalised
 // copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
 template <int LOGN, int K, bool BNF, bool L1>
-__global__ __launch_bounds__((Shape<LOGN, K>::T)) MI_SHAPE_WAVES void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
+__global__ __launch_bounds__((Shape<LOGN, K>::T)) __attribute__((amdgpu_waves_per_eu(shape_waves<LOGN, K, L1, true>())))
+void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                                              PbsIo io, const u64* __restrict__ bsk,
                                                              uint32_t n_lwe, uint32_t batch, int base_log, int level,
                                                              const u64* __restrict__ tw, const u64* __restrict__ itw,
