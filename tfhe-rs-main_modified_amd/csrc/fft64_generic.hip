@@ -695,9 +695,13 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
 }
 
 // Lanes, as launch_pbs_large (pbs_large.hip): a chunk of >= FFTG_LANE_MIN ciphertexts is split into
-// mi::pbs_lane_count() parts on the caller's stream and pooled side streams (mi::StreamFork), launches interleaved step
+// mi::pbs_lane_count(fftg_default_lanes(logn)) parts on the caller's stream and pooled side streams (mi::StreamFork), launches interleaved step
 // by step, so one part's memory-bound passes overlap another's transform rows.  MI_PBS_LANES=<n> (1: one lane, A/B).
 static constexpr uint32_t FFTG_LANE_MIN = 64;
+// default lane count per N, from the one-box sweep of profiles/r4/session24/lane_sweep.txt (PBS/s at 1 / 2 / 3 / 4
+// lanes: 1_1 (N 512) 35.6 / 41.9 / 41.4 / 34.8 k, 3_3 (N 8192) 2.36 / 2.55 / 2.53 / 2.67 k, 4_4 (N 65536) 176 / 184 /
+// 187 / 181) and the next boxes (4_4: 184.4 at 2 lanes, 180.1 at 3; 3_3: 2.67 k at 4 again, profiles/r4/session27/)
+static int fftg_default_lanes(uint32_t logn) { return logn >= 16 ? 2 : logn >= 13 ? 4 : 2; }
 
 
 hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const PbsIo& io, const double* fbsk,
@@ -731,7 +735,7 @@ hipError_t launch_fftg_pbs(int k, uint64_t* out, const uint64_t* lwe_in, const P
   for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
     const uint32_t nb_all = (uint32_t)std::min(chunk, batch - c0);
     mi::StreamFork fork;
-    const int want = nb_all >= FFTG_LANE_MIN ? std::min<int>(mi::pbs_lane_count(), (int)(nb_all / 16)) : 1;
+    const int want = nb_all >= FFTG_LANE_MIN ? std::min<int>(mi::pbs_lane_count(fftg_default_lanes(g.logn)), (int)(nb_all / 16)) : 1;
     if (want > 1) (void)fork.fork(s, want - 1);  // fewer lanes when a side stream cannot be had
     const int lanes = 1 + fork.sides();
     Lane L[1 + mi::StreamFork::MAX_SIDE];

@@ -699,7 +699,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   for (size_t c0 = 0; c0 < batch && e == hipSuccess; c0 += chunk) {
     const uint32_t nb = (uint32_t)std::min(chunk, batch - c0);
     mi::StreamFork fork;
-    const int want = nb >= PBS_LANE_MIN ? std::min<int>(mi::pbs_lane_count(), (int)(nb / 16)) : 1;
+    const int want = nb >= PBS_LANE_MIN ? std::min<int>(mi::pbs_lane_count(2), (int)(nb / 16)) : 1;
     if (want > 1) (void)fork.fork(s, want - 1);  // fewer lanes when a side stream cannot be had
     const int lanes = 1 + fork.sides();
     Lane L[1 + mi::StreamFork::MAX_SIDE];

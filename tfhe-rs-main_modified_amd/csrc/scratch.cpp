@@ -218,13 +218,12 @@ hipError_t StreamFork::join() {
   return first;
 }
 
-int pbs_lane_count() {
-  static const int n = [] {
+int pbs_lane_count(int dflt) {
+  static const int env = [] {
     const char* v = getenv("MI_PBS_LANES");
-    const int k = v ? atoi(v) : 2;
-    return std::max(1, std::min(k, 1 + StreamFork::MAX_SIDE));
+    return v ? atoi(v) : 0;
   }();
-  return n;
+  return std::max(1, std::min(env > 0 ? env : dflt, 1 + StreamFork::MAX_SIDE));
 }
 
 size_t scratch_bytes(int device) {

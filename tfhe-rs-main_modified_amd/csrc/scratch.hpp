@@ -44,7 +44,8 @@ class StreamFork {
   int device_ = 0, n_ = 0;
 };
 
-// lanes a batched blind rotation splits a chunk into (MI_PBS_LANES in the environment, 1 ... 1 + MAX_SIDE; default 2)
-int pbs_lane_count();
+// lanes a batched blind rotation splits a chunk into: MI_PBS_LANES in the environment (1 ... 1 + MAX_SIDE), else the
+// caller's measured default for its shape
+int pbs_lane_count(int dflt);
 
 }  // namespace mi
