@@ -263,6 +263,7 @@ def bench_pbs_solinas(args, eng, torch, dev, world, barrier, dist):
     del key
     return {"metric": "PBS/sec, Solinas modulus (ntt64_pbs), PARAM_MESSAGE_2_CARRY_2 shape", "value": world * batch * K / el,
             "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms,
+            "ntt_equivalents_per_s": world * batch * K / el * 4 * n_lwe,
             "config": {"workload": "programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized, q = 2^64 - 2^32 + 1, "
                                    "n=918 k=1 N=2048 base_log=23 level=1 (pbs_bench.rs:646-905 shape)",
                        "batch_per_gpu": batch},
@@ -555,6 +556,7 @@ def bench_ext_product(args, eng, torch, dev, world, barrier, dist):
     hbm = EXT_BYTES * batch / (kernel_ms * 1e-3) / 1e9
     return {"metric": "GGSW x GLWE external products/sec (config 3)", "value": world * batch * K / el,
             "unit": "external products/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms,
+            "ntt_equivalents_per_s": world * batch * K / el * 4,
             "config": {"workload": "add_external_product_ntt64_bnf_assign, N=2048, k=1, level 1, base_log 23, "
                                    "prepared GGSW (NttGgswList)",
                        "batch_per_gpu": batch},
@@ -1179,24 +1181,73 @@ def main():
             for name, (n_, k_, nl_, bl_, lv_, _) in (SHAPE_LEGS.items() if not args.no_shapes else ()):
                 out["pbs_shapes_fft"][name]["cpu_numpy_restatement"] = cpu_baseline_pbs_fft(
                     n_, k_, nl_, bl_, lv_, min(args.cpu_seconds, 3.0))
-    out["legs_summary"] = legs_summary(out)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        full_path = write_full_record(out)
+        # the driver parses the LAST stdout line and keeps only the tail: one compact line (<= LINE_MAX_BYTES)
+        print(json.dumps(compact_line(out, full_path)), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
+LINE_MAX_BYTES = 12 * 1024  # the parsed line must fit the driver's captured tail
+FULL_RECORD = os.path.join("gpurun_out", "bench_full.json")
+
+
+def write_full_record(out):
+    """The whole record (host path, default-stream, per-shape legs, CPU baselines of every leg) goes to a file, not
+    stdout. Returns the path written, or None when the tree is read-only."""
+    path = os.path.join(ROOT, FULL_RECORD)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return FULL_RECORD
+    except OSError as e:
+        print(f"bench.py: full record not written ({e})", file=sys.stderr)
+        return None
+
+
+def compact_line(out, full_path=None):
+    """The one JSON line the driver parses: the contract's keys, the headline's roofline and CPU baseline, and one
+    short row per leg. Everything else stays in the full record."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out.get(k) for k in keep}
+    cfg = out.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "n", "batch_per_gpu", "global_batch", "parallelism") if k in cfg}
+    build = cfg.get("build") or {}
+    if build:
+        line["config"]["source_sha16"] = (build.get("so_source_hash") or "")[:16]
+        line["config"]["build_matches_tree"] = build.get("match")
+    roof = out.get("roofline") or {}
+    line["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                "algorithmic_bytes_per_launch", "kernel")}
+    line["cpu_baseline"] = out.get("cpu_baseline")
+    kern = out.get("kernels") or {}
+    line["kernels"] = {k: kern.get(k) for k in ("timed_launch_ms", "fwd_ms", "inv_ms")}
+    line["valu_bound_frac"] = {k: v.get("frac") for k, v in (out.get("valu_bound") or {}).items()}
+    line["legs_summary"] = legs_summary(out)
+    line["full_record"] = full_path
+    return line
+
+
 def legs_summary(out):
-    """One compact row per leg (value, unit, roofline frac), the last key of the line."""
+    """One compact row per leg: value, unit, ms_per_step, steps, roofline frac + bound, CPU baseline value, and for
+    the NTT-built legs `alg_frac` = the leg's NTT-equivalents/s over the standalone transform's single-transform
+    rate (2 x the headline pairs/s), the algorithmic view beside the VALU-model `frac`."""
     rows = {}
+    single_rate = 2.0 * out["value"] if out.get("value") else None
 
     def row(d):
         roof = d.get("roofline") or {}
-        r = {"value": d.get("value"), "unit": d.get("unit"), "frac": roof.get("frac"), "bound": roof.get("bound")}
+        r = {"value": d.get("value"), "unit": d.get("unit"), "ms_per_step": d.get("ms_per_step"),
+             "steps": d.get("steps"), "frac": roof.get("frac"), "bound": roof.get("bound")}
         cpu = d.get("cpu_baseline") or {}
         if cpu.get("value") is not None:
             r["cpu"] = cpu["value"]
-        return r
+        if d.get("ntt_equivalents_per_s") and single_rate:
+            r["alg_frac"] = d["ntt_equivalents_per_s"] / single_rate
+        return {k: v for k, v in r.items() if v is not None}
 
     for name in LEG_ORDER:
         d = out.get(name)
