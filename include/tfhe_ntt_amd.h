@@ -88,6 +88,15 @@ int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan *plan, uint64_t *acc, cons
  * plumbing and the tests.  `buf` holds batch * n contiguous u64 on the host. */
 int mi_ntt64_fwd_host(const mi_ntt64_plan *plan, uint64_t *buf, size_t batch);
 int mi_ntt64_inv_host(const mi_ntt64_plan *plan, uint64_t *buf, size_t batch);
+/* The same host form of the pointwise ops, on `batch` contiguous polynomials per operand, through the pooled
+ * staging slots of mi_ntt64_fwd_host (no allocation, no device synchronisation in the steady state):
+ * Plan::normalize (prime64.rs:1137-1179), Plan::mul_assign_normalize (prime64.rs:1050-1133),
+ * Plan::mul_accumulate (prime64.rs:1182-1222) — what Ntt64View's update_with_fmadd reaches per polynomial
+ * (ntt64_pbs.rs:683-702). */
+int mi_ntt64_normalize_host(const mi_ntt64_plan *plan, uint64_t *buf, size_t batch);
+int mi_ntt64_mul_assign_normalize_host(const mi_ntt64_plan *plan, uint64_t *lhs, const uint64_t *rhs, size_t batch);
+int mi_ntt64_mul_accumulate_host(const mi_ntt64_plan *plan, uint64_t *acc, const uint64_t *lhs, const uint64_t *rhs,
+                                 size_t batch);
 
 /* ---- Synthetic input (device, async) ----------------------------------------------------
  * Fills `count` u64 with the counter-based generator of SURVEY.md §8d (splitmix64 finaliser over

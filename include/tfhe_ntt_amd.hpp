@@ -82,33 +82,23 @@ class Plan {
     require(len);
     check(mi_ntt64_inv_host(raw_, buf, 1));
   }
+  // the pointwise ops on host slices go through the library's pooled staging slots (mi_ntt64_*_host): no device
+  // allocation and no device-wide synchronisation per call
   void normalize(uint64_t* buf, size_t len) const {
     require(len);
-    DeviceBuffer d(n_, 1);
-    d.upload(0, buf);
-    check(mi_ntt64_normalize_batch(raw_, d.at(0), 1, n_, nullptr));
-    d.download(0, buf);
+    check(mi_ntt64_normalize_host(raw_, buf, 1));
   }
   void mul_assign_normalize(uint64_t* lhs, size_t lhs_len, const uint64_t* rhs, size_t rhs_len) const {
     require(lhs_len);
     require(rhs_len);
-    DeviceBuffer d(n_, 2);
-    d.upload(0, lhs);
-    d.upload(1, rhs);
-    check(mi_ntt64_mul_assign_normalize_batch(raw_, d.at(0), d.at(1), 1, n_, nullptr));
-    d.download(0, lhs);
+    check(mi_ntt64_mul_assign_normalize_host(raw_, lhs, rhs, 1));
   }
   void mul_accumulate(uint64_t* acc, size_t acc_len, const uint64_t* lhs, size_t lhs_len, const uint64_t* rhs,
                       size_t rhs_len) const {
     require(acc_len);
     require(lhs_len);
     require(rhs_len);
-    DeviceBuffer d(n_, 3);
-    d.upload(0, acc);
-    d.upload(1, lhs);
-    d.upload(2, rhs);
-    check(mi_ntt64_mul_accumulate_batch(raw_, d.at(0), d.at(1), d.at(2), 1, n_, nullptr));
-    d.download(0, acc);
+    check(mi_ntt64_mul_accumulate_host(raw_, acc, lhs, rhs, 1));
   }
 
   // ---- device batches (batch polynomials, `stride` u64 apart), async on `stream` ---------------
@@ -141,21 +131,6 @@ class Plan {
       throw std::invalid_argument("assertion `left == right` failed: slice length " + std::to_string(len) +
                                   " != ntt_size " + std::to_string(n_));
   }
-
-  // scratch for the host-slice pointwise ops: `count` polynomials on the plan's device, through the
-  // engine's own staging calls (mi_ntt64_*_host copy in / run / copy out for the transforms)
-  class DeviceBuffer {
-   public:
-    DeviceBuffer(size_t n, size_t count);
-    ~DeviceBuffer();
-    uint64_t* at(size_t i) const { return ptr_ + i * n_; }
-    void upload(size_t i, const uint64_t* src) const;
-    void download(size_t i, uint64_t* dst) const;
-
-   private:
-    uint64_t* ptr_ = nullptr;
-    size_t n_;
-  };
 
   mi_ntt64_plan* raw_ = nullptr;
   size_t n_ = 0;
@@ -426,22 +401,3 @@ inline void programmable_bootstrap_lwe_ciphertext(const FourierBootstrapKey& key
 
 }  // namespace fft64
 }  // namespace tfhe_ntt_amd
-
-// The staging buffer uses the HIP runtime directly (the only HIP dependency of this header).
-#include <hip/hip_runtime_api.h>
-
-inline tfhe_ntt_amd::prime64::Plan::DeviceBuffer::DeviceBuffer(size_t n, size_t count) : n_(n) {
-  const hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr_), n * count * sizeof(uint64_t));
-  if (e != hipSuccess) throw Error(MI_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
-}
-inline tfhe_ntt_amd::prime64::Plan::DeviceBuffer::~DeviceBuffer() {
-  if (ptr_) (void)hipFree(ptr_);
-}
-inline void tfhe_ntt_amd::prime64::Plan::DeviceBuffer::upload(size_t i, const uint64_t* src) const {
-  const hipError_t e = hipMemcpy(at(i), src, n_ * sizeof(uint64_t), hipMemcpyHostToDevice);
-  if (e != hipSuccess) throw Error(MI_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
-}
-inline void tfhe_ntt_amd::prime64::Plan::DeviceBuffer::download(size_t i, uint64_t* dst) const {
-  const hipError_t e = hipMemcpy(dst, at(i), n_ * sizeof(uint64_t), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) throw Error(MI_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
-}

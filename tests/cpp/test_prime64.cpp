@@ -12,6 +12,8 @@
 #include <random>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "tfhe_ntt_amd.hpp"
 
 using tfhe_ntt_amd::prime64::Plan;
@@ -144,6 +146,38 @@ static void test_length_mismatch_throws() {
   EXPECT(threw);
 }
 
+// the host-slice pointwise ops run through the library's pooled staging slots: after the first call, a long run of
+// calls allocates no device memory (hipMemGetInfo's free bytes do not move) and every result is exact
+static void test_pointwise_host_no_allocation() {
+  const size_t n = 2048;
+  auto plan = Plan::try_new(n, SOLINAS);
+  EXPECT(plan.has_value());
+  if (!plan) return;
+  const uint64_t p = SOLINAS, n_inv = powm(p, n, p - 2);
+  auto acc = random_poly(n, p), lhs = random_poly(n, p), rhs = random_poly(n, p);
+  plan->mul_accumulate(acc.data(), n, lhs.data(), n, rhs.data(), n);  // warm the slot
+  plan->normalize(acc.data(), n);
+  size_t free0 = 0, free1 = 0, total = 0;
+  EXPECT(hipMemGetInfo(&free0, &total) == hipSuccess);
+  bool exact = true;
+  for (int it = 0; it < 300; ++it) {
+    auto want = acc;
+    for (size_t i = 0; i < n; ++i) want[i] = addm(p, mulm(p, lhs[i], rhs[i]), want[i]);
+    plan->mul_accumulate(acc.data(), n, lhs.data(), n, rhs.data(), n);
+    exact = exact && acc == want;
+    for (size_t i = 0; i < n; ++i) want[i] = mulm(p, mulm(p, acc[i], rhs[i]), n_inv);
+    plan->mul_assign_normalize(acc.data(), n, rhs.data(), n);
+    exact = exact && acc == want;
+    for (size_t i = 0; i < n; ++i) want[i] = mulm(p, acc[i], n_inv);
+    plan->normalize(acc.data(), n);
+    exact = exact && acc == want;
+  }
+  EXPECT(exact);
+  EXPECT(hipMemGetInfo(&free1, &total) == hipSuccess);
+  EXPECT(free1 == free0);
+  if (free1 != free0) std::fprintf(stderr, "device free bytes moved: %zu -> %zu\n", free0, free1);
+}
+
 int main(int argc, char** argv) {
   const bool cpu_only = argc > 1 && std::string(argv[1]) == "--cpu";
   test_try_new_none();
@@ -152,6 +186,7 @@ int main(int argc, char** argv) {
     test_normalize_and_mul_assign_normalize();
     test_mul_accumulate();
     test_length_mismatch_throws();
+    test_pointwise_host_no_allocation();
   }
   if (g_failures) {
     std::fprintf(stderr, "%d expectation(s) failed\n", g_failures);

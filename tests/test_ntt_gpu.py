@@ -96,7 +96,7 @@ def test_fwd_inv_other_primes(engine, oracle, name, logn):
     assert np.array_equal(host(t), ora.inv(x))
 
 
-@pytest.mark.parametrize("logn,batch", [(12, 5), (13, 3), (14, 3), (15, 3), (17, 2)])
+@pytest.mark.parametrize("logn,batch", [(12, 5), (13, 3), (14, 3), (15, 3), (17, 2), (19, 2)])
 def test_large_n_strided_batch(engine, oracle, logn, batch):
     """Large-N path on a padded-stride batch (2^12 ... 2^14: the one-launch split transform, ntt_tw_fused_kernel):
     bit-exact, gaps never written, inv(fwd(x)) = N x."""

@@ -4,8 +4,8 @@ shortint/parameters/v1_4/classic/tuniform/p_fail_2_minus_128/ks_pbs.rs:71-90), b
 (ntt64_bnf_pbs.rs:208-726, ntt64_pbs.rs:213-702):
 
 * key conversion, external product, CMUX (shared and per-item indexed GGSW) and PBS on random keys vs the oracle, bit
-  for bit (N = 65536, 16384 and 8192 — the last two through the one-launch rotation + forward and inverse +
-  accumulate kernels of the split transform —, small n);
+  for bit (N = 8192 … 131072, every size the large engine accepts — through the one-launch rotation + forward and
+  inverse + accumulate kernels of the split transform, the K = 4 / 5 cooperative tiles and the two-pass top —, small n);
 * real keys at the full shape: every one of the 256 messages of the padded 4+4-bit space decrypts to f(m) after the
   PBS (lwe_programmable_bootstrapping.rs:708-865, 1002-1163) — BNF with the centered modulus switch the shortint
   parameters use, Solinas with its own switch; and, on the same real key cut to its first 24 GGSWs (the oracle PBS
@@ -34,9 +34,11 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-@pytest.mark.parametrize("n", [8192, 16384, 65536])
+@pytest.mark.parametrize("n", [8192, 16384, 32768, 65536, 131072])
 @pytest.mark.parametrize("bnf", [True, False])
 def test_large_random_keys(engine, oracle, n, bnf):
+    """Every N check_pbs_shape accepts past 8192: 32768 runs the K = 4 cooperative first top pass
+    (large_rotdec_tile), 131072 the two-pass split (large_rotdec_top<3> then the skip-first split) — ADVICE r4."""
     q = 0 if bnf else P
     k = 1
     pl = engine.Plan.try_new(n, P)

@@ -40,6 +40,7 @@ def run_seg(sg, regs_in, pairs_out, in_order=False):
     w = asm_emu.Wave({}, {})
     w.s[G.S_X15] = np.uint64(0x11111111)
     w.s[G.S_PAR], w.s[G.S_PAR + 1] = np.uint64(0xAAAAAAAA), np.uint64(0xAAAAAAAA)
+    w.s[G.S_EXE], w.s[G.S_EXE + 1] = np.uint64(0xFFFFFFFF), np.uint64(0xFFFFFFFF)  # the body's saved EXEC
     for b, vals in regs_in.items():
         arr = np.array(vals, dtype=np.uint64)
         w.v[b] = arr & np.uint64(0xFFFFFFFF)

@@ -212,7 +212,17 @@ static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_pla
         pow2_ok = pow2_ok && plan->twid[i] == mi::host::exp_mod(2, (u64)mi::tower_exp(true, st, g), p) &&
                   plan->inv_twid[i] == mi::host::exp_mod(2, (u64)mi::tower_exp(false, st, g), p);
       }
-    if (pow2_ok && mi_ntt64_plan_cached(2048, p, device, &sub) == MI_OK && sub->twisted &&
+    // a failure to build the cached 2048 sub-plan (e.g. a transient OOM) fails this plan too, with the sub-plan's
+    // status and message, instead of quietly leaving it on the slower window kernels for its lifetime
+    if (pow2_ok) {
+      const int rc = mi_ntt64_plan_cached(2048, p, device, &sub);
+      if (rc != MI_OK) {
+        (void)hipFree(plan->d_twid);
+        (void)hipFree(plan->d_inv_twid);
+        return rc;
+      }
+    }
+    if (pow2_ok && sub->twisted &&
         mi::host::exp_mod(psi, (u64)(n / 2048), p) == sub->twid[mi::host::bit_rev(11, 1)]) {
       const int t = logn - 11;
       std::vector<u64> blk(2 * n);
@@ -508,6 +518,59 @@ static int run_host(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t b
 }
 
 int mi_ntt64_fwd_host(const mi_ntt64_plan* plan, uint64_t* buf, size_t batch) { return run_host(true, plan, buf, batch); }
+
+// The host form of the pointwise ops (Plan::normalize / mul_assign_normalize / mul_accumulate on `&mut [u64]`,
+// prime64.rs:1050-1222; update_with_fmadd's per-polynomial calls, ntt64_pbs.rs:683-702): the operands go into one
+// pooled staging slot (operand k at k * batch * n), the kernel runs on the slot's stream — in place on the mapped
+// pinned buffer up to ZERO_COPY_BYTES, staged through the slot's device buffer above — and the result comes back.
+// Same slot pool as run_host: no allocation and no device-wide synchronisation in the steady state.
+static int run_host_pw(int op, const mi_ntt64_plan* plan, uint64_t* out, const uint64_t* a, const uint64_t* b,
+                       size_t batch) {
+  int st = check_batch(plan, out, batch, plan ? plan->n : 0);
+  if (st != MI_OK || batch == 0) return st;
+  if (op >= 1 && !b) return fail(MI_ERR_INVALID_ARG, "rhs is NULL");
+  if (op == 2 && !a) return fail(MI_ERR_INVALID_ARG, "lhs is NULL");
+  DeviceGuard g(plan->device);
+  if (!g.ok) return fail(MI_ERR_HIP, "hipSetDevice failed");
+  HostSlot* slot = acquire_slot(plan->device);
+  if (!slot) return fail(MI_ERR_HIP, "staging stream creation failed");
+  const size_t elems = batch * plan->n, bytes = elems * sizeof(u64);
+  const size_t nops = op == 0 ? 1 : (op == 1 ? 2 : 3);
+  hipError_t e = slot_reserve(slot, nops * elems);
+  if (e != hipSuccess) {
+    release_slot(slot);
+    return fail(MI_ERR_OOM, std::string("staging buffer allocation failed: ") + hipGetErrorString(e));
+  }
+  // operand order in the slot: out, then a (mul_accumulate's lhs), then b (the rhs)
+  std::memcpy(slot->hbuf, out, bytes);
+  if (op == 2) std::memcpy(slot->hbuf + elems, a, bytes);
+  if (op >= 1) std::memcpy(slot->hbuf + (nops - 1) * elems, b, bytes);
+  const bool zero_copy = nops * bytes <= ZERO_COPY_BYTES;
+  u64* base = zero_copy ? slot->hdev : slot->dbuf;
+  if (!zero_copy) e = hipMemcpyAsync(slot->dbuf, slot->hbuf, nops * bytes, hipMemcpyHostToDevice, slot->stream);
+  const u64 c = op == 0 ? plan->c_normalize : (op == 1 ? plan->c_man : plan->c_macc);
+  if (e == hipSuccess)
+    e = mi::launch_pointwise(op, plan->goldilocks, plan->mp, base, op == 2 ? base + elems : nullptr,
+                             op >= 1 ? base + (nops - 1) * elems : nullptr, plan->n, batch, plan->n, c, slot->stream);
+  if (e == hipSuccess && !zero_copy) e = hipMemcpyAsync(slot->hbuf, slot->dbuf, bytes, hipMemcpyDeviceToHost, slot->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(slot->stream);
+  if (e == hipSuccess) std::memcpy(out, slot->hbuf, bytes);
+  release_slot(slot);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "host pointwise op");
+}
+
+int mi_ntt64_normalize_host(const mi_ntt64_plan* plan, uint64_t* buf, size_t batch) {
+  return run_host_pw(0, plan, buf, nullptr, nullptr, batch);
+}
+
+int mi_ntt64_mul_assign_normalize_host(const mi_ntt64_plan* plan, uint64_t* lhs, const uint64_t* rhs, size_t batch) {
+  return run_host_pw(1, plan, lhs, nullptr, rhs, batch);
+}
+
+int mi_ntt64_mul_accumulate_host(const mi_ntt64_plan* plan, uint64_t* acc, const uint64_t* lhs, const uint64_t* rhs,
+                                 size_t batch) {
+  return run_host_pw(2, plan, acc, lhs, rhs, batch);
+}
 
 int mi_ntt64_inv_host(const mi_ntt64_plan* plan, uint64_t* buf, size_t batch) { return run_host(false, plan, buf, batch); }
 

@@ -313,8 +313,8 @@ static hipError_t dispatch(int logn, IO* data, size_t batch, size_t stride, cons
 // ---------------------------------------------------------------------------------------------
 // The split transform (ntt64_launch.hpp SplitTw): t = logn - 11 top stages on strided columns with the block twist
 // fused into the forward's last / the inverse's first pass, and the 2048-blocks through the twisted N = 2048 body.
-// Factorisation (checked against the oracle for N = 2^12 ... 2^17, fwd and inv: tests/test_ntt_gpu.py and
-// tools/check_split_factorisation.py): after the reference's first t stages, block b of 2048 coefficients holds the
+// Factorisation (checked against the oracle on the CPU for N = 2^12 ... 2^17, fwd and inv:
+// tools/check_split_factorisation.py; on the GPU for every N = 2^12 ... 2^20 the split engine serves: tests/test_ntt_gpu.py): after the reference's first t stages, block b of 2048 coefficients holds the
 // residue mod X^2048 - zeta_b; with alpha_b = psi_N^(2 bitrev_t(b) + 1 - 2^t) (alpha_b^2048 = -zeta_b) the substitution
 // X = alpha_b Y makes it the negacyclic (mod Y^2048 + 1) transform of the 2048 plan, whose root is psi_N^(N / 2048)
 // (the Solinas root tower), in the same bit-reversed output order.

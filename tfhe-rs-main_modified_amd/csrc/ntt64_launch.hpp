@@ -32,7 +32,9 @@ hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
                          hipStream_t s, int sub_log = 0);
 
-// The split transform of a Solinas plan with 2^12 <= N <= 2^17 (ntt64_kernels.hip): the reference's first
+// The split transform of a Solinas plan with 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN = 2^20 (ntt64_kernels.hip; GPU parity:
+// tests/test_ntt_gpu.py test_fwd_inv_all_sizes_solinas 2^12 .. 2^18, test_fwd_inv_beyond_2_18 2^19 / 2^20 — the
+// two-pass tops t = 7 .. 9 —, test_large_n_strided_batch up to 2^19): the reference's first
 // t = log2 N - 11 stages as passes over strided columns, the block twist (element j of 2048-block b times alpha_b^j,
 // alpha_b = psi_N^(2 bitrev_t(b) + 1 - 2^t)) fused into the last forward / first inverse pass, and every 2048-block
 // through the twisted N = 2048 body (ntt64_tw.hip) of the cached 2048-point Solinas plan.  Device tables:

@@ -73,6 +73,12 @@ hipError_t order_after(hipStream_t to, hipStream_t from) {
 
 constexpr size_t GRAIN = (size_t)1 << 20;  // blocks are whole MiB
 
+// an idle block serves a request only when it is at most 4x the request or 64 MiB above it, so a small request does
+// not take (and pin) a block sized for the large-N blind rotation while a concurrent large request allocates another
+bool fits_snugly(size_t block, size_t request) {
+  return block / 4 <= request || block - request <= ((size_t)64 << 20);
+}
+
 // frees blocks that no longer have a pending user (their event has completed)
 void release(std::vector<Block>& blocks) {
   int cur = 0;
@@ -102,14 +108,19 @@ hipError_t scratch_alloc(void** out, size_t bytes, hipStream_t s) {
     std::lock_guard<std::mutex> lk(P.mu);
     auto best = P.idle.end();
     for (auto it = P.idle.begin(); it != P.idle.end(); ++it)
-      if (it->device == dev && it->bytes >= bytes && (best == P.idle.end() || it->bytes < best->bytes)) best = it;
+      if (it->device == dev && it->bytes >= bytes && fits_snugly(it->bytes, bytes) &&
+          (best == P.idle.end() || it->bytes < best->bytes))
+        best = it;
     if (best != P.idle.end()) {
       blk = *best;
       P.idle.erase(best);
       P.busy[blk.p] = blk;
       found = true;
     } else {
-      auto keep = std::partition(P.idle.begin(), P.idle.end(), [&](const Block& b) { return b.device != dev; });
+      // only the idle blocks too small for this request are superseded; a much larger idle block stays for the
+      // large requests it was made for (a small request no longer takes the 4 GiB PBS block)
+      auto keep = std::partition(P.idle.begin(), P.idle.end(),
+                                 [&](const Block& b) { return b.device != dev || b.bytes >= bytes; });
       smaller.assign(keep, P.idle.end());
       P.idle.erase(keep, P.idle.end());
     }

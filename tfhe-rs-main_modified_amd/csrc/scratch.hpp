@@ -5,8 +5,12 @@
 // A per-device pool of plain hipMalloc blocks, kept for reuse and grown on demand (scratch.cpp).  Ordering is by event,
 // not by host synchronisation: each block carries the event recorded on the stream of its last user, and the next
 // user's stream waits on it (hipStreamWaitEvent) before its first launch.  So a block is never reissued before the
-// last kernel that read it retired, on any stream, and no call blocks the host — on the legacy null stream or on a
-// caller's stream alike.  The stream-ordered allocator (hipMallocAsync) is not used: DESIGN.md §5 records why.
+// last kernel that read it retired, on any stream, and reusing a pooled block never blocks the host — on the legacy null
+// stream or on a caller's stream alike.  Growing the pool does: a request no idle block fits (an idle block serves a
+// request only if it is at most 4x or 64 MiB above it) hipMallocs a new block and first frees the idle blocks of that
+// device too small for it, each after hipEventSynchronize on its last use.  The high-water mark is the largest set of
+// blocks in use at once plus the idle ones kept (up to the 4 GiB chunks of a large-N blind rotation) until
+// mi_scratch_trim.  The stream-ordered allocator (hipMallocAsync) is not used: DESIGN.md §5 records why.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>

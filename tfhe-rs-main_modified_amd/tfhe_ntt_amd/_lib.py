@@ -52,6 +52,9 @@ _SIGS = {
     "mi_ntt64_mul_accumulate_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
     "mi_ntt64_fwd_host": (_int, [_vp, _p64, _sz]),
     "mi_ntt64_inv_host": (_int, [_vp, _p64, _sz]),
+    "mi_ntt64_normalize_host": (_int, [_vp, _p64, _sz]),
+    "mi_ntt64_mul_assign_normalize_host": (_int, [_vp, _p64, _p64, _sz]),
+    "mi_ntt64_mul_accumulate_host": (_int, [_vp, _p64, _p64, _p64, _sz]),
     "mi_fill_uniform": (_int, [_vp, _sz, _u64, _u64, _int, _vp]),
     "mi_bsk_to_ntt64": (_int, [_vp, _vp, _vp, _sz, ctypes.c_uint, _int, _vp]),
     "mi_ext_product_ntt64_batch": (_int, [_vp, _vp, _vp, _vp, _int, _int, _int, _sz, _int, _vp]),

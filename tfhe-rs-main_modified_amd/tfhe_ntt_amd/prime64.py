@@ -146,20 +146,43 @@ class Plan:
             check(fn(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), batch))
 
     # -- pointwise ops (prime64.rs:1050-1222) --------------------------------------------
+    # device tensors run async on the tensor's stream; numpy uint64 arrays (the reference's `&mut [u64]` slices) go
+    # through the library's pooled staging slots (mi_ntt64_*_host: copy in, run, copy out, no allocation per call)
     def normalize(self, values) -> None:
+        if not _is_torch(values):
+            b = self._host_layout(values, "values")
+            check(lib().mi_ntt64_normalize_host(self._h, _u64p(values), b))
+            return
         b, s = self._dev_layout(values, "values")
         check(lib().mi_ntt64_normalize_batch(self._h, ctypes.c_void_p(values.data_ptr()), b, s, self._stream(values)))
 
     def mul_assign_normalize(self, lhs, rhs) -> None:
+        if not _is_torch(lhs):
+            b = self._same_host_layout(lhs, rhs)
+            check(lib().mi_ntt64_mul_assign_normalize_host(self._h, _u64p(lhs), _u64p(rhs), b))
+            return
         b, s = self._same_layout(lhs, rhs)
         check(lib().mi_ntt64_mul_assign_normalize_batch(self._h, ctypes.c_void_p(lhs.data_ptr()),
                                                         ctypes.c_void_p(rhs.data_ptr()), b, s, self._stream(lhs)))
 
     def mul_accumulate(self, acc, lhs, rhs) -> None:
+        if not _is_torch(acc):
+            b = self._same_host_layout(acc, lhs, rhs)
+            check(lib().mi_ntt64_mul_accumulate_host(self._h, _u64p(acc), _u64p(lhs), _u64p(rhs), b))
+            return
         b, s = self._same_layout(acc, lhs, rhs)
         check(lib().mi_ntt64_mul_accumulate_batch(self._h, ctypes.c_void_p(acc.data_ptr()),
                                                   ctypes.c_void_p(lhs.data_ptr()), ctypes.c_void_p(rhs.data_ptr()),
                                                   b, s, self._stream(acc)))
+
+    def _same_host_layout(self, out, *ins):
+        b = self._host_layout(out)
+        for a in ins:
+            if not isinstance(a, np.ndarray) or a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+                raise TypeError("host pointwise operands must be C-contiguous numpy uint64 arrays")
+            if a.shape != out.shape:
+                raise ValueError(f"assertion `left == right` failed: operand shapes {out.shape} vs {a.shape}")
+        return b
 
     def _same_layout(self, *ts):
         if not all(_is_torch(t) for t in ts):
@@ -171,6 +194,10 @@ class Plan:
 
     def __repr__(self):
         return f"Plan {{ ntt_size: {self._n}, modulus: {self._p} }}"
+
+
+def _u64p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
 
 
 def fill_uniform(t, seed: int, p: int = SOLINAS_P) -> None:

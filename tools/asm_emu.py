@@ -62,7 +62,7 @@ class Wave:
         return _bits(int(self.s[b]) | (int(self.s[b + 1]) << 32))
 
     def set_mask(self, tok, m):
-        m = (m & self.exec) | (self.mask(tok) & ~self.exec)
+        m = m & self.exec  # a VALU lane-mask write clears the bits of inactive lanes
         word = _word(m)
         b = self.spair(tok)
         self.s[b] = np.uint64(word & 0xFFFFFFFF)
@@ -132,6 +132,9 @@ class Wave:
     # VALU
     def op_v_mov_b32(self, a):
         self.wv(self.vreg(a[0]), self.src32(a[1]))
+
+    def op_v_mov_b64(self, a):
+        self.wv64(self.vpair(a[0]), self.src64(a[1]))
 
     def op_v_mov_b32_dpp(self, a):
         src = self.src32(a[1].split()[0])
@@ -280,13 +283,25 @@ class Wave:
         else:
             raise NotImplementedError(a)
 
+    def _set_exec_or(self, a, m):
+        """SALU write of EXEC (the EXEC-masked arithmetic of gen_tw_kernel); True when a[0] is exec."""
+        if a[0] != "exec":
+            return False
+        self.exec = m
+        self.scc = int(m.any())
+        return True
+
     def op_s_not_b64(self, a):
+        if self._set_exec_or(a, ~self.mask(a[1])):
+            return
         word = _word(~self.mask(a[1]))
         b = self.VCC if a[0] == "vcc" else self.spair(a[0])
         self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)
         self.scc = int(word != 0)
 
     def op_s_or_b64(self, a):
+        if self._set_exec_or(a, self.mask(a[1]) | self.mask(a[2])):
+            return
         word = _word(self.mask(a[1]) | self.mask(a[2]))
         b = self.spair(a[0])
         self.s[b], self.s[b + 1] = np.uint64(word & 0xFFFFFFFF), np.uint64(word >> 32)

@@ -37,16 +37,17 @@ def pv(b):
 
 
 class Op:
-    __slots__ = ("text", "reads", "writes", "kind", "cost", "preds", "succs", "prio", "idx")
+    __slots__ = ("text", "reads", "writes", "kind", "cost", "preds", "succs", "prio", "idx", "mask_reads")
 
     def __init__(self, text, reads, writes, kind="valu"):
         self.text, self.kind = text, kind
         self.reads, self.writes = set(), set()
+        self.mask_reads = set()
         for r in reads:
             self.reads.update(expand(r))
         for w in writes:
             self.writes.update(expand(w))
-        m = text.split()[0]
+        m = (text[1] if isinstance(text, list) else text).split()[0]
         if kind == "salu":
             self.cost = 0.0
         elif m in ("v_mov_b32", "v_lshrrev_b32", "v_lshlrev_b32") or kind == "dpp":
@@ -74,6 +75,16 @@ class Seg:
 
     def add(self, text, reads=(), writes=(), kind="valu"):
         self.ops.append(Op(text, reads, writes, kind))
+
+    def add_masked(self, set_line, set_reads, text, reads=(), writes=()):
+        """One VALU instruction under EXEC = a lane mask the SALU `set_line` writes from the SGPR pairs `set_reads`
+        (carry / borrow masks of earlier VALU ops), EXEC restored to the saved full mask right after.  Scheduled as one
+        unit; the SALU read of the mask obeys the VALU-write -> SALU-read wait state.  Back-to-back masked units drop
+        the restore between them (masked_peephole)."""
+        op = Op([set_line, text, EXEC_RESTORE], list(reads) + list(set_reads), writes)
+        for r in set_reads:
+            op.mask_reads.update(expand(r))
+        self.ops.append(op)
 
     def schedule(self):
         ops = self.ops
@@ -125,7 +136,7 @@ class Seg:
                     if p is None or p.kind == "salu":
                         continue
                     if r[0] == "s" or r == "vcc":
-                        need = 2 if op.kind == "salu" else 3
+                        need = 2 if (op.kind == "salu" or r in op.mask_reads) else 3
                     elif op.kind == "dpp":
                         need = 3
                     else:
@@ -142,15 +153,31 @@ class Seg:
                 out.append("s_nop 0")
                 slot += 1
                 continue
-            out.append(best.text)
+            if isinstance(best.text, list):
+                out.extend(best.text)
+            else:
+                out.append(best.text)
             issued[best] = slot
             slot += 1
             done.add(best)
             remaining.remove(best)
-        return merge_nops(out)
+        return merge_nops(masked_peephole(out))
 
     def emit_in_order(self):
-        return [op.text for op in self.ops]
+        out = []
+        for op in self.ops:
+            out.extend(op.text if isinstance(op.text, list) else [op.text])
+        return out
+
+
+def masked_peephole(lines):
+    """Drop an EXEC restore that the next instruction overwrites (two masked units back to back)."""
+    res = []
+    for i, l in enumerate(lines):
+        if l == EXEC_RESTORE and i + 1 < len(lines) and lines[i + 1].split(" ")[1:2] == ["exec,"]:
+            continue
+        res.append(l)
+    return res
 
 
 def merge_nops(lines):
@@ -283,7 +310,10 @@ def pair_of(lo, hi):
 
 def minus_eps(sg, m, c, dp):
     """dp <- dp - EPS where the SGPR mask c is set (a borrow: + p mod 2^64): m = c ? -15 : 0, then
-    dp += m * 0x11111111 (signed 32 x 32 + 64)."""
+    dp += m * 0x11111111 (signed 32 x 32 + 64).  EXEC_MASK: one masked v_mad_i64_i32 (m unused)."""
+    if EXEC_MASK:
+        minus_eps_masked(sg, c, dp)
+        return
     sg.add(f"v_cndmask_b32_e64 {m}, 0, -15, {c}", [c], [m])
     sg.add(f"v_mad_i64_i32 {dp}, {JUNK}, {m}, s{S_X15}, {dp}", [m, dp], [dp, JUNK])
 
@@ -297,6 +327,11 @@ def sub_seq(sg, sl, dlo, dhi, alo, ahi, tlo, thi):
 
 def ct_core(sg, sl, a, b, neg, tsrc=None):
     """t in sl.v2:v3 (or tsrc) canonical; a, b = (lo, hi, pair)."""
+    if EXEC_MASK:
+        if tsrc:
+            assert tsrc == (b[0], b[1]), tsrc
+            return ct_x(sg, sl, a, b, 96 if neg else 0, b_canon=True)
+        return ct_core_x(sg, sl, a, b, neg, (sl.v[2], sl.v[3]))
     alo, ahi, ap = a
     blo, bhi, bp = b
     tlo, thi = tsrc if tsrc else (sl.v[2], sl.v[3])
@@ -320,6 +355,8 @@ def ct_core_canon(sg, sl, a, b, neg):
     """ct_core for a canonical a and the canonical t in sl.v2:v3, with canonical outputs: the difference of
     two canonical values needs only the borrow fix (sub_seq), and their sum is canonical after one select
     between s and U = s + EPS (U when the add carried, s + 2^64 = U mod p, or when U carried, s >= p)."""
+    if EXEC_MASK:
+        return ct_core_x(sg, sl, a, b, neg, (sl.v[2], sl.v[3]), canon_out=True)
     alo, ahi, ap = a
     blo, bhi, bp = b
     v, P, c = sl.v, sl.P, sl.c
@@ -338,6 +375,8 @@ def ct_core_canon(sg, sl, a, b, neg):
 
 
 def ct(sg, sl, a, b, S):
+    if EXEC_MASK:
+        return ct_x(sg, sl, a, b, S)
     neg = tmul(sg, S, b[0], b[1], b[2], sl, sl.v[2], sl.v[3])
     ct_core(sg, sl, a, b, neg)
 
@@ -364,6 +403,8 @@ def gs(sg, sl, a, b, S, ac=False, bc=False):
     same one), so the new b is always the canonical, positive tmul magnitude: no negation is ever
     emitted.  When both inputs are canonical the sum is made canonical too (one select after the add:
     +1 VALU, and the next stage needs no canonicalisation).  Returns (new a canonical, new b canonical)."""
+    if EXEC_MASK:
+        return gs_x(sg, sl, a, b, S, ac, bc)
     alo, ahi, ap = a
     blo, bhi, bp = b
     v, P, c = sl.v, sl.P, sl.c
@@ -404,6 +445,28 @@ def gmul(sg, ms, x, wlo, whi, olo, ohi, zero_hi=True):
     v, P, c = ms.v, ms.P, ms.c
     PA, PB, PC, PD, Z1, Z2 = P
     A0, A1, B0, B1, C0, C1, D0, D1, Z1l, Z1h, Z2l, Z2h = v
+    if EXEC_MASK:
+        # the same product; R = T + H0 EPS goes straight into o (every read of x is earlier), the borrow fix and
+        # the canonicalising select are EXEC-masked single instructions (13 VALU)
+        op = pair_of(olo, ohi)
+        if zero_hi:
+            sg.add(f"v_mov_b32 {Z1h}, 0", [], [Z1h])
+            sg.add(f"v_mov_b32 {Z2h}, 0", [], [Z2h])
+        sg.add(f"v_mad_u64_u32 {PA}, {JUNK}, {xlo}, {wlo}, 0", [xlo, wlo], [PA, JUNK])
+        sg.add(f"v_mov_b32 {Z1l}, {A1}", [A1], [Z1l])
+        sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {xlo}, {whi}, {Z1}", [xlo, whi, Z1], [PB, JUNK])
+        sg.add(f"v_mov_b32 {Z2l}, {B0}", [B0], [Z2l])
+        sg.add(f"v_mov_b32 {Z1l}, {B1}", [B1], [Z1l])
+        sg.add(f"v_mad_u64_u32 {PC}, {JUNK}, {xhi}, {wlo}, {Z2}", [xhi, wlo, Z2], [PC, JUNK])
+        sg.add(f"v_mad_u64_u32 {PD}, {JUNK}, {xhi}, {whi}, {Z1}", [xhi, whi, Z1], [PD, JUNK])
+        sg.add(f"v_mad_u64_u32 {PB}, {JUNK}, {C1}, 1, {PD}", [C1, PD], [PB, JUNK])          # H = D + C.hi
+        sg.add(f"v_sub_co_u32_e64 {D0}, {c[0]}, {A0}, {B1}", [A0, B1], [D0, c[0]])          # T = L - H1
+        sg.add(f"v_subb_co_u32_e64 {D1}, {c[1]}, {C0}, 0, {c[0]}", [C0, c[0]], [D1, c[1]])
+        minus_eps_masked(sg, c[1], PD)
+        sg.add(f"v_mad_u64_u32 {op}, {c[0]}, {B0}, -1, {PD}", [B0, PD], [op, c[0]])         # R = T + H0 EPS
+        sg.add(f"v_mad_u64_u32 {PC}, {c[1]}, -1, 1, {op}", [op], [PC, c[1]])                # U = R + EPS
+        mov64_masked(sg, ("or", c[1], c[0]), op, PC)
+        return
     if zero_hi:
         sg.add(f"v_mov_b32 {Z1h}, 0", [], [Z1h])
         sg.add(f"v_mov_b32 {Z2h}, 0", [], [Z2h])
@@ -428,9 +491,178 @@ def gmul(sg, ms, x, wlo, whi, olo, ohi, zero_hi=True):
 def canon(sg, sl, x):
     xlo, xhi, xp = x
     v, P, c = sl.v, sl.P, sl.c
+    if EXEC_MASK:
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {xp}", [xp], [P[0], c[1]])
+        mov64_masked(sg, c[1], xp, P[0])
+        return
     sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {xp}", [xp], [P[0], c[1]])
     sg.add(f"v_cndmask_b32_e64 {xlo}, {xlo}, {v[0]}, {c[1]}", [xlo, v[0], c[1]], [xlo])
     sg.add(f"v_cndmask_b32_e64 {xhi}, {xhi}, {v[1]}, {c[1]}", [xhi, v[1], c[1]], [xhi])
+
+
+# ------------------------------------------------------------------------------------------------
+# EXEC-masked arithmetic (r5).  Every conditional step of the Goldilocks arithmetic (fold a carry: + EPS; fix a
+# borrow: - EPS; canonicalise: select x + EPS) was a VALU select (v_cndmask on the carry mask, 4.3 cycles per 32-bit
+# word) feeding a multiply-add, or a pair of selects.  Here the carry mask goes into EXEC through the SALU (off the
+# VALU issue path) and the step is ONE VALU instruction on the lanes that need it: a fold or a borrow fix is one
+# v_mad (4.6 instead of 8.9 cycles), a select one v_mov_b64 (4.2 instead of 8.6).  Every result is written in
+# place, so the butterflies also need no sum / difference temporaries.  The arithmetic is unchanged: same values,
+# lane by lane (the emulator tests and the GPU parity tests check it).
+EXEC_MASK = True
+
+
+def cond_exec(cond):
+    """(SALU line writing EXEC, SGPR pairs it reads) for cond = an SGPR pair, ("or", c1, c0) or ("not", c)."""
+    if isinstance(cond, tuple):
+        if cond[0] == "or":
+            return f"s_or_b64 exec, {cond[1]}, {cond[2]}", [cond[1], cond[2]]
+        return f"s_not_b64 exec, {cond[1]}", [cond[1]]
+    return f"s_mov_b64 exec, {cond}", [cond]
+
+
+def mov64_masked(sg, cond, dst, src):
+    """dst <- src (u64 pairs) on the lanes of cond."""
+    line, sr = cond_exec(cond)
+    sg.add_masked(line, sr, f"v_mov_b64 {dst}, {src}", [src, dst], [dst])
+
+
+def plus_eps_masked(sg, cond, dp):
+    """dp += EPS on the lanes of cond (the fold of a carry out of bit 64: 2^64 = EPS mod p)."""
+    line, sr = cond_exec(cond)
+    sg.add_masked(line, sr, f"v_mad_u64_u32 {dp}, {JUNK}, -1, 1, {dp}", [dp], [dp, JUNK])
+
+
+def minus_eps_masked(sg, cond, dp):
+    """dp -= EPS on the lanes of cond (a borrow out of bit 64: d - 2^64 = d - EPS mod p); -15 * 0x11111111 = -EPS."""
+    line, sr = cond_exec(cond)
+    sg.add_masked(line, sr, f"v_mad_i64_i32 {dp}, {JUNK}, -15, s{S_X15}, {dp}", [dp], [dp, JUNK])
+
+
+def tmul_x(sg, S, x, sl, T, copy_u=False):
+    """T (an aligned pair, may be x itself) <- canonical t with x * 2^S = (neg ? -t : t); returns neg.  Scratch: the
+    slot's P0, v4 and (class 1) P3, carry pairs c0 / c1.  The raw product goes straight into T, so x may be T: every
+    read of x precedes the first write of T in program order (the scheduler keeps that order)."""
+    xlo, xhi, xp = x
+    tlo, thi = T
+    tp = pair_of(tlo, thi)
+    e = S % 96
+    neg = (S >= 96) != (e >= 64)
+    v, P, c = sl.v, sl.P, sl.c
+    if e == 0:
+        if tp == xp:
+            canon(sg, sl, x)
+        else:
+            sg.add(f"v_mad_u64_u32 {tp}, {c[1]}, -1, 1, {xp}", [xp], [tp, c[1]])   # T = x + EPS
+            mov64_masked(sg, ("not", c[1]), tp, xp)                                # x < p: T = x
+        return neg
+    if e < 64:
+        r = e if e <= 32 else e - 32
+        sg.add(f"v_lshlrev_b64 {P[0]}, {r}, {xp}", [xp], [P[0]])
+        if r == 32:
+            h = xhi
+        else:
+            h = v[4]
+            sg.add(f"v_lshrrev_b32 {h}, {32 - r}, {xhi}", [xhi], [h])
+        sg.add(f"v_mad_u64_u32 {tp}, {c[0]}, {h}, -1, {P[0]}", [h, P[0]], [tp, c[0]])   # x 2^r = T + c0 2^64
+        if e > 32:
+            # y = x 2^r folded (T < (2^32 - 1)^2 when c0: no second wrap), then y 2^32 = (y_lo << 32) + y_hi EPS
+            plus_eps_masked(sg, c[0], tp)
+            sg.add(f"v_lshlrev_b64 {P[3]}, 32, {tp}", [tp], [P[3]])
+            sg.add(f"v_mad_u64_u32 {tp}, {c[0]}, {thi}, -1, {P[3]}", [thi, P[3]], [tp, c[0]])
+        sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {tp}", [tp], [P[0], c[1]])        # U = T + EPS
+        mov64_masked(sg, ("or", c[1], c[0]), tp, P[0])                                  # canonical: U if a carry
+        return neg
+    K = 96 - e
+    sg.add(f"v_lshrrev_b64 {P[0]}, {K}, {xp}", [xp], [P[0]])
+    if K == 32 and tp != xp:
+        u = xlo
+    else:
+        u = v[4]
+        if K == 32:
+            sg.add(f"v_mov_b32 {u}, {xlo}", [xlo], [u])
+        else:
+            sg.add(f"v_lshlrev_b32 {u}, {32 - K}, {xlo}", [xlo], [u])
+    sg.add(f"v_mad_u64_u32 {tp}, {JUNK}, {u}, 1, {P[0]}", [u, P[0]], [tp, JUNK])
+    sg.add(f"v_sub_co_u32_e64 {thi}, {c[0]}, {thi}, {u}", [thi, u], [thi, c[0]])
+    minus_eps_masked(sg, c[0], tp)
+    return neg
+
+
+def ct_core_x(sg, sl, a, b, neg, t, canon_out=False):
+    """In-place CT butterfly with the canonical t (= w b, or its negation when neg): not neg: b <- a - t, a <- a + t;
+    neg: b <- a + t, a <- a - t.  The destination of the first result is dead (its value is in t), so nothing needs a
+    temporary.  canon_out (a canonical): both outputs canonical (the sum by a select between s and s + EPS)."""
+    alo, ahi, ap = a
+    blo, bhi, bp = b
+    tlo, thi = t
+    c = sl.c
+    S, D = (b, a) if neg else (a, b)
+
+    def diff(dst):
+        sg.add(f"v_sub_co_u32_e64 {dst[0]}, {c[0]}, {alo}, {tlo}", [alo, tlo], [dst[0], c[0]])
+        sg.add(f"v_subb_co_u32_e64 {dst[1]}, {c[1]}, {ahi}, {thi}, {c[0]}", [ahi, thi, c[0]], [dst[1], c[1]])
+        minus_eps_masked(sg, c[1], dst[2])
+
+    def add(dst):
+        sg.add(f"v_add_co_u32_e64 {dst[0]}, {c[2]}, {alo}, {tlo}", [alo, tlo], [dst[0], c[2]])
+        sg.add(f"v_addc_co_u32_e64 {dst[1]}, {c[2]}, {ahi}, {thi}, {c[2]}", [ahi, thi, c[2]], [dst[1], c[2]])
+        if canon_out:
+            P3 = sl.P[3]
+            sg.add(f"v_mad_u64_u32 {P3}, {c[0]}, -1, 1, {dst[2]}", [dst[2]], [P3, c[0]])
+            mov64_masked(sg, ("or", c[0], c[2]), dst[2], P3)
+        else:
+            plus_eps_masked(sg, c[2], dst[2])
+
+    # the dead destination first (b, whose value t carries), then the other one in place
+    if neg:
+        add(S)
+        diff(D)
+    else:
+        diff(D)
+        add(S)
+
+
+def ct_x(sg, sl, a, b, S, b_canon=False):
+    """CT butterfly (a, b) with twiddle 2^S: t = 2^S b canonical in the slot's P1, then ct_core_x."""
+    t = (sl.v[2], sl.v[3])
+    if S % 96 == 0 and b_canon:
+        sg.add(f"v_mov_b64 {sl.P[1]}, {b[2]}", [b[2]], [sl.P[1]])
+        neg = S >= 96
+    else:
+        neg = tmul_x(sg, S, b, sl, t)
+    ct_core_x(sg, sl, a, b, neg, t)
+
+
+def gs_x(sg, sl, a, b, S, ac=False, bc=False):
+    """EXEC-masked gs (same contract): the difference goes to the slot's P1, the sum into a in place, then
+    b <- |w| (difference) canonical (tmul_x from P1 into b)."""
+    alo, ahi, ap = a
+    blo, bhi, bp = b
+    c, P = sl.c, sl.P
+    dl, dh, dpair = sl.v[2], sl.v[3], P[1]
+    e = S % 96
+    neg = (S >= 96) != (e >= 64)
+    both = ac and bc
+    if not both:
+        if neg and not ac:
+            canon(sg, sl, a)
+        if not neg and not bc:
+            canon(sg, sl, b)
+    # difference (the subtrahend is canonical): a - b, or b - a when the twiddle is negative
+    m, s_ = (b, a) if neg else (a, b)
+    sg.add(f"v_sub_co_u32_e64 {dl}, {c[0]}, {m[0]}, {s_[0]}", [m[0], s_[0]], [dl, c[0]])
+    sg.add(f"v_subb_co_u32_e64 {dh}, {c[1]}, {m[1]}, {s_[1]}, {c[0]}", [m[1], s_[1], c[0]], [dh, c[1]])
+    minus_eps_masked(sg, c[1], dpair)
+    # sum into a in place
+    sg.add(f"v_add_co_u32_e64 {alo}, {c[2]}, {alo}, {blo}", [alo, blo], [alo, c[2]])
+    sg.add(f"v_addc_co_u32_e64 {ahi}, {c[2]}, {ahi}, {bhi}, {c[2]}", [ahi, bhi, c[2]], [ahi, c[2]])
+    if both:
+        sg.add(f"v_mad_u64_u32 {P[3]}, {c[0]}, -1, 1, {ap}", [ap], [P[3], c[0]])
+        mov64_masked(sg, ("or", c[0], c[2]), ap, P[3])
+    else:
+        plus_eps_masked(sg, c[2], ap)
+    tmul_x(sg, S, (dl, dh, dpair), sl, (blo, bhi))
+    return both, True
 
 
 # ------------------------------------------------------------------------------------------------
@@ -524,6 +756,7 @@ S_TB = 86    # s[86:93]: table bases
 S_PAR = 20   # s[20:21]: odd-lane mask
 S_X15 = 27   # s27 = 0x11111111 = EPS / 15: d - EPS = d + (-15) * 0x11111111 in one v_mad_i64_i32
 S_EXE = 22   # s[22:23]: saved exec
+EXEC_RESTORE = f"s_mov_b64 exec, s[{S_EXE}:{S_EXE + 1}]"
 
 
 def bases(body, reg_g, dst):
@@ -721,6 +954,16 @@ def regroup(sg, dmap, k, tmp, to_pairs, k2=None):
         sg.add(f"v_cndmask_b32_dpp {hi0}, {hi1}, {hi0}, vcc {dpp}", [hi1, hi0, "vcc"], [hi0], "dpp")
         dmap[kk2] = int(T0[1:])
         return old
+    if EXEC_MASK:
+        # both directions: T = partner's x[k], U = partner's x[k2] (four DPP moves, all lanes), then the odd lanes take
+        # x[k] <- U and the even lanes x[k2] <- T, each one EXEC-masked 64-bit move instead of two selects
+        sg.add(f"v_mov_b32_dpp {T0}, {lo0} {dpp}", [lo0], [T0], "dpp")
+        sg.add(f"v_mov_b32_dpp {T1}, {hi0} {dpp}", [hi0], [T1], "dpp")
+        sg.add(f"v_mov_b32_dpp {U0}, {lo1} {dpp}", [lo1], [U0], "dpp")
+        sg.add(f"v_mov_b32_dpp {U1}, {hi1} {dpp}", [hi1], [U1], "dpp")
+        mov64_masked(sg, par, p0, pair_of(U0, U1))
+        mov64_masked(sg, ("not", par), p1, pair_of(T0, T1))
+        return None
     if to_pairs:
         # T = partner x[k], U = partner x[k+16]; even: x[k+16] <- T ; odd: x[k] <- U
         sg.add(f"v_mov_b32_dpp {T0}, {lo0} {dpp}", [lo0], [T0], "dpp")
@@ -795,6 +1038,33 @@ def tmul_lane(sg, S_even, S_odd, x, sl, tlo, thi, par3, amt):
     op_up = "v_add_u32" if e1 > e0 else "v_sub_u32"      # amount grows with the exponent
     op_dn = "v_sub_u32" if e1 > e0 else "v_add_u32"
     cls = shift_class(e0)
+    if EXEC_MASK:
+        tp = pair_of(tlo, thi)
+        if cls in (0, 1):
+            r0, w0 = (e0, 32 - e0) if cls == 0 else (e0 - 32, 64 - e0)
+            sg.add(f"{op_up} {A0}, {r0}, {par3}", [par3], [A0])
+            sg.add(f"{op_dn} {A1}, {w0}, {par3}", [par3], [A1])
+            sg.add(f"v_lshlrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
+            if cls == 0:
+                sg.add(f"v_bfe_u32 {v[4]}, {xhi}, {A1}, {A0}", [xhi, A1, A0], [v[4]])
+            else:
+                sg.add(f"v_lshrrev_b32 {v[4]}, {A1}, {xhi}", [A1, xhi], [v[4]])
+            sg.add(f"v_mad_u64_u32 {tp}, {c[0]}, {v[4]}, -1, {P[0]}", [v[4], P[0]], [tp, c[0]])
+            if cls == 1:
+                plus_eps_masked(sg, c[0], tp)
+                sg.add(f"v_lshlrev_b64 {P[3]}, 32, {tp}", [tp], [P[3]])
+                sg.add(f"v_mad_u64_u32 {tp}, {c[0]}, {thi}, -1, {P[3]}", [thi, P[3]], [tp, c[0]])
+            sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {tp}", [tp], [P[0], c[1]])
+            mov64_masked(sg, ("or", c[1], c[0]), tp, P[0])
+            return neg
+        sg.add(f"{op_dn} {A0}, {96 - e0}, {par3}", [par3], [A0])
+        sg.add(f"{op_up} {A1}, {e0 - 64}, {par3}", [par3], [A1])
+        sg.add(f"v_lshrrev_b64 {P[0]}, {A0}, {xp}", [A0, xp], [P[0]])
+        sg.add(f"v_lshlrev_b32 {v[4]}, {A1}, {xlo}", [A1, xlo], [v[4]])
+        sg.add(f"v_mad_u64_u32 {tp}, {JUNK}, {v[4]}, 1, {P[0]}", [v[4], P[0]], [tp, JUNK])
+        sg.add(f"v_sub_co_u32_e64 {thi}, {c[0]}, {thi}, {v[4]}", [thi, v[4]], [thi, c[0]])
+        minus_eps_masked(sg, c[0], tp)
+        return neg
     if cls == 0:
         # r = e, h = top r bits of x_hi (v_bfe: width 0 gives 0, so r = 0 needs no special case)
         sg.add(f"{op_up} {A0}, {e0}, {par3}", [par3], [A0])
