@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Integer-VALU issue model of the generated bodies (tools/valu_cost.py: instruction mix x the issue
 # costs measured by tools/valu_probe.hip; tests/test_bench_contract.py keeps these in sync), and the
 # MI355X peak engine clock it is priced at.
-VALU_CYCLES = {"fwd": 11321.0, "inv": 11486.8, "pbs_step": 29576.1, "pbs_sol_step": 29759.5, "ext_bnf": 28387.2}
+VALU_CYCLES = {"fwd": 14341.4, "inv": 14447.5, "pbs_step": 35478.9, "pbs_sol_step": 35800.2, "ext_bnf": 34290.0}
 SIMDS, PEAK_CLOCK_HZ = 256 * 4, 2.4e9
 # PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
 PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
@@ -72,7 +72,8 @@ def parse():
 LEG_SECONDS = 0.3  # every non-headline leg times at least this much GPU work (no --steps-scaled legs)
 # order of the legs in the JSON line (not the order they run in): the driver keeps only the tail of stdout, so the
 # config-3 / config-4 legs come last, followed only by the compact legs_summary
-LEG_ORDER = ("pbs_shapes", "pbs_shapes_fft", "keyswitch", "ks_pbs", "ks_pbs_fft", "ext_product_fft", "bsk_conversion",
+LEG_ORDER = ("pbs_shapes", "pbs_shapes_fft", "keyswitch", "ks_pbs", "ks32_pbs", "ks_pbs_fft", "ext_product_fft",
+             "bsk_conversion",
              "pbs_fft", "ext_product", "pbs_solinas", "pbs")
 
 
@@ -763,6 +764,62 @@ def bench_ks_pbs(args, eng, torch, dev, world, barrier, dist):
                        "batch_per_gpu": batch}}
 
 
+KS32_IN, KS32_N_LWE, KS32_BASE_LOG, KS32_LEVEL, KS32_MOD_LOG = 2048, 879, 2, 8, 21
+
+
+def bench_ks32_pbs(args, eng, torch, dev, world, barrier, dist):
+    """The HPU KS32 bootstrap at V1_5_HPU_PARAM_MESSAGE_2_CARRY_2_KS32_PBS_TUNIFORM_2M128 (shortint/parameters/v1_5/
+    hpu.rs:57-76), the parameter set of BASELINE.md's one NTT-PBS figure (HPU, 14,167 KS-PBS/s): keyswitch with a scalar
+    change (2048 -> 879, base 2^2, 8 levels, u32 output of modulus 2^21), the centered binary modulus switch of the u32
+    LWE to 2N, and the NTT BNF bootstrap (n 879, N 2048, base 2^23, level 1) on the switched input — the order of the
+    HPU mockup (mockups/tfhe-hpu-mockup/src/lib.rs:720-761, one LUT); both keys resident, one stream."""
+    KS, M = eng.lwe_keyswitch, eng.ntt64_pbs
+    batch, n_lwe = args.pbs_batch, KS32_N_LWE
+    ksk = torch.empty((KS32_IN, KS32_LEVEL, n_lwe + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(ksk, SEED + 70, 0)
+    ksk32 = (ksk & ((1 << 32) - 1)).to(torch.int32)  # u32 key words (their low 11 bits need not be 0 for timing)
+    del ksk
+    kkey = KS.LweKeyswitchKey32(ksk32, KS32_BASE_LOG, KS32_LEVEL, KS32_MOD_LOG)
+    del ksk32
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    bsk = torch.empty((n_lwe, PBS_LEVEL, 2, 2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(bsk, SEED + 71, SOLINAS_P)
+    bkey = M.NttBootstrapKey(plan, bsk, PBS_BASE_LOG, PBS_LEVEL, M.BNF)
+    del bsk
+    lut = torch.empty((2, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(lut, SEED + 72, 0)
+    big = torch.empty((batch, KS32_IN + 1), dtype=torch.int64, device=dev)
+    eng.fill_uniform(big, SEED + 73, 0)
+    small = torch.empty((batch, n_lwe + 1), dtype=torch.int32, device=dev)
+    switched = torch.empty((batch, n_lwe + 1), dtype=torch.int64, device=dev)
+    out = torch.empty((batch, N + 1), dtype=torch.int64, device=dev)
+    log2n = (2 * N).bit_length() - 1
+
+    def run_ks():
+        KS.keyswitch_lwe_ciphertext_with_scalar_change(kkey, big, small)
+        KS.lwe_ciphertext_centered_binary_modulus_switch32(small, switched, log2n)
+
+    def run():
+        run_ks()
+        M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(switched, out, lut, bkey, M.MS_PRE_SWITCHED)
+
+    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev)
+    K_ks, el_ks, ks_ms = timed_leg(run_ks, torch, barrier, dist, dev)
+    del bkey, kkey
+    return {"metric": "KS-PBS/sec, HPU KS32 parameters (V1_5_HPU_PARAM_MESSAGE_2_CARRY_2_KS32_PBS_TUNIFORM_2M128)",
+            "value": world * batch * K / el, "unit": "KS-PBS/s", "ms_per_step": el / K * 1e3, "steps": K,
+            "kernel_ms": kernel_ms,
+            "ntt_equivalents_per_s": world * batch * K / el * 4 * n_lwe,
+            "keyswitch_and_switch": {"value": world * batch * K_ks / el_ks, "unit": "KS/s", "kernel_ms": ks_ms,
+                                     "steps": K_ks},
+            "vs_hpu_published": {"value": 14167.0, "unit": "KS-PBS/s",
+                                 "source": "BASELINE.md: AMD Alveo V80 HPU, batch 12 (hpu-programmable-bootstrapping.md)"},
+            "config": {"workload": "keyswitch_lwe_ciphertext_with_scalar_change 2048 -> 879 (B 2^2, L 8, u32 mod 2^21) "
+                                   "-> lwe_ciphertext_centered_binary_modulus_switch (u32, 2N) -> NTT BNF PBS "
+                                   "(n 879, N 2048, B 2^23, L 1) on the switched input, one stream",
+                       "batch_per_gpu": batch}}
+
+
 def bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist):
     """The shortint server key's KS-PBS as tfhe-rs runs it by default: keyswitch (2048 -> 918, B 2^4, L 4) then the
     f64-FFT PBS (n 918, N 2048, B 2^23, L 1), both keys resident, one stream."""
@@ -1055,6 +1112,7 @@ def main():
                                       for name in SHAPE_LEGS}
         legs["keyswitch"] = bench_keyswitch(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs"] = bench_ks_pbs(args, eng, torch, dev, world, barrier, dist)
+        legs["ks32_pbs"] = bench_ks32_pbs(args, eng, torch, dev, world, barrier, dist)
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
         legs["ext_product_fft"] = bench_ext_product_fft(args, eng, torch, dev, world, barrier, dist)
         legs["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier, dist)

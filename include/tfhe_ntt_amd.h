@@ -492,6 +492,33 @@ int mi_lwe_ksk_info(const mi_lwe_ksk *key, size_t *in_dim, size_t *out_dim, int 
 int mi_lwe_keyswitch_batch(const mi_lwe_ksk *key, uint64_t *lwe_out, const uint64_t *lwe_in, size_t batch,
                            void *stream);
 
+/* ---- KS32: the keyswitch with a scalar change of the HPU KS32 parameter sets ----------------------------------
+ * keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447), as V1_5_HPU_PARAM_MESSAGE_2_CARRY_2_KS32_
+ * PBS_TUNIFORM_2M128 runs it (shortint/parameters/v1_5/hpu.rs:57-76: 2048 -> 879, ks base 2^2, 8 levels,
+ * post_keyswitch_ciphertext_modulus 2^21; mockups/tfhe-hpu-mockup/src/lib.rs:720-736): u64 input LWEs (native
+ * modulus) -> u32 output LWEs of modulus 2^out_modulus_log, power-of-two encoded in the MSBs of the u32 words, as the
+ * reference stores non-native power-of-two moduli.  The key: in_dim blocks of `level` u32 LWE ciphertexts of
+ * out_dim + 1 words (the LweKeyswitchKey<Vec<u32>> layout, levels as generate_lwe_keyswitch_key writes them).
+ * The body is closest_representable(b) at out_modulus_log bits, shifted down by 32; every mask digit of the u64
+ * SignedDecomposer (base_log, level) times its key row is subtracted with wrapping u32 arithmetic.
+ * MI_ERR_INVALID_ARG where the reference asserts (base_log * level > 32) or out_modulus_log is outside [1, 32];
+ * the same 2^17 GEMM-depth bound as mi_lwe_ksk_create.  Bit-exact. */
+typedef struct mi_lwe_ksk32 mi_lwe_ksk32;
+int mi_lwe_ksk32_create(const uint32_t *ksk, size_t in_dim, size_t out_dim, int base_log, int level,
+                        int out_modulus_log, int device, void *stream, mi_lwe_ksk32 **out_key);
+int mi_lwe_ksk32_destroy(mi_lwe_ksk32 *key);
+int mi_lwe_ksk32_info(const mi_lwe_ksk32 *key, size_t *in_dim, size_t *out_dim, int *base_log, int *level,
+                      int *out_modulus_log);
+int mi_lwe_keyswitch32_batch(const mi_lwe_ksk32 *key, uint32_t *lwe_out, const uint64_t *lwe_in, size_t batch,
+                             void *stream);
+/* The modulus switch of u32 LWEs (lwe_dim mask words + body) to [0, 2^log_modulus): MI_MS_STANDARD =
+ * lwe_ciphertext_modulus_switch, MI_MS_CENTERED = lwe_ciphertext_centered_binary_modulus_switch
+ * (algorithms/modulus_switch.rs:14-104, at Scalar = u32), materialised as the ModulusSwitchedLweCiphertext values
+ * (entities/modulus_switched_lwe_ciphertext.rs:150-175): switched[b] = lwe_dim + 1 u64 in [0, 2^log_modulus), the
+ * MI_MS_PRE_SWITCHED input of mi_blind_rotate_ntt64_batch / mi_pbs_ntt64_batch (log_modulus = log2(2N)). */
+int mi_lwe_modulus_switch32_batch(uint64_t *switched, const uint32_t *lwe_in, size_t lwe_dim, size_t batch,
+                                  int log_modulus, int ms_mode, int device, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

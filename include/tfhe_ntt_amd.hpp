@@ -266,6 +266,44 @@ inline void keyswitch_lwe_ciphertext(const LweKeyswitchKey& key, const uint64_t*
   check(mi_lwe_keyswitch_batch(key.raw(), lwe_out, lwe_in, batch, stream));
 }
 
+// LweKeyswitchKey<Vec<u32>> of the KS32 parameter sets (shortint/parameters/v1_5/hpu.rs:57-76); move-only
+class LweKeyswitchKey32 {
+ public:
+  LweKeyswitchKey32(const uint32_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level, int out_modulus_log,
+                    int device = 0, void* stream = nullptr)
+      : in_(in_dim), out_(out_dim) {
+    check(mi_lwe_ksk32_create(ksk, in_dim, out_dim, base_log, level, out_modulus_log, device, stream, &raw_));
+  }
+  LweKeyswitchKey32(LweKeyswitchKey32&& o) noexcept : raw_(std::exchange(o.raw_, nullptr)), in_(o.in_), out_(o.out_) {}
+  LweKeyswitchKey32(const LweKeyswitchKey32&) = delete;
+  LweKeyswitchKey32& operator=(const LweKeyswitchKey32&) = delete;
+  ~LweKeyswitchKey32() {
+    if (raw_) (void)mi_lwe_ksk32_destroy(raw_);
+  }
+  const mi_lwe_ksk32* raw() const noexcept { return raw_; }
+  size_t input_key_lwe_dimension() const noexcept { return in_; }
+  size_t output_key_lwe_dimension() const noexcept { return out_; }
+
+ private:
+  mi_lwe_ksk32* raw_ = nullptr;
+  size_t in_, out_;
+};
+
+// keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447) over a batch: u64 in, u32 out
+inline void keyswitch_lwe_ciphertext_with_scalar_change(const LweKeyswitchKey32& key, const uint64_t* lwe_in,
+                                                        uint32_t* lwe_out, size_t batch, void* stream = nullptr) {
+  check(mi_lwe_keyswitch32_batch(key.raw(), lwe_out, lwe_in, batch, stream));
+}
+
+// lwe_ciphertext_[centered_binary_]modulus_switch of u32 LWEs (modulus_switch.rs:14-104), materialised into
+// [0, 2^log_modulus) u64 values: the MI_MS_PRE_SWITCHED input of the blind rotation
+inline void lwe_ciphertext_modulus_switch32(const uint32_t* lwe_in, uint64_t* switched, size_t lwe_dimension,
+                                            size_t batch, int log_modulus, bool centered, int device = 0,
+                                            void* stream = nullptr) {
+  check(mi_lwe_modulus_switch32_batch(switched, lwe_in, lwe_dimension, batch, log_modulus,
+                                      centered ? MI_MS_CENTERED : MI_MS_STANDARD, device, stream));
+}
+
 // On-disk NTT bootstrap key (entities/ntt_lwe_bootstrap_key.rs:26-33): plain bincode or the versioned
 // form, parsed and written by the library (mi_ntt_bsk_parse / mi_ntt_bsk_write, pure host code, no
 // device needed); the layouts are documented in include/tfhe_ntt_amd.h.  Same bytes as

@@ -414,6 +414,9 @@ def sample_extract_nth(glwe, n, k, nth, q=0):
 _KS_SIGS = {
     "ora_lwe_keyswitch": (None, [_p64, _sz, _sz, ctypes.c_int, ctypes.c_int, _p64, _p64]),
     "ora_lwe_keyswitch_batch": (None, [_p64, _sz, _sz, ctypes.c_int, ctypes.c_int, _p64, _p64, _sz, ctypes.c_int]),
+    "ora_lwe_keyswitch32_batch": (None, [ctypes.c_void_p, _sz, _sz, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64,
+                                         ctypes.c_void_p, _sz, ctypes.c_int]),
+    "ora_lwe_ms32": (None, [ctypes.c_void_p, _sz, ctypes.c_int, ctypes.c_int, _p64]),
 }
 _ks_ready = False
 
@@ -440,4 +443,33 @@ def lwe_keyswitch(ksk, lwe_in, out_dim, base_log, level, threads=8):
     batch = x.size // (in_dim + 1)
     out = np.zeros(x.shape[:-1] + (out_dim + 1,), np.uint64)
     _klib().ora_lwe_keyswitch_batch(_ptr(k), in_dim, out_dim, base_log, level, _ptr(x), _ptr(out), batch, threads)
+    return out
+
+
+def lwe_keyswitch32(ksk, lwe_in, out_dim, base_log, level, out_mod_log, threads=8):
+    """keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447) over a batch: lwe_in u64
+    (..., in_dim + 1), ksk u32 (in_dim, level, out_dim + 1) -> u32 (..., out_dim + 1)."""
+    k = np.ascontiguousarray(ksk, dtype=np.uint32)
+    x = _u(lwe_in)
+    in_dim = x.shape[-1] - 1
+    assert k.size == in_dim * level * (out_dim + 1), "ksk shape"
+    batch = x.size // (in_dim + 1)
+    out = np.zeros(x.shape[:-1] + (out_dim + 1,), np.uint32)
+    _klib().ora_lwe_keyswitch32_batch(k.ctypes.data, in_dim, out_dim, base_log, level, out_mod_log, _ptr(x),
+                                      out.ctypes.data, batch, threads)
+    return out
+
+
+def lwe_ms32(lwe, log_mod, centered):
+    """lwe_ciphertext_[centered_binary_]modulus_switch of u32 LWEs (modulus_switch.rs:14-104) -> u64 values in
+    [0, 2^log_mod), same shape."""
+    x = np.ascontiguousarray(lwe, dtype=np.uint32)
+    dim = x.shape[-1] - 1
+    out = np.zeros(x.shape, np.uint64)
+    flat, oflat = x.reshape(-1, dim + 1), out.reshape(-1, dim + 1)
+    for b in range(flat.shape[0]):
+        row = np.ascontiguousarray(flat[b])
+        orow = np.zeros(dim + 1, np.uint64)
+        _klib().ora_lwe_ms32(row.ctypes.data, dim, log_mod, 1 if centered else 0, _ptr(orow))
+        oflat[b] = orow
     return out

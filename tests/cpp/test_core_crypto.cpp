@@ -5,6 +5,8 @@
 //   add_external_product_ntt64_assign (BNF)        ntt64_bnf_pbs.rs:541-681
 //   programmable_bootstrap_ntt64_lwe_ciphertext    ntt64_bnf_pbs.rs:469-540 (standard modulus switch)
 //   keyswitch_lwe_ciphertext                       lwe_keyswitch.rs:137-227 (2048 -> 918, B 2^4, L 4)
+//   keyswitch_lwe_ciphertext_with_scalar_change    lwe_keyswitch.rs:331-447 (KS32: 2048 -> 879, B 2^2, L 8, 2^21)
+//   lwe_ciphertext_centered_binary_modulus_switch  modulus_switch.rs:35-104 (u32 LWEs)
 // and the f64-FFT mirror (namespace fft64) against exact integer arithmetic within the f64 error bound:
 //   forward_as_torus -> backward_as_torus round trip, add_external_product_assign vs the exact negacyclic product
 // Needs a HIP device.  Build: make -C tests/cpp.
@@ -121,6 +123,36 @@ int main() {
     cc::LweKeyswitchKey key(d_ksk.p, in_dim, out_dim, bl, lv);
     cc::keyswitch_lwe_ciphertext(key, d_lwe.p, d_out.p, batch);
     EXPECT(d_out.host() == want);
+  }
+
+  // KS32: keyswitch_lwe_ciphertext_with_scalar_change 2048 -> 879, base 2^2, 8 levels, u32 output mod 2^21 (the HPU
+  // KS32 parameters), then the centered binary modulus switch of the u32 LWEs to 2N = 4096, batch 6
+  {
+    const size_t in_dim = 2048, out_dim = 879, batch = 6;
+    const int bl = 2, lv = 8, w = 21;
+    const auto raw = uniform(109, 0, in_dim * lv * (out_dim + 1)), lwe = uniform(110, 0, batch * (in_dim + 1));
+    std::vector<uint32_t> ksk(raw.size());
+    for (size_t i = 0; i < raw.size(); ++i) ksk[i] = (uint32_t)raw[i] & ~((1u << (32 - w)) - 1);
+    std::vector<uint32_t> want(batch * (out_dim + 1));
+    ora_lwe_keyswitch32_batch(ksk.data(), in_dim, out_dim, bl, lv, w, lwe.data(), want.data(), batch, 4);
+    uint32_t *d_ksk = nullptr, *d_out = nullptr;
+    EXPECT(hipMalloc(reinterpret_cast<void**>(&d_ksk), ksk.size() * 4) == hipSuccess);
+    EXPECT(hipMalloc(reinterpret_cast<void**>(&d_out), want.size() * 4) == hipSuccess);
+    EXPECT(hipMemcpy(d_ksk, ksk.data(), ksk.size() * 4, hipMemcpyHostToDevice) == hipSuccess);
+    Dev d_lwe(lwe), d_sw(batch * (out_dim + 1));
+    cc::LweKeyswitchKey32 key(d_ksk, in_dim, out_dim, bl, lv, w);
+    cc::keyswitch_lwe_ciphertext_with_scalar_change(key, d_lwe.p, d_out, batch);
+    std::vector<uint32_t> got(want.size());
+    EXPECT(hipDeviceSynchronize() == hipSuccess);
+    EXPECT(hipMemcpy(got.data(), d_out, got.size() * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    EXPECT(got == want);
+    cc::lwe_ciphertext_modulus_switch32(d_out, d_sw.p, out_dim, batch, 12, true);
+    std::vector<uint64_t> want_sw(batch * (out_dim + 1));
+    for (size_t b = 0; b < batch; ++b)
+      ora_lwe_ms32(want.data() + b * (out_dim + 1), out_dim, 12, 1, want_sw.data() + b * (out_dim + 1));
+    EXPECT(d_sw.host() == want_sw);
+    (void)hipFree(d_ksk);
+    (void)hipFree(d_out);
   }
 
   // errors surface as tfhe_ntt_amd::Error with the C status (base_log * level >= 64)

@@ -379,6 +379,35 @@ def test_pbs_solinas_config4_shape(engine, plan, ctx, batch):
         assert np.array_equal(got[b], want)
 
 
+def test_pbs_solinas_config4_full_batch(engine, plan, ctx, oracle):
+    """The Solinas-modulus PBS (ntt64_pbs.rs:482-538, the reference's own NTT-PBS bench shape, pbs_bench.rs:646-905) at
+    config 4's full batch: 4096 PBS at n = 918, B = 2^23, l = 1 on a random key, bit-exact vs the oracle on ALL 4096
+    outputs — the oracle's Solinas PBS with its AVX-512 transform restatement, itself checked equal
+    to the scalar restatement on 8 of them first."""
+    g = H.rng(4096 + 918 + 1)
+    n_lwe, base_log, level, batch = 918, 23, 1, 4096
+    bsk = rand_q(g, (n_lwe, level, K + 1, K + 1, N), P)
+    lut = rand_q(g, (K + 1, N), P)
+    lwe = _pbs_inputs(g, batch, n_lwe, P)
+    lwe[:, 9::17] = np.uint64(P - 1)
+    M = engine.ntt64_pbs
+    key = M.NttBootstrapKey(plan, dev(bsk), base_log, level, M.SOLINAS)
+    out = dev(np.zeros((batch, K * N + 1), np.uint64))
+    M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized(dev(lwe), out, dev(lut), key)
+    got = host(out)
+    idx = np.array([0, 1, 511, 1024, 2047, 2048, 3071, batch - 1])
+    scalar = ctx.pbs_batch_solinas(lwe[idx], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, threads=8)
+    assert np.array_equal(got[idx], scalar)
+    oracle.pbs_set_fast_ntt(True)
+    try:
+        fast8 = ctx.pbs_batch_solinas(lwe[idx], lut.reshape(-1), bsk.reshape(-1), K, base_log, level, threads=8)
+        assert np.array_equal(fast8, scalar)
+        want = ctx.pbs_batch_solinas(lwe, lut.reshape(-1), bsk.reshape(-1), K, base_log, level, threads=16)
+    finally:
+        oracle.pbs_set_fast_ntt(False)
+    assert np.array_equal(got, want)
+
+
 SHAPES = [(1024, 1), (1024, 2), (2048, 2), (4096, 1), (4096, 2)]
 
 

@@ -258,3 +258,25 @@ def bsk_gen_fast(g, oracle, lwe_sk, glwe_sk, base_log, level, noise_log2, q=0):
     bsk[..., :k, :] = masks
     bsk[..., k, :] = body
     return bsk
+
+
+def ksk32_gen(g, in_sk, out_sk, base_log, level, noise_log2, out_mod_log=32):
+    """LweKeyswitchKey<Vec<u32>> of output modulus 2^out_mod_log (values in the MSBs, as the reference encodes a
+    non-native power of two): block i, entry li encrypts s_in[i] << (32 - base_log * (level - li)) under out_sk
+    (lwe_keyswitch_key_generation.rs:169-199 at OutputScalar = u32).  Test infrastructure only."""
+    in_dim, out_dim = in_sk.size, out_sk.size
+    scale = np.uint32(1 << (32 - out_mod_log)) if out_mod_log < 32 else np.uint32(1)
+    pts = np.array([(int(s) << (32 - base_log * (level - li))) % 2**32 for s in in_sk for li in range(level)],
+                   dtype=np.uint32)
+    mask = g.integers(0, 1 << out_mod_log, size=(pts.size, out_dim), dtype=np.uint64).astype(np.uint32) * scale
+    noise = (g.integers(-(1 << noise_log2), 1 << noise_log2, size=pts.size, dtype=np.int64)
+             .astype(np.uint32) * scale)
+    with np.errstate(over="ignore"):
+        body = (mask.astype(np.uint64) * out_sk.astype(np.uint64)).sum(axis=1).astype(np.uint32) + pts + noise
+    return np.concatenate([mask, body[:, None]], axis=1).reshape(in_dim, level, out_dim + 1)
+
+
+def lwe32_decrypt_batch(cts, lwe_sk):
+    with np.errstate(over="ignore"):
+        return (cts[..., -1].astype(np.uint64) - (cts[..., :-1].astype(np.uint64) * lwe_sk).sum(axis=-1)) \
+            .astype(np.uint32)

@@ -20,6 +20,7 @@
 
 #include "scratch.hpp"
 #include "build_info.hpp"  // build/ (Makefile): MI_SOURCE_HASH
+#include "keyswitch_launch.hpp"
 #include "c_api_internal.hpp"
 #include "mi_arith.hpp"
 #include "ntt64_tw_tables.hpp"
@@ -1268,6 +1269,114 @@ int mi_lwe_keyswitch_batch(const mi_lwe_ksk* key, uint64_t* lwe_out, const uint6
                                       key->base_log, key->level, s);
   (void)mi::scratch_free(digits, s);
   return e == hipSuccess ? MI_OK : hip_fail(e, "keyswitch launch");
+}
+
+// ---- KS32: keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447) ------------------------------
+// The keyswitch of the HPU KS32 parameter sets (shortint/parameters/v1_5/hpu.rs:57-76: 2048 -> 879, base 2^2, 8
+// levels, post_keyswitch_ciphertext_modulus 2^21): u64 input LWEs of the native modulus, u32 key and output words
+// with the power-of-two output modulus 2^out_modulus_log encoded in the MSBs, as the reference stores it.
+
+struct mi_lwe_ksk32 {
+  int device = 0;
+  size_t in_dim = 0, out_dim = 0;
+  int base_log = 0, level = 0, out_modulus_log = 32;
+  void* frag = nullptr;  // byte-plane MFMA fragments of the zero-extended u32 key words (keyswitch.hip)
+};
+
+int mi_lwe_ksk32_create(const uint32_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level,
+                        int out_modulus_log, int device, void* stream, mi_lwe_ksk32** out_key) {
+  if (!out_key) return fail(MI_ERR_INVALID_ARG, "out_key is NULL");
+  *out_key = nullptr;
+  if (!ksk) return fail(MI_ERR_INVALID_ARG, "ksk is NULL");
+  if (in_dim == 0 || out_dim == 0 || in_dim > 0xFFFFFFull || out_dim > 0xFFFFFFull)
+    return fail(MI_ERR_INVALID_ARG, "lwe dimension out of range");
+  if (out_modulus_log < 1 || out_modulus_log > 32)
+    return fail(MI_ERR_INVALID_ARG, "output modulus must be 2^w with 1 <= w <= 32");
+  // lwe_keyswitch.rs:378-384: base_log * level <= OutputScalar::BITS (and SignedDecomposer::new's >= 1 each)
+  if (base_log < 1 || level < 1 || base_log * level > 32)
+    return fail(MI_ERR_INVALID_ARG, "decomposition base_log * level must be in [1, 32]");
+  if ((double)in_dim * level * mi::ks_digit_bytes_per_term(base_log) >= 131072.0)
+    return fail(MI_ERR_UNSUPPORTED, "in_dim * level * ceil((base_log + 1) / 8) must stay below 2^17");
+  mi_lwe_ksk32* key = new (std::nothrow) mi_lwe_ksk32;
+  if (!key) return fail(MI_ERR_OOM, "host allocation failed");
+  key->device = device;
+  key->in_dim = in_dim;
+  key->out_dim = out_dim;
+  key->base_log = base_log;
+  key->level = level;
+  key->out_modulus_log = out_modulus_log;
+  DeviceGuard g(device);
+  if (!g.ok) {
+    delete key;
+    return fail(MI_ERR_INVALID_ARG, "bad device");
+  }
+  if (hipMalloc(&key->frag, mi::ks_key_bytes(in_dim, out_dim, base_log, level)) != hipSuccess) {
+    delete key;
+    return fail(MI_ERR_OOM, "keyswitch key allocation failed");
+  }
+  hipError_t e = mi::launch_ksk32_prepare(key->frag, ksk, in_dim, out_dim, base_log, level, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) {
+    (void)hipFree(key->frag);
+    delete key;
+    return hip_fail(e, "keyswitch key preparation");
+  }
+  *out_key = key;
+  return MI_OK;
+}
+
+int mi_lwe_ksk32_destroy(mi_lwe_ksk32* key) {
+  if (!key) return MI_OK;
+  {
+    DeviceGuard g(key->device);
+    if (key->frag) (void)hipFree(key->frag);
+  }
+  delete key;
+  return MI_OK;
+}
+
+int mi_lwe_ksk32_info(const mi_lwe_ksk32* key, size_t* in_dim, size_t* out_dim, int* base_log, int* level,
+                      int* out_modulus_log) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (in_dim) *in_dim = key->in_dim;
+  if (out_dim) *out_dim = key->out_dim;
+  if (base_log) *base_log = key->base_log;
+  if (level) *level = key->level;
+  if (out_modulus_log) *out_modulus_log = key->out_modulus_log;
+  return MI_OK;
+}
+
+int mi_lwe_keyswitch32_batch(const mi_lwe_ksk32* key, uint32_t* lwe_out, const uint64_t* lwe_in, size_t batch,
+                             void* stream) {
+  if (!key) return fail(MI_ERR_INVALID_ARG, "key is NULL");
+  if (batch == 0) return MI_OK;
+  if (!lwe_out || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (batch > 0x3FFFFFull) return fail(MI_ERR_INVALID_ARG, "batch too large");
+  const hipStream_t s = (hipStream_t)stream;
+  DeviceGuard g(key->device);
+  void* digits = nullptr;
+  if (mi::scratch_alloc((void**)&digits, mi::ks_digit_bytes(key->in_dim, key->base_log, key->level, batch), s) != hipSuccess)
+    return fail(MI_ERR_OOM, "scratch allocation failed");
+  hipError_t e = mi::launch_keyswitch32(lwe_out, lwe_in, key->frag, digits, batch, key->in_dim, key->out_dim,
+                                        key->base_log, key->level, key->out_modulus_log, s);
+  (void)mi::scratch_free(digits, s);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "keyswitch launch");
+}
+
+int mi_lwe_modulus_switch32_batch(uint64_t* switched, const uint32_t* lwe_in, size_t lwe_dim, size_t batch,
+                                  int log_modulus, int ms_mode, int device, void* stream) {
+  if (batch == 0) return MI_OK;
+  if (!switched || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
+  if (lwe_dim == 0 || lwe_dim > 0xFFFFFFull || batch > 0xFFFFFFFFull)
+    return fail(MI_ERR_INVALID_ARG, "lwe dimension or batch out of range");
+  if (log_modulus < 1 || log_modulus > 32) return fail(MI_ERR_INVALID_ARG, "log_modulus must be in [1, 32]");
+  if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED)
+    return fail(MI_ERR_INVALID_ARG, "ms_mode must be MI_MS_STANDARD or MI_MS_CENTERED");
+  DeviceGuard g(device);
+  if (!g.ok) return fail(MI_ERR_INVALID_ARG, "bad device");
+  hipError_t e = mi::launch_lwe_ms32(switched, lwe_in, lwe_dim, batch, log_modulus, ms_mode == MI_MS_CENTERED,
+                                     (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "modulus switch launch");
 }
 
 }  // extern "C"

@@ -32,6 +32,7 @@
 #include <stdint.h>
 
 #include "ntt64_launch.hpp"
+#include "keyswitch_launch.hpp"
 
 namespace mi {
 namespace ks {
@@ -75,6 +76,7 @@ __device__ __forceinline__ int8_t signed_byte(u64 x, int t) {
 
 struct Shape {
   uint32_t in_dim, out_size, level, base_log, nd, K, KB, CT;
+  uint32_t body_log;  // KS32 (keyswitch_lwe_ciphertext_with_scalar_change): the output modulus 2^body_log
 };
 
 __device__ __forceinline__ uint4 pack16(const int8_t (&b)[16]) {
@@ -102,7 +104,9 @@ static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 mea
 // frag[(((cg * KB + kb) * GN + ci) * 8 + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
 // column 16 (GN cg + ci) + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
 // (in_dim blocks of `level` LWEs) shifted left by 8 s.
-__global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ frag, const u64* __restrict__ ksk,
+// W = u64 (native keyswitch) or uint32_t (KS32: the u32 key words zero-extended; only planes 0..3 matter mod 2^32)
+template <typename W>
+__global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ frag, const W* __restrict__ ksk,
                                                           Shape s) {
   const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;  // CT is a multiple of GN
   for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ fr
     for (int j = 0; j < 16; ++j) {
       const uint32_t k = kb * 64 + 16 * (lane >> 4) + j;
       const uint32_t row = k / s.nd, sh = 8 * (k % s.nd);
-      const u64 x = (k < s.K && col < s.out_size) ? ksk[(uint64_t)row * s.out_size + col] << sh : 0;
+      const u64 x = (k < s.K && col < s.out_size) ? (u64)ksk[(uint64_t)row * s.out_size + col] << sh : 0;
       b[j] = signed_byte(x, (int)t);
     }
     frag[idx] = pack16(b);
@@ -185,7 +189,16 @@ __device__ __forceinline__ i32x4 frag(const uint4* p) {
   return i32x4{(int)x.x, (int)x.y, (int)x.z, (int)x.w};
 }
 
-__global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, const u64* __restrict__ lwe_in,
+// native_closest_representable (decomposer.rs:25-49) of a u64 at one level of `bits` bits
+__device__ __forceinline__ u64 closest_representable(u64 x, uint32_t bits) {
+  const uint32_t shift = 64u - bits - 1u;
+  return (((x >> shift) + 1u) & ~(u64)1) << shift;
+}
+
+// OUT32: keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447): the body is the input body rounded
+// to the output modulus' 2^body_log and scaled down by 2^32, the sums wrap mod 2^32, and u32 words are stored
+template <bool OUT32>
+__global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_v, const u64* __restrict__ lwe_in,
                                                          const uint4* __restrict__ afrag,
                                                          const uint4* __restrict__ bfrag, uint32_t batch,
                                                          uint32_t n_mg, Shape s) {
@@ -316,10 +329,62 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(u64* __restrict__ out, 
         u64 v = 0;
 #pragma unroll
         for (int t = 0; t < 8; ++t) v += (u64)(int64_t)acc[m][c][t][r] << (8 * t);
-        const u64 base = is_body ? lwe_in[(uint64_t)row * (s.in_dim + 1) + s.in_dim] : 0;
-        out[(uint64_t)row * s.out_size + col] = base - v;
+        u64 base = is_body ? lwe_in[(uint64_t)row * (s.in_dim + 1) + s.in_dim] : 0;
+        if constexpr (OUT32) {
+          if (is_body) base = closest_representable(base, s.body_log) >> 32;
+          static_cast<uint32_t*>(out_v)[(uint64_t)row * s.out_size + col] = (uint32_t)(base - v);
+        } else {
+          static_cast<u64*>(out_v)[(uint64_t)row * s.out_size + col] = base - v;
+        }
       }
     }
+  }
+}
+
+// ---- the modulus switch of a u32 LWE (the KS32 bootstrap's input, mockups/tfhe-hpu-mockup/src/lib.rs:720-736) ----
+// modulus_switch (fft_impl/common.rs:10-23) at Scalar = u32
+__device__ __forceinline__ uint32_t ms32(uint32_t x, uint32_t log_mod) {
+  return log_mod >= 32 ? x : (uint32_t)(x + (1u << (32u - log_mod - 1u))) >> (32u - log_mod);
+}
+
+// One wave per ciphertext: the switched mask (LazyStandardModulusSwitchedLweCiphertext::mask,
+// modulus_switched_lwe_ciphertext.rs:164-172) and, when `centered`, the body correction of
+// lwe_ciphertext_centered_binary_modulus_switch (modulus_switch.rs:35-104) at Scalar = u32 / Signed = i32: the wrapping
+// u32 sum of the halved rounding errors and the exact sum of the halving errors are order-free, so the lanes' partial
+// sums combine by a butterfly reduction; then body = modulus_switch(b + correction) (:150-162).  out: (dim + 1) u64 per
+// ciphertext, every value in [0, 2^log_mod) (the blind rotation's MI_MS_PRE_SWITCHED input).
+__global__ __launch_bounds__(256) void lwe_ms32_kernel(u64* __restrict__ out, const uint32_t* __restrict__ in,
+                                                       uint32_t dim, uint32_t batch, uint32_t log_mod, int centered) {
+  const uint32_t lane = threadIdx.x & 63, item = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (item >= batch) return;
+  const uint32_t* x = in + (uint64_t)item * (dim + 1);
+  u64* y = out + (uint64_t)item * (dim + 1);
+  uint32_t sum_half = 0;
+  int32_t sum_hed = 0;
+  for (uint32_t i = lane; i < dim; i += 64) {
+    const uint32_t a = x[i], sw = ms32(a, log_mod);
+    y[i] = sw;
+    if (centered) {
+      const uint32_t round = log_mod >= 32 ? sw : sw << (32u - log_mod);
+      const int32_t err = (int32_t)(round - a), half = err / 2;  // i32 division truncates toward zero, as Rust's
+      sum_half += (uint32_t)half;
+      sum_hed += 2 * half - err;
+    }
+  }
+  if (centered) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      sum_half += (uint32_t)__shfl_xor((int)sum_half, off, 64);
+      sum_hed += __shfl_xor(sum_hed, off, 64);
+    }
+  }
+  if (lane == 0) {
+    uint32_t corr = 0;
+    if (centered) {
+      const uint32_t half_case = log_mod >= 32 ? 0u : 1u << (32u - log_mod - 1u);
+      corr = (sum_half - (uint32_t)(sum_hed / 2)) - half_case;
+    }
+    y[dim] = ms32(x[dim] + corr, log_mod);
   }
 }
 
@@ -337,6 +402,7 @@ static ks::Shape ks_shape(size_t in_dim, size_t out_dim, int base_log, int level
   s.K = (uint32_t)(in_dim * (size_t)level * s.nd);
   s.KB = (s.K + 63) / 64;
   s.CT = (s.out_size + 16 * ks::GN - 1) / (16 * ks::GN) * ks::GN;  // whole column groups
+  s.body_log = 64;
   return s;
 }
 
@@ -356,14 +422,34 @@ hipError_t launch_ksk_prepare(void* frag, const uint64_t* ksk, size_t in_dim, si
   const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
   const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;
   const unsigned grid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
-  hipLaunchKernelGGL(ks::ksk_prepare_kernel, dim3(grid), dim3(256), 0, st, (uint4*)frag, ksk, s);
+  hipLaunchKernelGGL(ks::ksk_prepare_kernel<uint64_t>, dim3(grid), dim3(256), 0, st, (uint4*)frag, ksk, s);
   return hipGetLastError();
 }
 
-hipError_t launch_keyswitch(uint64_t* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
-                            size_t in_dim, size_t out_dim, int base_log, int level, hipStream_t st) {
-  if (batch == 0) return hipSuccess;
+hipError_t launch_ksk32_prepare(void* frag, const uint32_t* ksk, size_t in_dim, size_t out_dim, int base_log,
+                                int level, hipStream_t st) {
   const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
+  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;
+  const unsigned grid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
+  hipLaunchKernelGGL(ks::ksk_prepare_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, (uint4*)frag, ksk, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_lwe_ms32(uint64_t* out, const uint32_t* in, size_t dim, size_t batch, int log_mod, bool centered,
+                           hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((batch + 3) / 4);
+  hipLaunchKernelGGL(ks::lwe_ms32_kernel, dim3(grid), dim3(256), 0, st, out, in, (uint32_t)dim, (uint32_t)batch,
+                     (uint32_t)log_mod, centered ? 1 : 0);
+  return hipGetLastError();
+}
+
+// out_log 0: the native u64 keyswitch into `out` (u64); else KS32 into u32 words with output modulus 2^out_log
+static hipError_t keyswitch_launch(void* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
+                                   size_t in_dim, size_t out_dim, int base_log, int level, int out_log, hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
+  if (out_log) s.body_log = (uint32_t)out_log;
   const uint32_t rows = (uint32_t)((batch + 16 * ks::GM - 1) / (16 * ks::GM) * 16 * ks::GM);
   const uint64_t total = (uint64_t)rows * s.KB * 4;
   const unsigned dgrid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
@@ -374,9 +460,23 @@ hipError_t launch_keyswitch(uint64_t* out, const uint64_t* lwe_in, const void* f
   const uint32_t n_mg = rows / (16 * ks::GM), n_cg = s.CT / ks::GN;
   const uint32_t tiles = (n_mg + 7) / 8 * 8 * n_cg;
   const unsigned grid = 8 * ((tiles + 7) / 8);
-  hipLaunchKernelGGL(ks::ks_gemm_kernel, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
-                     (const uint4*)frag, (uint32_t)batch, n_mg, s);
+  if (out_log)
+    hipLaunchKernelGGL(ks::ks_gemm_kernel<true>, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
+                       (const uint4*)frag, (uint32_t)batch, n_mg, s);
+  else
+    hipLaunchKernelGGL(ks::ks_gemm_kernel<false>, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
+                       (const uint4*)frag, (uint32_t)batch, n_mg, s);
   return hipGetLastError();
+}
+
+hipError_t launch_keyswitch(uint64_t* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
+                            size_t in_dim, size_t out_dim, int base_log, int level, hipStream_t st) {
+  return keyswitch_launch(out, lwe_in, frag, digits, batch, in_dim, out_dim, base_log, level, 0, st);
+}
+
+hipError_t launch_keyswitch32(uint32_t* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
+                              size_t in_dim, size_t out_dim, int base_log, int level, int out_log, hipStream_t st) {
+  return keyswitch_launch(out, lwe_in, frag, digits, batch, in_dim, out_dim, base_log, level, out_log, st);
 }
 
 }  // namespace mi

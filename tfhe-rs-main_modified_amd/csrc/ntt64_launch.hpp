@@ -140,16 +140,4 @@ hipError_t launch_pbs_tw(uint64_t* out, const uint64_t* lwe_in, const PbsIo& io,
                          size_t batch, int base_log, const uint64_t* tab, int centered, hipStream_t s);
 
 }  // namespace mi
-
-namespace mi {
-
-// keyswitch.hip — native-modulus LWE keyswitch on the int8 matrix cores.
-size_t ks_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level);
-int ks_digit_bytes_per_term(int base_log);  // signed bytes per decomposition digit
-size_t ks_digit_bytes(size_t in_dim, int base_log, int level, size_t batch);
-hipError_t launch_ksk_prepare(void* frag, const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level,
-                              hipStream_t s);
-hipError_t launch_keyswitch(uint64_t* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
-                            size_t in_dim, size_t out_dim, int base_log, int level, hipStream_t s);
-
-}  // namespace mi
+// (keyswitch.hip's entry points: keyswitch_launch.hpp)

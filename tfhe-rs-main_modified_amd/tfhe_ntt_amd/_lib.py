@@ -134,6 +134,12 @@ _SIGS = {
     "mi_lwe_ksk_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_int),
                                ctypes.POINTER(_int)]),
     "mi_lwe_keyswitch_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_lwe_ksk32_create": (_int, [_vp, _sz, _sz, _int, _int, _int, _int, _vp, ctypes.POINTER(_vp)]),
+    "mi_lwe_ksk32_destroy": (_int, [_vp]),
+    "mi_lwe_ksk32_info": (_int, [_vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz), ctypes.POINTER(_int),
+                                 ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "mi_lwe_keyswitch32_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "mi_lwe_modulus_switch32_batch": (_int, [_vp, _vp, _sz, _sz, _int, _int, _int, _vp]),
 }
 
 

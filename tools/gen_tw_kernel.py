@@ -508,7 +508,7 @@ def canon(sg, sl, x):
 # v_mad (4.6 instead of 8.9 cycles), a select one v_mov_b64 (4.2 instead of 8.6).  Every result is written in
 # place, so the butterflies also need no sum / difference temporaries.  The arithmetic is unchanged: same values,
 # lane by lane (the emulator tests and the GPU parity tests check it).
-EXEC_MASK = True
+EXEC_MASK = False  # measured slower on MI355X (r5, tools/variant_probe): see DESIGN.md §4
 
 
 def cond_exec(cond):
