@@ -136,7 +136,9 @@ class Seg:
                     if p is None or p.kind == "salu":
                         continue
                     if r[0] == "s" or r == "vcc":
-                        need = 2 if (op.kind == "salu" or r in op.mask_reads) else 3
+                        need = 2 if op.kind == "salu" else 3
+                        if r in op.mask_reads:  # a VALU-written carry mask read by the SALU that sets EXEC
+                            need = max(2, MASK_LATENCY)
                     elif op.kind == "dpp":
                         need = 3
                     else:
@@ -509,6 +511,7 @@ def canon(sg, sl, x):
 # place, so the butterflies also need no sum / difference temporaries.  The arithmetic is unchanged: same values,
 # lane by lane (the emulator tests and the GPU parity tests check it).
 EXEC_MASK = False  # measured slower on MI355X (r5, tools/variant_probe): see DESIGN.md §4
+MASK_LATENCY = 2   # list-scheduler slots between a VALU carry write and the SALU EXEC write that reads it
 
 
 def cond_exec(cond):
