@@ -157,7 +157,10 @@ static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_pla
         const u64 rho_inv = mi::host::exp_mod(rho, p - 2, p);
         u64 f = 1, b = 1;
         for (unsigned j = 0; j < 64; ++j) {
-          tf[64 * i + j] = f;
+          // the forward bodies' scale plan (ntt64_tw_tables.hpp, tools/tw_scale_plan.py): the five G1 stages leave
+          // block i scaled by 2^TW_G1_OUT_SCALE[i], the cyclic stages take element j scaled by 2^TW_CYC_IN_SCALE[j >> 1]
+          const int sc = (mi::tw::TW_CYC_IN_SCALE[0][j >> 1] - mi::tw::TW_G1_OUT_SCALE[0][i] + 192) % 192;
+          tf[64 * i + j] = sc ? mi::host::mul_mod(f, mi::host::exp_mod(2, (u64)sc, p), p) : f;
           ti[64 * i + j] = b;
           f = mi::host::mul_mod(f, rho, p);
           b = mi::host::mul_mod(b, rho_inv, p);

@@ -440,6 +440,42 @@ def gs(sg, sl, a, b, S, ac=False, bc=False):
     return False, True
 
 
+def scaled_ct(sg, sl, dmap, ra, rb, S, mode, scales, canon):
+    """CT butterfly on logical registers (ra, rb), twiddle 2^S, inputs carrying the scales (ea, eb) (register r holds
+    2^scales[r] times its value).  Mode 0: t = 2^(S + ea - eb) b, outputs a + t / a - t of scale ea.  Mode 1:
+    t = 2^(eb - S - ea) a, outputs t + b = 2^(eb - S) (a + 2^S b) to position ra and b - t = -2^(eb - S) (a - 2^S b)
+    to position rb (scale eb - S + 96), each into the register of its position (under EXEC_MASK the two logical
+    registers swap their physical ones instead)."""
+    ea, eb = scales[ra], scales[rb]
+    a, b = X(dmap, ra), X(dmap, rb)
+    if mode == 0:
+        m = (S + ea - eb) % 192
+        if m % 96 == 0 and canon[rb]:
+            ct_core(sg, sl, a, b, m >= 96, tsrc=(b[0], b[1]))
+        else:
+            ct(sg, sl, a, b, m)
+        scales[ra] = scales[rb] = ea % 192
+    elif EXEC_MASK:  # the masked primitives write the sum into their first operand: the logical registers swap
+        m = (eb - S - ea) % 192
+        if m % 96 == 0 and canon[ra]:
+            ct_core(sg, sl, b, a, m >= 96, tsrc=(a[0], a[1]))
+        else:
+            ct(sg, sl, b, a, m)
+        dmap[ra], dmap[rb] = dmap[rb], dmap[ra]
+    else:
+        # ct_core's neg flag exchanges which register receives the sum: with it flipped, b + t lands in a's register
+        # and b - t in b's, so the register map is unchanged (the PBS bodies' fixed MAC / inverse layout needs that)
+        m = (eb - S - ea) % 192
+        if m % 96 == 0 and canon[ra]:
+            ct_core(sg, sl, b, a, m < 96, tsrc=(a[0], a[1]))
+        else:
+            neg = tmul(sg, m, a[0], a[1], a[2], sl, sl.v[2], sl.v[3])
+            ct_core(sg, sl, b, a, not neg)
+        scales[ra] = (eb - S) % 192
+        scales[rb] = (eb - S + 96) % 192
+    canon[ra] = canon[rb] = False
+
+
 def gmul(sg, ms, x, wlo, whi, olo, ohi, zero_hi=True):
     """o = x * w canonical (x semi, w canonical), general 64x64 multiply (17 VALU; 15 with
     zero_hi=False, when the caller keeps the slot's Z1h / Z2h at 0 across a run of multiplies)."""
@@ -500,6 +536,25 @@ def canon(sg, sl, x):
     sg.add(f"v_mad_u64_u32 {P[0]}, {c[1]}, -1, 1, {xp}", [xp], [P[0], c[1]])
     sg.add(f"v_cndmask_b32_e64 {xlo}, {xlo}, {v[0]}, {c[1]}", [xlo, v[0], c[1]], [xlo])
     sg.add(f"v_cndmask_b32_e64 {xhi}, {xhi}, {v[1]}, {c[1]}", [xhi, v[1], c[1]], [xhi])
+
+
+# ------------------------------------------------------------------------------------------------
+# The scale plan (r5, tools/tw_scale_plan.py): the forward's in-register butterfly networks carry power-of-two scales
+# that the twist table absorbs, so each butterfly may multiply whichever input makes the cheaper shift class.  The
+# plan's table side (ntt64_tw_tables.hpp TW_G1_OUT_SCALE / TW_CYC_IN_SCALE) is generated from the same JSON.
+SCALE_PLAN = True
+_PLAN = None
+
+
+def scale_plan():
+    global _PLAN
+    if not SCALE_PLAN:
+        return None
+    if _PLAN is None:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import tw_scale_plan
+        _PLAN = tw_scale_plan.load()
+    return _PLAN
 
 
 # ------------------------------------------------------------------------------------------------
@@ -690,10 +745,14 @@ class Body:
             sl.append(Slot(b, SG0 + 6 * i))
         return sl
 
-    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None, by_reg=False, group_waits=None):
+    def stage(self, kind, dist, exps, dmap, free_blocks, canon=None, by_reg=False, group_waits=None, modes=None,
+              scales=None):
         """canon: list of 32 flags (logical registers known canonical), updated in place.  The twiddle
         exponent of the butterfly on registers (r, r + dist) is exps[r // (2 dist)] (one per group, the
-        natural-in CT / GS stages), or exps[r] with by_reg (one per position, the DIT stages)."""
+        natural-in CT / GS stages), or exps[r] with by_reg (one per position, the DIT stages).
+        modes / scales (CT only, the scale plan of tools/tw_scale_plan.py): scales[r] is the power-of-two exponent
+        logical register r carries (updated in place); butterfly k of the stage multiplies b (mode 0) or a (mode 1),
+        see scaled_ct."""
         sg = Seg()
         slots = self.slots(free_blocks)
         bf = 0
@@ -711,7 +770,9 @@ class Body:
             S = exps[r] if by_reg else exps[r // (2 * dist)]
             sl = slots[bf % len(slots)]
             a, b = X(dmap, r), X(dmap, r + dist)
-            if kind == "ct":
+            if kind == "ct" and modes is not None:
+                scaled_ct(sg, sl, dmap, r, r + dist, S, modes[bf], scales, canon)
+            elif kind == "ct":
                 if S % 96 == 0 and canon[r + dist]:
                     ct_core(sg, sl, a, b, S >= 96, tsrc=(b[0], b[1]))
                 else:
@@ -1227,11 +1288,17 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
     if prefetch:
         B.raw(*[ad.tw_load(0, k, 8 + 2 * k) for k in range(8)])
     fb = free_blocks_except(dmap, busy)
+    plan = scale_plan()
+    g1_scales = [0] * 32
     for s in range(first_stage, 5):  # first_stage 1: the caller ran stage 0 (the PBS bodies' signed digits)
         gw = None
         if s == 0 and PROGRESSIVE and prefetch:  # rows issued as pairs (k, k + 16), then the 8 twist-row loads
             gw = [f"s_waitcnt vmcnt({40 - 8 * (g + 1)})" for g in range(4)]
-        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb, group_waits=gw)
+        modes = plan["fwd_g1"]["modes"][16 * s:16 * s + 16] if plan else None
+        B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb, group_waits=gw, modes=modes,
+                scales=g1_scales if plan else None)
+    if plan:
+        assert g1_scales == [v % 192 for v in plan["fwd_g1"]["out_scales"]], "G1 scales differ from the plan's"
     if stop == "g1":
         return dmap
     # twist: 4 batches of 8 rows; table rows double-buffered in v8..v23 / v48..v63 (batch bt + 1
@@ -1254,8 +1321,12 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
         B.raw(*[ad.lw_load(r, k) for k, r in pre.items()])
     fb = free_blocks_except(dmap, busy)
     cf = [True] * 32  # twist outputs are canonical
+    cyc_scales = list(plan["fwd_cyc"]["in_scales"]) if plan else None
     for q in range(5):
-        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf)
+        B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf, modes=plan["fwd_cyc"]["modes"][16 * q:16 * q + 16]
+                if plan else None, scales=cyc_scales)
+    if plan:
+        assert all(v % 192 == 0 for v in cyc_scales), "the cyclic blocks' outputs must be unscaled"
     if stop == "cyc":
         return dmap
     pair_stage(B, dmap, True, ad, tabs, pre, busy)

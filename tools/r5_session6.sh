@@ -1,0 +1,7 @@
+#!/bin/bash
+# r5 GPU session 6: one-process A/B of the forward scale plan (tools/tw_scale_plan.py) against the library's bodies,
+# then the kernel-level breakdown of the multi-kernel NTT blind rotation at 3_3 and 4_4 (shape probe under rocprofv3)
+source tools/gpu_session_lib.sh
+step variant_probe_plan 240 ./tools/variant_probe || exit 1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+step shape_trace 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/shape_trace -o run -- python3 -u tools/shape_probe.py message_3_carry_3 message_4_carry_4 || exit 1
