@@ -196,3 +196,26 @@ def test_large_real_keys_message_4_carry_4(engine, oracle, bnf):
     else:
         want = ctx.pbs_batch_solinas(lwe2, lut.reshape(-1), nbsk.reshape(-1), k, base_log, level, threads=4)
     assert np.array_equal(host(out2), want)
+
+
+@pytest.mark.parametrize("k,level", [(2, 1), (1, 4), (2, 2)])
+@pytest.mark.parametrize("bnf", [True, False])
+def test_large_pbs_mac_fused_term_counts(engine, oracle, k, level, bnf):
+    """The MAC-fused inverse bodies (ntt64_tw.hip ntt_tw_inv_mac_kernel, r5) at the term counts l (k + 1) = 3, 8 and
+    6 with k = 2 (the shortint shapes run 4 and 6): random-key PBS at N = 16384 bit for bit vs the oracle."""
+    n, base_log, n_lwe, batch = 16384, 23 // level if level > 1 else 23, 2, 2
+    q = 0 if bnf else P
+    pl = engine.Plan.try_new(n, P)
+    c = oracle.NttContext(n)
+    M = engine.ntt64_pbs
+    g = H.rng(900 + 10 * k + level + bnf)
+    bsk = rand_q(g, (n_lwe, level, k + 1, k + 1, n), P)
+    lut = rand_q(g, (k + 1, n), q)
+    lwe = rand_q(g, (batch, n_lwe + 1), q)
+    want = np.stack([c.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), k, base_log, level, bnf=bnf)
+                     for b in range(batch)])
+    key = M.NttBootstrapKey(pl, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
+    o = dev(np.zeros((batch, k * n + 1), np.uint64))
+    (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf else
+     M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)(dev(lwe), o, dev(lut), key)
+    assert np.array_equal(host(o), want)

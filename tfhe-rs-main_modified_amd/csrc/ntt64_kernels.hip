@@ -357,7 +357,7 @@ static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int log
 
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,
                             const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first) {
-  if ((acc && fwd) || (skip_first && !fwd)) return hipErrorInvalidValue;  // acc: inverse only; skip_first: forward only
+  if (acc && fwd) return hipErrorInvalidValue;  // acc: inverse only
   const int t = logn - 11;
   if (t < 1 || t > 10) return hipErrorInvalidValue;
   if (batch == 0) return hipSuccess;
@@ -371,7 +371,7 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
   const int passes = (t + 4) / 5;
   int ks[2] = {(t + passes - 1) / passes, t - (t + passes - 1) / passes};
   auto tops = [&](u64* d, size_t nb) -> hipError_t {
-    for (int q = skip_first ? 1 : 0; q < passes; ++q) {
+    for (int q = skip_first && fwd ? 1 : 0; q < passes; ++q) {
       const int pi = fwd ? q : passes - 1 - q;
       const int s0 = pi == 0 ? 0 : ks[0], kk = ks[pi];
       const bool twist_here = fwd ? (pi == passes - 1) : (q == 0);
@@ -399,7 +399,7 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
     }
     return hipSuccess;
   };
-  hipError_t e = fwd ? all_tops() : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t);
+  hipError_t e = fwd ? all_tops() : (skip_first ? hipSuccess : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t));
   if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t) : all_tops();
   return e;
 }

@@ -31,6 +31,13 @@ hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys
                               hipStream_t s);
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
                          hipStream_t s, int sub_log = 0);
+// The MAC-fused inverse bodies of the large-N blind rotation (ntt64_tw.hip): for n_items ciphertexts, every 2048-block
+// of the k + 1 products y[b][c] = sum_{li, r} digits[b][li][r] . ggsw[li][r][c] (NTT domain, the step's GGSW with any
+// normalisation folded in) formed on load and run through the inverse body (the split inverse's first phase);
+// twist = the 2048 plan's inverse body table (SplitTw body_inv).  l (k + 1) in {2, 3, 4, 6, 8} (inv_mac_supported).
+bool inv_mac_supported(int level, int kp1);
+hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
+                                 int level, int logn, const uint64_t* twist, hipStream_t s);
 
 // The split transform of a Solinas plan with 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN = 2^20 (ntt64_kernels.hip; GPU parity:
 // tests/test_ntt_gpu.py test_fwd_inv_all_sizes_solinas 2^12 .. 2^18, test_fwd_inv_beyond_2_18 2^19 / 2^20 — the
@@ -47,6 +54,8 @@ struct SplitTw {
 // tw = the N plan's forward (fwd) or inverse (inv) twiddle table; data: batch polynomials `stride` u64 apart
 // acc (inverse only): the last top pass accumulates its output into acc (same layout as data) instead of storing it,
 // acc_mode 1 = BNF (acc += modswitch p -> 2^64), 2 = Solinas (acc = acc + x mod p); data then holds an intermediate
+// skip_first: the transform's first phase already ran — the forward's first top pass (fused into the blind rotation's
+// rotation + decomposition pass) or the inverse's 2048-block bodies (launch_ntt_tw_inv_mac)
 // the split transform of N = 2^(11 + t), t <= 3, as one launch (ntt64_tw.hip ntt_tw_fused_kernel): blk = the block
 // twist (SplitTw blk_fwd / blk_inv), body_tab = the 2048 body's table (body_fwd / body_inv)
 hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch, size_t stride, const uint64_t* blk,

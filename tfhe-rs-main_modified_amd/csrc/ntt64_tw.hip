@@ -171,6 +171,52 @@ __global__ __launch_bounds__(64) void ntt_tw_ms64_kernel(u64* dst, const u64* sr
                       [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r), [lwo] "v"(lwo));
 }
 
+
+// ---- the MAC-fused inverse bodies of the large-N blind rotation (pbs_large.hip, tools/gen_tw_kernel.py gen_inv_mac) ---
+// Unit u = 2048-block blk = u mod 2^sub_log of product polynomial pc = u >> sub_log, pc = b (k + 1) + c.  The body forms
+// the block of y_c = sum over the L = l (k + 1) terms q = li (k + 1) + r of digits[b][li][r] . GGSW[li][r][c] on load
+// (digit q at digits + b L N + q N, GGSW row q at ggsw + (q (k + 1) + c) N, both + blk 2048), runs the inverse body on
+// it and stores y (y + u 2048: the products' [b][c][N] layout).  Four waves per workgroup, as the inverse.
+template <int L>
+__global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
+                                                             const u64* __restrict__ ggsw, uint32_t units,
+                                                             uint32_t sub_log, uint32_t kp1,
+                                                             const u64* __restrict__ twist) {
+  constexpr uint32_t W = 4;
+  __shared__ u64 lds[W * WAVE_LDS2];
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t u = blockIdx.x * W + wv;
+  if (u >= units) return;
+  const uint32_t blk = u & ((1u << sub_log) - 1), pc = u >> sub_log, b = pc / kp1, c = pc % kp1;
+  const uint64_t n = (uint64_t)2048 << sub_log;
+  u64* p = y + (uint64_t)u * 2048;
+  const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
+  const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
+  const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
+  const uint32_t par = lane & 1, i = lane >> 1;
+  const uint32_t l8 = lane * 8;
+  const uint32_t lwo = par * 128;
+  const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
+  const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
+  const u64* lw = twist + 2 * (2048 + 32);  // the last-DIT-stage table (tw_body<false>)
+  const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
+  const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
+  const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
+  const uint32_t dlo = (uint32_t)(uintptr_t)d, dhi = (uint32_t)((uintptr_t)d >> 32);
+  const uint32_t gglo = (uint32_t)(uintptr_t)g, gghi = (uint32_t)((uintptr_t)g >> 32);
+  const uint32_t dstep = (uint32_t)(n * 8), gstep = (uint32_t)(kp1 * n * 8);
+#define MI_INV_MAC_OPS                                                                                             \
+  [g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t4w] "v"(t4w), \
+      [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo), [d_lo] "s"(dlo), [d_hi] "s"(dhi), [dstep] "s"(dstep),           \
+      [gg_lo] "s"(gglo), [gg_hi] "s"(gghi), [gstep] "s"(gstep)
+  if constexpr (L == 2) MI_TW_BODY_INV_MAC2(MI_INV_MAC_OPS);
+  else if constexpr (L == 3) MI_TW_BODY_INV_MAC3(MI_INV_MAC_OPS);
+  else if constexpr (L == 4) MI_TW_BODY_INV_MAC4(MI_INV_MAC_OPS);
+  else if constexpr (L == 6) MI_TW_BODY_INV_MAC6(MI_INV_MAC_OPS);
+  else MI_TW_BODY_INV_MAC8(MI_INV_MAC_OPS);
+#undef MI_INV_MAC_OPS
+}
+
 }  // namespace tw
 
 hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
@@ -214,6 +260,30 @@ hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch,
       case 2: fused_launch<2>(fwd, d, n, stride, blk, body_tab, s); break;
       default: fused_launch<3>(fwd, d, n, stride, blk, body_tab, s); break;
     }
+  }
+  return hipGetLastError();
+}
+
+bool inv_mac_supported(int level, int kp1) {
+  const int L = level * kp1;
+  return L == 2 || L == 3 || L == 4 || L == 6 || L == 8;
+}
+
+hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
+                                 int level, int logn, const uint64_t* twist, hipStream_t s) {
+  const int sub_log = logn - 11;
+  if (sub_log < 1 || !inv_mac_supported(level, kp1)) return hipErrorInvalidValue;
+  if (n_items == 0) return hipSuccess;
+  const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
+  if (units > 0x7fffffffull * 4) return hipErrorInvalidValue;  // one launch (the callers' chunks are far below)
+  const dim3 grid((unsigned)((units + 3) / 4)), block(256);
+  const uint32_t un = (uint32_t)units, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
+  switch (level * kp1) {
+    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
+    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
+    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
+    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
+    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
   }
   return hipGetLastError();
 }

@@ -594,6 +594,14 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 }  // namespace pbs
 
+static bool mac_fused_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("MI_PBS_MAC_FUSED");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // Lanes: a chunk of >= PBS_LANE_MIN ciphertexts is split into mi::pbs_lane_count() parts (default 2, >= 16 ciphertexts
 // each), the first on the caller's stream and the others on pooled side streams (mi::StreamFork), their launches
 // interleaved step by step.  Each ciphertext's blind rotation is independent, so the parts share nothing but the key,
@@ -617,6 +625,9 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   int k0 = 0;
   bool only = false;
   if (split) split_first_pass(logn, &k0, &only);
+  // r5: the MAC fused into the inverse's bodies (ntt64_tw.hip ntt_tw_inv_mac_kernel) where generated; 16-byte aligned
+  // key; MI_PBS_MAC_FUSED=0 in the environment keeps the separate MAC pass (A/B)
+  const bool mac_fused = split && inv_mac_supported(level, k + 1) && mac_fused_enabled();
   // one lane's share of a chunk: ciphertexts [b0, b0 + nb) of the batch, its scratch slices, its stream
   struct Lane {
     size_t b0;
@@ -654,7 +665,14 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
                            L.in, (uint32_t)n_lwe, i, nb, sh);
       e = ntt_large(true, logn, L.digits, (size_t)nb * level * (k + 1), sh.n, tw, split, L.st);
     }
-    if (e == hipSuccess) e = launch_large_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, sh, (u64)0, nullptr, 1u, L.st);
+    if (e != hipSuccess) return e;
+    if (mac_fused)  // the MAC formed on load by the inverse's 2048-block bodies, then the inverse's top passes
+      return (e = launch_ntt_tw_inv_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, k + 1, level, logn,
+                                         split->body_inv, L.st)) != hipSuccess
+                 ? e
+                 : launch_ntt_split(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, *split, L.st, L.acc,
+                                    bnf ? 1 : 2, true);
+    e = launch_large_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, sh, (u64)0, nullptr, 1u, L.st);
     if (e != hipSuccess) return e;
     if (split)  // the inverse's last pass accumulates into acc itself (launch_ntt_split acc_mode)
       return launch_ntt_split(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, *split, L.st, L.acc, bnf ? 1 : 2);

@@ -417,9 +417,10 @@ def body_lines(hdr, name, prefix="MI_TW_BODY_"):
     return [m.group(1) for m in re.finditer(r'"(.*?)\\n"', txt[start:end])]
 
 
-def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False):
+def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra=None, ops_extra=None):
     """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial.  out_of_place: the body
-    writes another buffer (%[o_lo] / %[o_hi], the key-conversion body), which is returned."""
+    writes another buffer (%[o_lo] / %[o_hi], the key-conversion body), which is returned.  mem_extra / ops_extra:
+    more memory regions (base address -> u64 array) and operand bindings (the MAC-fused inverse's term bases)."""
     data = np.array(poly, dtype=np.uint64).copy()
     tw = np.array(twist_tab, dtype=np.uint64)
     GB, TB, OB = 0x100000000, 0x200000000, 0x300000000
@@ -442,6 +443,10 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False):
     # an SGPR pair no body clobbers (the key-conversion body owns s94..s101)
     w.s[104], w.s[105] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
     ops["lw"] = "s[104:105]"
+    if mem_extra:
+        mem.update(mem_extra)
+    if ops_extra:
+        ops.update(ops_extra)
     w.ops = ops
     w.run(body_lines(hdr, name))
     return out if out_of_place else data

@@ -1682,8 +1682,136 @@ def gen_inv(tabs, stop=None):
     return B
 
 
-def emit(name, body, ops_in, sgpr_extra=()):
-    clob = ([f'"v{i}"' for i in range(VLO, VHI)] + [f'"s{i}"' for i in list(SGPR_CLOBBER) + list(sgpr_extra)] +
+# ---- the MAC-fused inverse of the large-N blind rotation (pbs_large.hip, r5) ------------------------------------------
+# One CMUX step at N > 2048 runs the forward on the (k + 1) l digit polynomials, the MAC with the step's GGSW, then the
+# inverse on the k + 1 products; with the split transform the inverse starts with the 2048-block bodies.  This body
+# forms its block of the product on load, y = sum_q d_q . G_q over the L = l (k + 1) digit / GGSW rows of the block
+# (update_with_fmadd, ntt64_pbs.rs:683-702 / ntt64_bnf_pbs.rs:707-726), then runs the standalone inverse on it and
+# stores y: the separate MAC pass (the product written and read back) disappears.
+# Each product term is 4 v_mad_u64_u32 into three 64-bit column accumulators (bits 0, 32, 64) whose carries are
+# counted (4 v_addc), one reduction per row at the end (as pbs_large.hip Acc128).  The term loads stream through a ring
+# of 4-VGPR buffers (digit pair, GGSW pair) issued MAC_RING terms ahead.
+S_MB = 64        # s[64 ..]: term base pairs, the digits' D_q then the GGSW's G_q (2 L pairs; L <= 8: up to s95)
+MAC_LS = (2, 3, 4, 6, 8)   # generated term counts: l (k + 1) for k = 1, l = 1..4 and k = 2, l = 1..2
+MAC_VHI = 128    # VGPR ceiling of the bodies (168: a longer ring at 3 waves per SIMD)
+
+
+def mac_ring(vhi):
+    """Ring buffer bases (4 VGPRs each: digit pair, GGSW pair) and the slot's base: v8..v63 (+ v128..vhi-1)."""
+    slot = 52
+    bufs = [8 + 4 * k for k in range(11)] + [128 + 4 * k for k in range((vhi - 128) // 4)]
+    return bufs, slot
+
+
+def mac_row(sg, L, bufs_of_terms, slot, out):
+    """Seg ops of one row: y = sum_q x_q w_q (x, w in the term buffers), reduced into the pair `out`, canonical."""
+    A0, A32, A64 = slot, slot + 2, slot + 4
+    n0, n32, n64 = f"v{slot + 6}", f"v{slot + 7}", f"v{slot + 8}"
+    c = [f"s[{36 + 2 * i}:{37 + 2 * i}]" for i in range(4)]
+    f = [f"s[{44 + 2 * i}:{45 + 2 * i}]" for i in range(10)]
+    v = lambda r: f"v{r}"
+    for q, X in enumerate(bufs_of_terms):
+        x0, x1, w0, w1 = v(X), v(X + 1), v(X + 2), v(X + 3)
+        if q == 0:
+            sg.add(f"v_mad_u64_u32 {pv(A0)}, {JUNK}, {x0}, {w0}, 0", [x0, w0], [pv(A0), JUNK])
+            sg.add(f"v_mad_u64_u32 {pv(A32)}, {JUNK}, {x0}, {w1}, 0", [x0, w1], [pv(A32), JUNK])
+            sg.add(f"v_mad_u64_u32 {pv(A64)}, {JUNK}, {x1}, {w1}, 0", [x1, w1], [pv(A64), JUNK])
+            sg.add(f"v_mad_u64_u32 {pv(A32)}, {c[2]}, {x1}, {w0}, {pv(A32)}", [x1, w0, pv(A32)], [pv(A32), c[2]])
+            sg.add(f"v_cndmask_b32_e64 {n32}, 0, 1, {c[2]}", [c[2]], [n32])
+            continue
+        first = q == 1  # n0 / n64 start from this term's carries
+        sg.add(f"v_mad_u64_u32 {pv(A0)}, {c[0]}, {x0}, {w0}, {pv(A0)}", [x0, w0, pv(A0)], [pv(A0), c[0]])
+        sg.add(f"v_mad_u64_u32 {pv(A32)}, {c[1]}, {x0}, {w1}, {pv(A32)}", [x0, w1, pv(A32)], [pv(A32), c[1]])
+        sg.add(f"v_mad_u64_u32 {pv(A64)}, {c[3]}, {x1}, {w1}, {pv(A64)}", [x1, w1, pv(A64)], [pv(A64), c[3]])
+        sg.add(f"v_mad_u64_u32 {pv(A32)}, {c[2]}, {x1}, {w0}, {pv(A32)}", [x1, w0, pv(A32)], [pv(A32), c[2]])
+        sg.add(f"v_addc_co_u32_e64 {n0}, {JUNK}, {0 if first else n0}, 0, {c[0]}", [c[0]] + ([] if first else [n0]),
+               [n0, JUNK])
+        sg.add(f"v_addc_co_u32_e64 {n32}, {JUNK}, {n32}, 0, {c[1]}", [n32, c[1]], [n32, JUNK])
+        sg.add(f"v_addc_co_u32_e64 {n64}, {JUNK}, {0 if first else n64}, 0, {c[3]}", [c[3]] + ([] if first else [n64]),
+               [n64, JUNK])
+        sg.add(f"v_addc_co_u32_e64 {n32}, {JUNK}, {n32}, 0, {c[2]}", [n32, c[2]], [n32, JUNK])
+    # S = A0 + A32 2^32 + (A64 + n0) 2^64 + n32 2^96 + n64 2^128 -> lo = A0 (64), hi = A64 (64), top = n64:
+    a0l, a0h, a32l, a32h, a64l, a64h = v(A0), v(A0 + 1), v(A32), v(A32 + 1), v(A64), v(A64 + 1)
+    sg.add(f"v_add_co_u32_e64 {a0h}, {f[0]}, {a0h}, {a32l}", [a0h, a32l], [a0h, f[0]])
+    sg.add(f"v_addc_co_u32_e64 {a64l}, {f[1]}, {a64l}, {a32h}, {f[0]}", [a64l, a32h, f[0]], [a64l, f[1]])
+    sg.add(f"v_addc_co_u32_e64 {a64h}, {f[2]}, {a64h}, {n32}, {f[1]}", [a64h, n32, f[1]], [a64h, f[2]])
+    sg.add(f"v_addc_co_u32_e64 {n64}, {JUNK}, {n64}, 0, {f[2]}", [n64, f[2]], [n64, JUNK])
+    sg.add(f"v_add_co_u32_e64 {a64l}, {f[3]}, {a64l}, {n0}", [a64l, n0], [a64l, f[3]])
+    sg.add(f"v_addc_co_u32_e64 {a64h}, {f[4]}, {a64h}, 0, {f[3]}", [a64h, f[3]], [a64h, f[4]])
+    sg.add(f"v_addc_co_u32_e64 {n64}, {JUNK}, {n64}, 0, {f[4]}", [n64, f[4]], [n64, JUNK])
+    # with hi = hh 2^32 + hl, 2^64 = EPS, 2^96 = -1, 2^128 = -2^32: S = lo - (top 2^32 + hh) + hl EPS.  D = lo - (top:hh)
+    # (into A32); a borrow adds 2^64 = EPS too many: D - EPS (top <= L + 1, so D >= 2^64 - 2^36 there: no wrap)
+    sg.add(f"v_sub_co_u32_e64 {a32l}, {f[5]}, {a0l}, {a64h}", [a0l, a64h], [a32l, f[5]])
+    sg.add(f"v_subb_co_u32_e64 {a32h}, {f[6]}, {a0h}, {n64}, {f[5]}", [a0h, n64, f[5]], [a32h, f[6]])
+    minus_eps(sg, n0, f[6], pv(A32))
+    # R = D + hl EPS (carry: R + 2^64 = R + EPS), U = R + EPS; canonical = (carry(R) | carry(U)) ? U : R
+    o = pv(out)
+    sg.add(f"v_mad_u64_u32 {o}, {f[7]}, {a64l}, -1, {pv(A32)}", [a64l, pv(A32)], [o, f[7]])
+    sg.add(f"v_mad_u64_u32 {pv(A0)}, {f[8]}, -1, 1, {o}", [o], [pv(A0), f[8]])
+    sg.add(f"s_or_b64 {f[9]}, {f[7]}, {f[8]}", [f[7], f[8]], [f[9]], kind="salu")
+    sg.add(f"v_cndmask_b32_e64 v{out}, v{out}, {a0l}, {f[9]}", [f"v{out}", a0l, f[9]], [f"v{out}"])
+    sg.add(f"v_cndmask_b32_e64 v{out + 1}, v{out + 1}, {a0h}, {f[9]}", [f"v{out + 1}", a0h, f[9]], [f"v{out + 1}"])
+
+
+def mac_phase(B, L, dmap, vhi=MAC_VHI):
+    """Rows 0..31 of y = sum_q d_q G_q into dmap (W0: lane j of row r = element 64 r + j of the block).  Term (r, q)
+    loads d_q row r from %[d] + q %[dstep] and G_q row r from %[gg] + q %[gstep] (bytes)."""
+    assert 2 <= L <= 8 and S_MB + 4 * L <= 96
+    bufs, slot = mac_ring(vhi)
+    ring = len(bufs)
+    dq = lambda q: S_MB + 2 * q
+    gq = lambda q: S_MB + 2 * L + 2 * q
+    sp = lambda b: f"s[{b}:{b + 1}]"
+    lines = [f"s_mov_b32 s{dq(0)}, %[d_lo]", f"s_mov_b32 s{dq(0) + 1}, %[d_hi]",
+             f"s_mov_b32 s{gq(0)}, %[gg_lo]", f"s_mov_b32 s{gq(0) + 1}, %[gg_hi]"]
+    for q in range(1, L):
+        lines += [f"s_add_u32 s{dq(q)}, s{dq(q - 1)}, %[dstep]", f"s_addc_u32 s{dq(q) + 1}, s{dq(q - 1) + 1}, 0",
+                  f"s_add_u32 s{gq(q)}, s{gq(q - 1)}, %[gstep]", f"s_addc_u32 s{gq(q) + 1}, s{gq(q - 1) + 1}, 0"]
+    B.raw(*lines)
+    total = 32 * L
+
+    def issue(t):
+        r, q = divmod(t, L)
+        out = []
+        if q == 0 and r % 8 == 0 and r:  # next row group: every term base 4096 bytes on
+            for b in [dq(i) for i in range(L)] + [gq(i) for i in range(L)]:
+                out += [f"s_add_u32 s{b}, s{b}, 0x1000", f"s_addc_u32 s{b + 1}, s{b + 1}, 0"]
+        X = bufs[t % ring]
+        off = 512 * (r % 8)
+        out += [f"global_load_dwordx2 {pv(X)}, %[l8], {sp(dq(q))} offset:{off}{LOAD_POLICY}",
+                f"global_load_dwordx2 {pv(X + 2)}, %[l8], {sp(gq(q))} offset:{off}{LOAD_POLICY}"]
+        return out
+
+    issued = min(ring, total)
+    B.raw(*[l for t in range(issued) for l in issue(t)])
+    for r in range(32):
+        last = r * L + L - 1
+        B.raw(f"s_waitcnt vmcnt({2 * (issued - last - 1)})")
+        sg = Seg()
+        mac_row(sg, L, [bufs[(r * L + q) % ring] for q in range(L)], slot, dmap[r])
+        for j, op in enumerate(sg.ops):
+            op.idx = j
+        B.out(sg.schedule())
+        nxt = min(issued + L, total)
+        B.raw(*[l for t in range(issued, nxt) for l in issue(t)])
+        issued = nxt
+
+
+def gen_inv_mac(tabs, L, vhi=MAC_VHI):
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
+    mac_phase(B, L, dmap, vhi)
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    assert INV_W1PP
+    dmap = inv_core(B, tabs, dmap, w1pp=True)
+    B.raw(*store_rows(dmap, S_GB))
+    return B
+
+
+def emit(name, body, ops_in, sgpr_extra=(), vhi=None):
+    clob = ([f'"v{i}"' for i in range(VLO, vhi or VHI)] + [f'"s{i}"' for i in list(SGPR_CLOBBER) + list(sgpr_extra)] +
             ['"scc"', '"memory"'] + (['"vcc"'] if REGROUP_DPP_SELECT else []))
     text = "\n".join(f'      "{l}\\n"' for l in body.lines)
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
@@ -1701,6 +1829,8 @@ def main():
     print(emit("fwd", f, None))
     print(emit("inv", i, None))
     print(emit("fwd_ms64", gen_fwd_ms64(tabs), None, MS_SGPRS))
+    for L in MAC_LS:
+        print(emit(f"inv_mac{L}", gen_inv_mac(tabs, L), None, range(94, max(94, S_MB + 4 * L)), MAC_VHI))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 
