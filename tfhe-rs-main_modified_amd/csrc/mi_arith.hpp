@@ -54,6 +54,20 @@ struct Goldilocks {
     const u64 d = a - b;
     return (a < b) ? d - GL_EPS : d;
   }
+  // Lazy forms (r5) for butterfly chains whose values need only be congruent mod p (any 64-bit value) until a final
+  // multiply or canonicalisation: a + t for a canonical t and any a (a carry folds as + EPS and cannot carry again:
+  // a + t - 2^64 < a - EPS + 1), a - t for a canonical t (a borrow subtracts EPS: a - t + 2^64 > EPS, no wrap)
+  __device__ __forceinline__ static u64 add_lazy(u64 a, u64 t) {
+    unsigned long long c;
+    const u64 s = __builtin_addcll(a, t, 0ull, &c);  // the add's own carry (not a 64-bit compare)
+    return s + (c ? GL_EPS : 0);
+  }
+  __device__ __forceinline__ static u64 sub_lazy(u64 a, u64 t) {
+    unsigned long long b;
+    const u64 d = __builtin_subcll(a, t, 0ull, &b);
+    return d - (b ? GL_EPS : 0);
+  }
+  __device__ __forceinline__ static u64 canon(u64 x) { return x >= P ? x - P : x; }
   // (hi:lo) mod p for any 128-bit value: hi = hh*2^32 + hl, 2^96 = -1, 2^64 = 2^32 - 1.
   __device__ __forceinline__ static u64 reduce128(u64 lo, u64 hi) {
     const u32 hh = hi32(hi), hl = lo32(hi);

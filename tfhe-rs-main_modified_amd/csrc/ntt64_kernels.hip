@@ -181,7 +181,7 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::b(W, k) * cols + col;
-      poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : x[k];
+      poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : Goldilocks::canon(x[k]);  // lazy stages
     }
   } else {
 #pragma unroll

@@ -7,6 +7,8 @@
 //   phase A: lane (wave w, column c) holds rows w + 4 k: the stages whose butterflies are >= 4 rows apart
 //            (s <= K - 3) pair registers k and k + d / 4 of the same lane;
 //   phase B: rows 2^(K-2) w + k: the last two stages (2 and 1 rows apart) pair registers k, k + d.
+// Forward stages are lazy (Goldilocks::add_lazy / sub_lazy: any 64-bit representative, r5): the callers multiply by
+// the block twist (canonical product) or canonicalise before storing.
 // The forward runs A, LDS transpose (16 KiB: rows x 64 columns, a wave writes / reads whole 512-B rows: conflict-free),
 // B; the inverse B, transpose, A.  Every twiddle of stages 0 .. 4 is a power of two by the Solinas tower
 // (tower_exp, Goldilocks::mul_pow2), compile-time in each register because the wave index is a template parameter
@@ -38,11 +40,11 @@ __device__ __forceinline__ void stage(u64 (&x)[Rows<K>::RPT]) {
     const int row = PB ? Rows<K>::b(W, k) : Rows<K>::a(W, k);
     const int ex = tower_exp(FWD, S, row >> (K - S));
     bool ng;
-    if (FWD) {
+    if (FWD) {  // lazy: outputs congruent mod p, any 64-bit value (z canonical; the callers canonicalise or multiply)
       const u64 z = Goldilocks::mul_pow2(x[k + dk], ex, ng);
       const u64 u = x[k];
-      x[k] = ng ? Goldilocks::sub(u, z) : Goldilocks::add(u, z);
-      x[k + dk] = ng ? Goldilocks::add(u, z) : Goldilocks::sub(u, z);
+      x[k] = ng ? Goldilocks::sub_lazy(u, z) : Goldilocks::add_lazy(u, z);
+      x[k + dk] = ng ? Goldilocks::add_lazy(u, z) : Goldilocks::sub_lazy(u, z);
     } else {  // (a - b) w = (b - a) |w| for a negative w
       const u64 u = x[k], v = x[k + dk];
       x[k] = Goldilocks::add(u, v);

@@ -173,23 +173,26 @@ __global__ __launch_bounds__(64) void ntt_tw_ms64_kernel(u64* dst, const u64* sr
 
 
 // ---- the MAC-fused inverse bodies of the large-N blind rotation (pbs_large.hip, tools/gen_tw_kernel.py gen_inv_mac) ---
-// Unit u = 2048-block blk = u mod 2^sub_log of product polynomial pc = u >> sub_log, pc = b (k + 1) + c.  The body forms
-// the block of y_c = sum over the L = l (k + 1) terms q = li (k + 1) + r of digits[b][li][r] . GGSW[li][r][c] on load
-// (digit q at digits + b L N + q N, GGSW row q at ggsw + (q (k + 1) + c) N, both + blk 2048), runs the inverse body on
-// it and stores y (y + u 2048: the products' [b][c][N] layout).  Four waves per workgroup, as the inverse.
+// Unit u = (blk n_items + b) (k + 1) + c: output column c of item b, 2048-block blk.  The body forms the block of
+// y_c = sum over the L = l (k + 1) terms q = li (k + 1) + r of digits[b][li][r] . GGSW[li][r][c] on load (digit q at
+// digits + b L N + q N, GGSW row q at ggsw + (q (k + 1) + c) N, both + blk 2048), runs the inverse body on it and
+// stores y (the products' [b][c][N] layout).  Four waves per workgroup, as the inverse.  The unit order puts the k + 1
+// columns of one (item, block) in adjacent waves of a workgroup (the second reads the item's digit rows from L1 / L2,
+// not HBM: each digit row is read from HBM once, as large_mac_cols does) and walks the items of one block before the
+// next block (the step's GGSW rows of a block stay L2-resident across the items).
 template <int L>
 __global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
                                                              const u64* __restrict__ ggsw, uint32_t units,
-                                                             uint32_t sub_log, uint32_t kp1,
+                                                             uint32_t n_items, uint32_t sub_log, uint32_t kp1,
                                                              const u64* __restrict__ twist) {
   constexpr uint32_t W = 4;
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t u = blockIdx.x * W + wv;
   if (u >= units) return;
-  const uint32_t blk = u & ((1u << sub_log) - 1), pc = u >> sub_log, b = pc / kp1, c = pc % kp1;
+  const uint32_t c = u % kp1, ib = u / kp1, b = ib % n_items, blk = ib / n_items;
   const uint64_t n = (uint64_t)2048 << sub_log;
-  u64* p = y + (uint64_t)u * 2048;
+  u64* p = y + ((uint64_t)b * kp1 + c) * n + (uint64_t)blk * 2048;
   const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
   const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
@@ -277,13 +280,13 @@ hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint
   const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
   if (units > 0x7fffffffull * 4) return hipErrorInvalidValue;  // one launch (the callers' chunks are far below)
   const dim3 grid((unsigned)((units + 3) / 4)), block(256);
-  const uint32_t un = (uint32_t)units, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
+  const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
   switch (level * kp1) {
-    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
-    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
-    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
-    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
-    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, sl, kp, twist); break;
+    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
   }
   return hipGetLastError();
 }

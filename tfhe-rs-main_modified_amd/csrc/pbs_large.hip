@@ -243,7 +243,7 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
       const uint64_t e = Rw::b(W, k) * cols + col;
       // the digits are read once, by the next pass: non-temporal
       if constexpr (ONLY) __builtin_nontemporal_store(Goldilocks::mul(x[k], tv[k]), o + e);
-      else __builtin_nontemporal_store(x[k], o + e);
+      else __builtin_nontemporal_store(Goldilocks::canon(x[k]), o + e);  // the lazy tile stages
     }
   }
 }
