@@ -356,7 +356,8 @@ static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int log
 }
 
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,
-                            const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first) {
+                            const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first,
+                            size_t wave_cap) {
   if (acc && fwd) return hipErrorInvalidValue;  // acc: inverse only
   const int t = logn - 11;
   if (t < 1 || t > 10) return hipErrorInvalidValue;
@@ -399,8 +400,9 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
     }
     return hipSuccess;
   };
-  hipError_t e = fwd ? all_tops() : (skip_first ? hipSuccess : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t));
-  if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t) : all_tops();
+  hipError_t e = fwd ? all_tops()
+                     : (skip_first ? hipSuccess : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t, wave_cap));
+  if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t, wave_cap) : all_tops();
   return e;
 }
 

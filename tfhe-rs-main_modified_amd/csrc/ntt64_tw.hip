@@ -51,7 +51,9 @@ constexpr uint32_t tw_waves() { return FWD ? 1u : 4u; }
 
 // sub_log > 0 (the split transform of N = 2^(11 + sub_log), ntt64_kernels.hip launch_ntt_split): unit `poly` is block
 // poly & (2^sub_log - 1) of polynomial poly >> sub_log, 2048 contiguous coefficients at that block's offset
-template <bool FWD>
+// PERSIST (the blind rotation's capped launches, r5): the grid holds fewer waves than units and each wave loops over
+// units poly, poly + grid waves, ... (launch_ntt_tw wave_cap)
+template <bool FWD, bool PERSIST = false>
 __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* __restrict__ data, uint32_t batch,
                                                                           uint64_t stride,
                                                                           const u64* __restrict__ twist,
@@ -60,10 +62,14 @@ __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* 
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t poly = blockIdx.x * W + wv;
-  if (poly >= batch) return;
-  u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
-  tw_body<FWD>(p, twist, (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2), lane);
+  for (uint32_t poly = blockIdx.x * W + wv; poly < batch; poly += gridDim.x * W) {
+    u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
+    tw_body<FWD>(p, twist, (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2), lane);
+    if constexpr (!PERSIST) break;
+    // the body's stores drain before the next unit: its own vmcnt waits count only the loads it issues (loads and
+    // stores share vmcnt here and need not complete in order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 // ---- the split transform of N = 2^(11 + T), T <= 3, in one launch ------------------------------------------------
@@ -181,21 +187,16 @@ __global__ __launch_bounds__(64) void ntt_tw_ms64_kernel(u64* dst, const u64* sr
 // not HBM: each digit row is read from HBM once, as large_mac_cols does) and walks the items of one block before the
 // next block (the step's GGSW rows of a block stay L2-resident across the items).
 template <int L>
-__global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
-                                                             const u64* __restrict__ ggsw, uint32_t units,
-                                                             uint32_t n_items, uint32_t sub_log, uint32_t kp1,
-                                                             const u64* __restrict__ twist) {
-  constexpr uint32_t W = 4;
-  __shared__ u64 lds[W * WAVE_LDS2];
-  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t u = blockIdx.x * W + wv;
-  if (u >= units) return;
+__device__ __forceinline__ void inv_mac_unit(u64* __restrict__ y, const u64* __restrict__ digits,
+                                             const u64* __restrict__ ggsw, uint32_t u, uint32_t n_items,
+                                             uint32_t sub_log, uint32_t kp1, const u64* __restrict__ twist, u64* wl,
+                                             uint32_t lane) {
   const uint32_t c = u % kp1, ib = u / kp1, b = ib % n_items, blk = ib / n_items;
   const uint64_t n = (uint64_t)2048 << sub_log;
   u64* p = y + ((uint64_t)b * kp1 + c) * n + (uint64_t)blk * 2048;
   const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
   const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
-  const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
+  const uint32_t S = (uint32_t)(uintptr_t)wl;
   const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
   const uint32_t lwo = par * 128;
@@ -218,6 +219,20 @@ __global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y
   else if constexpr (L == 6) MI_TW_BODY_INV_MAC6(MI_INV_MAC_OPS);
   else MI_TW_BODY_INV_MAC8(MI_INV_MAC_OPS);
 #undef MI_INV_MAC_OPS
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
+                                                             const u64* __restrict__ ggsw, uint32_t units,
+                                                             uint32_t n_items, uint32_t sub_log, uint32_t kp1,
+                                                             const u64* __restrict__ twist) {
+  constexpr uint32_t W = 4;
+  __shared__ u64 lds[W * WAVE_LDS2];
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t u = blockIdx.x * W + wv; u < units; u += gridDim.x * W) {
+    inv_mac_unit<L>(y, digits, ggsw, u, n_items, sub_log, kp1, twist, lds + wv * WAVE_LDS2, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as ntt_tw_body_kernel<PERSIST>
+  }
 }
 
 }  // namespace tw
@@ -273,13 +288,14 @@ bool inv_mac_supported(int level, int kp1) {
 }
 
 hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
-                                 int level, int logn, const uint64_t* twist, hipStream_t s) {
+                                 int level, int logn, const uint64_t* twist, hipStream_t s, size_t wave_cap) {
   const int sub_log = logn - 11;
   if (sub_log < 1 || !inv_mac_supported(level, kp1)) return hipErrorInvalidValue;
   if (n_items == 0) return hipSuccess;
   const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
   if (units > 0x7fffffffull * 4) return hipErrorInvalidValue;  // one launch (the callers' chunks are far below)
-  const dim3 grid((unsigned)((units + 3) / 4)), block(256);
+  const uint64_t wgs = (units + 3) / 4, cap = wave_cap ? std::max<uint64_t>(1, wave_cap / 4) : wgs;
+  const dim3 grid((unsigned)std::min(wgs, cap)), block(256);
   const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
   switch (level * kp1) {
     case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
@@ -292,8 +308,23 @@ hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint
 }
 
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist, hipStream_t s,
-                         int sub_log) {
+                         int sub_log, size_t wave_cap) {
   if (batch == 0) return hipSuccess;
+  if (wave_cap && sub_log > 0 && (batch << sub_log) <= 0xffffffffull) {  // one capped, looping launch
+    const uint32_t n = (uint32_t)(batch << sub_log);
+    if (fwd) {
+      constexpr uint32_t W = tw::tw_waves<true>();
+      const uint32_t g = (uint32_t)std::min<size_t>((n + W - 1) / W, std::max<size_t>(1, wave_cap / W));
+      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<true, true>), dim3(g), dim3(64 * W), 0, s, data, n, (uint64_t)stride,
+                         twist, (uint32_t)sub_log);
+    } else {
+      constexpr uint32_t W = tw::tw_waves<false>();
+      const uint32_t g = (uint32_t)std::min<size_t>((n + W - 1) / W, std::max<size_t>(1, wave_cap / W));
+      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<false, true>), dim3(g), dim3(64 * W), 0, s, data, n,
+                         (uint64_t)stride, twist, (uint32_t)sub_log);
+    }
+    return hipGetLastError();
+  }
   // grid.x limit 2^31 - 1 (a whole chunk is 16 TiB of polynomials); a chunk of units holds whole polynomials
   const size_t CHUNK = (size_t(1) << 30) >> sub_log << sub_log;
   const size_t units = batch << sub_log;

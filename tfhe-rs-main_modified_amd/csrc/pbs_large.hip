@@ -594,6 +594,21 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 }  // namespace pbs
 
+static int pbs_wave_cap() {
+  static const int v = [] {
+    const char* e = getenv("MI_PBS_WAVE_CAP");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  return v;
+}
+
+static size_t device_simds(hipStream_t s) {
+  int dev = 0, cus = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  return (size_t)cus * 4;
+}
+
 static bool mac_fused_enabled() {
   static const bool on = [] {
     const char* v = getenv("MI_PBS_MAC_FUSED");
@@ -628,6 +643,10 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   // r5: the MAC fused into the inverse's bodies (ntt64_tw.hip ntt_tw_inv_mac_kernel) where generated; 16-byte aligned
   // key; MI_PBS_MAC_FUSED=0 in the environment keeps the separate MAC pass (A/B)
   const bool mac_fused = split && inv_mac_supported(level, k + 1) && mac_fused_enabled();
+  // MI_PBS_WAVE_CAP=<waves per SIMD> (r5 A/B): the step's body launches hold at most that many waves per SIMD of the
+  // device and loop over their units, so two lanes' launches can share every CU (one's memory phase beside the
+  // other's issue-bound bodies) instead of filling the device one after the other; 0 / unset: full grids
+  const size_t wave_cap = (size_t)pbs_wave_cap() * (size_t)device_simds(s);
   // one lane's share of a chunk: ciphertexts [b0, b0 + nb) of the batch, its scratch slices, its stream
   struct Lane {
     size_t b0;
@@ -655,7 +674,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
               : rotdec_top<false>(k0, only, L.digits, L.acc, L.in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, L.st);
       if (e == hipSuccess)
         e = launch_ntt_split(true, logn, L.digits, (size_t)nb * level * (k + 1), sh.n, tw, *split, L.st, nullptr, 0,
-                             true);
+                             true, wave_cap);
     } else {
       if (bnf)
         hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.digits, L.acc,
@@ -668,7 +687,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
     if (e != hipSuccess) return e;
     if (mac_fused)  // the MAC formed on load by the inverse's 2048-block bodies, then the inverse's top passes
       return (e = launch_ntt_tw_inv_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, k + 1, level, logn,
-                                         split->body_inv, L.st)) != hipSuccess
+                                         split->body_inv, L.st, wave_cap)) != hipSuccess
                  ? e
                  : launch_ntt_split(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, *split, L.st, L.acc,
                                     bnf ? 1 : 2, true);
