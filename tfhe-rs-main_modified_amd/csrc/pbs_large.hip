@@ -31,6 +31,7 @@
 #include "mi_arith.hpp"
 #include "ntt64_launch.hpp"
 #include "ntt64_tile.hpp"
+#include "ntt64_tile_asm.hpp"
 #include "pbs_device.hpp"
 
 namespace mi {
@@ -167,6 +168,18 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       if (!BNF && sg[r]) term = (u64)0 - term;
       x[r] = ((int64_t)term < 0) ? term + P : term;
     }
+    if constexpr (K == 2 && ONLY) {  // r5: the stages and the block twist as generated asm (tools/gen_tile_asm.py)
+      const u64* tws = twist;
+      asm volatile("" : "+s"(tws));
+      u64 tw[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) tw[r] = tws[j + r * cols];
+      tile_asm::k2_fwd_tw(x, tw);
+      u64* o = dp + (uint64_t)li * per;
+#pragma unroll
+      for (int r = 0; r < R; ++r) __builtin_nontemporal_store(x[r], o + r * cols);
+      continue;
+    }
 #pragma unroll
     for (int s = 0; s < K; ++s) {  // stage s: m = 2^s groups, pair distance 2^(K-1-s) in r; twiddle tw[m + g] = 2^e
       const int d = 1 << (K - 1 - s);
@@ -192,6 +205,22 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       __builtin_nontemporal_store(v, o + r * cols);  // the digits are read once, by the next pass
     }
   }
+}
+
+// the generated K = 5 blocks by wave index (tools/gen_tile_asm.py -> ntt64_tile_asm.hpp)
+template <int W>
+__device__ __forceinline__ void tile5_fwd_a(u64 (&x)[8]) {
+  if constexpr (W == 0) tile_asm::k5_fwd_a_w0(x);
+  else if constexpr (W == 1) tile_asm::k5_fwd_a_w1(x);
+  else if constexpr (W == 2) tile_asm::k5_fwd_a_w2(x);
+  else tile_asm::k5_fwd_a_w3(x);
+}
+template <int W>
+__device__ __forceinline__ void tile5_fwd_b_tw(u64 (&x)[8], const u64 (&tw)[8]) {
+  if constexpr (W == 0) tile_asm::k5_fwd_b_tw_w0(x, tw);
+  else if constexpr (W == 1) tile_asm::k5_fwd_b_tw_w1(x, tw);
+  else if constexpr (W == 2) tile_asm::k5_fwd_b_tw_w2(x, tw);
+  else tile_asm::k5_fwd_b_tw_w3(x, tw);
 }
 
 // The same step at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): lane (wave W, column c) forms ct1 and the
@@ -234,10 +263,18 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
       if (!BNF && sg[k]) term = (u64)0 - term;
       x[k] = ((int64_t)term < 0) ? term + P : term;
     }
+    u64* o = dp + (uint64_t)li * per;
+    if constexpr (K == 5 && ONLY) {  // r5: phase A, phase B and the block twist as generated asm (gen_tile_asm.py)
+      tile5_fwd_a<W>(x);
+      tile::exchange<K, W, true>(x, lds, c);
+      tile5_fwd_b_tw<W>(x, tv);
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) __builtin_nontemporal_store(x[k], o + Rw::b(W, k) * cols + col);
+      continue;
+    }
     tile::phase_a<K, true, W>(x);
     tile::exchange<K, W, true>(x, lds, c);
     tile::phase_b<K, true, W>(x);
-    u64* o = dp + (uint64_t)li * per;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::b(W, k) * cols + col;
