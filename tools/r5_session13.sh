@@ -15,7 +15,7 @@ tail -1 gpurun_out/bench_driver_cmd.txt > $O/bench_line_driver_cmd.json
 step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 -u bench.py --steps 3000 || exit 1
-tail -1 gpurun_out/trace.txt > $O/bench_line_under_rocprof.json
+grep "\"metric\"" gpurun_out/trace.txt | tail -1 > $O/bench_line_under_rocprof.json
 python3 tools/summarize_rocpd.py $O/trace/run_kernel_trace.csv $O/trace_sum $O/bench_line_under_rocprof.json > $O/trace_sum.txt 2>&1
 rm -f $O/trace/run_kernel_trace.csv
 P="--output-format csv -o run -- tools/headline_loop 20"
