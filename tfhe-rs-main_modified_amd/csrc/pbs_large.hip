@@ -160,6 +160,13 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       st[r] = closest_abs_nonnative(sg[r] ? P - x : x, sh.base_log, (int)sh.level) >> shift;
     }
   }
+  // K = 2 (ONLY): the 4 block-twist values of the lane's rows, loaded once for every level (8 VGPRs; the asm block
+  // needs them in registers before it starts, so a per-level load would expose its latency at every level)
+  u64 tw2[K == 2 ? R : 1];
+  if constexpr (K == 2 && ONLY) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) tw2[r] = twist[j + r * cols];
+  }
   for (uint32_t li = 0; li < sh.level; ++li) {
     u64 x[R];
 #pragma unroll
@@ -169,12 +176,7 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       x[r] = ((int64_t)term < 0) ? term + P : term;
     }
     if constexpr (K == 2 && ONLY) {  // r5: the stages and the block twist as generated asm (tools/gen_tile_asm.py)
-      const u64* tws = twist;
-      asm volatile("" : "+s"(tws));
-      u64 tw[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) tw[r] = tws[j + r * cols];
-      tile_asm::k2_fwd_tw(x, tw);
+      tile_asm::k2_fwd_tw(x, tw2);
       u64* o = dp + (uint64_t)li * per;
 #pragma unroll
       for (int r = 0; r < R; ++r) __builtin_nontemporal_store(x[r], o + r * cols);
