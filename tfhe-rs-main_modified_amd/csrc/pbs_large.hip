@@ -160,13 +160,6 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       st[r] = closest_abs_nonnative(sg[r] ? P - x : x, sh.base_log, (int)sh.level) >> shift;
     }
   }
-  // K = 2 (ONLY): the 4 block-twist values of the lane's rows, loaded once for every level (8 VGPRs; the asm block
-  // needs them in registers before it starts, so a per-level load would expose its latency at every level)
-  u64 tw2[K == 2 ? R : 1];
-  if constexpr (K == 2 && ONLY) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) tw2[r] = twist[j + r * cols];
-  }
   for (uint32_t li = 0; li < sh.level; ++li) {
     u64 x[R];
 #pragma unroll
@@ -174,13 +167,6 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       u64 term = decompose_one_level(sh.base_log, st[r]);
       if (!BNF && sg[r]) term = (u64)0 - term;
       x[r] = ((int64_t)term < 0) ? term + P : term;
-    }
-    if constexpr (K == 2 && ONLY) {  // r5: the stages and the block twist as generated asm (tools/gen_tile_asm.py)
-      tile_asm::k2_fwd_tw(x, tw2);
-      u64* o = dp + (uint64_t)li * per;
-#pragma unroll
-      for (int r = 0; r < R; ++r) __builtin_nontemporal_store(x[r], o + r * cols);
-      continue;
     }
 #pragma unroll
     for (int s = 0; s < K; ++s) {  // stage s: m = 2^s groups, pair distance 2^(K-1-s) in r; twiddle tw[m + g] = 2^e
