@@ -24,6 +24,7 @@
 #include "ntt64_launch.hpp"
 #include "ntt64_regs.hpp"
 #include "ntt64_tile.hpp"
+#include "ntt64_tile_asm.hpp"
 #include "pbs_device.hpp"
 
 namespace mi {
@@ -164,6 +165,22 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
   for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
 }
 
+// the generated inverse K = 5 blocks by wave index (tools/gen_tile_asm.py -> ntt64_tile_asm.hpp)
+template <int W>
+__device__ __forceinline__ void tile5_inv_tw_b(u64 (&x)[8], const u64 (&tw)[8]) {
+  if constexpr (W == 0) tile_asm::k5_inv_tw_b_w0(x, tw);
+  else if constexpr (W == 1) tile_asm::k5_inv_tw_b_w1(x, tw);
+  else if constexpr (W == 2) tile_asm::k5_inv_tw_b_w2(x, tw);
+  else tile_asm::k5_inv_tw_b_w3(x, tw);
+}
+template <int W>
+__device__ __forceinline__ void tile5_inv_a(u64 (&x)[8]) {
+  if constexpr (W == 0) tile_asm::k5_inv_a_w0(x);
+  else if constexpr (W == 1) tile_asm::k5_inv_a_w1(x);
+  else if constexpr (W == 2) tile_asm::k5_inv_a_w2(x);
+  else tile_asm::k5_inv_a_w3(x);
+}
+
 // The stage-0 pass of the split transform at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): the same function as
 // ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true> at s0 = 0.  Grid: x = column tiles of 64, y = polynomials.
 template <int K, bool FWD, int TWIST, int ACC, int W>
@@ -184,14 +201,27 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
       poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : Goldilocks::canon(x[k]);  // lazy stages
     }
   } else {
+    if constexpr (K == 5 && TWIST == 2) {  // r5: untwist + stages as generated asm (tools/gen_tile_asm.py)
+      u64 tw[RPT];
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const uint64_t e = Rw::b(W, k) * cols + col;
-      x[k] = TWIST == 2 ? Goldilocks::mul(poly[e], twist[e]) : poly[e];
+      for (int k = 0; k < RPT; ++k) {
+        const uint64_t e = Rw::b(W, k) * cols + col;
+        x[k] = poly[e];
+        tw[k] = twist[e];
+      }
+      tile5_inv_tw_b<W>(x, tw);
+      tile::exchange<K, W, false>(x, lds, c);
+      tile5_inv_a<W>(x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const uint64_t e = Rw::b(W, k) * cols + col;
+        x[k] = TWIST == 2 ? Goldilocks::mul(poly[e], twist[e]) : poly[e];
+      }
+      tile::phase_b<K, false, W>(x);
+      tile::exchange<K, W, false>(x, lds, c);
+      tile::phase_a<K, false, W>(x);
     }
-    tile::phase_b<K, false, W>(x);
-    tile::exchange<K, W, false>(x, lds, c);
-    tile::phase_a<K, false, W>(x);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::a(W, k) * cols + col;

@@ -220,22 +220,10 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
 
 // external product / CMUX batch (config 3): one workgroup per GLWE pair, wave w on polynomial w;
 // SOL: GLWEs modulo p with a Normalize GGSW (ntt64_pbs.rs:553-702), else BNF (native GLWEs, Raw GGSW)
-template <bool CMUX, bool SOL = false>
-__global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
-                                                     const u64* __restrict__ ggsw_list, uint32_t batch, int base_log,
-                                                     const u64* __restrict__ tab, const uint32_t* __restrict__ gidx,
-                                                     uint32_t n_ggsw) {
-  __shared__ u64 buf[2 * MI_EXT_LDS_STRIDE];
-  __shared__ u64 lwtab[64];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t b = blockIdx.x;
-  if (b >= batch) return;
-  // per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one shared GGSW
-  const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
-  if (gi >= n_ggsw) return;  // uniform per workgroup
-  const u64* ggsw = ggsw_list + (size_t)gi * 4 * N;
-  load_lane_pair_tables(lwtab, tab, threadIdx.x);
+template <bool CMUX, bool SOL>
+__device__ __forceinline__ void ext_tw_item(u64* __restrict__ out, u64* __restrict__ glwe, const u64* __restrict__ ggsw,
+                                            uint32_t b, int base_log, const u64* __restrict__ tab, u64* buf,
+                                            u64* lwtab, uint32_t lane, uint32_t w) {
   const uint32_t S = (uint32_t)(uintptr_t)(buf + w * MI_EXT_LDS_STRIDE),
                  SP = (uint32_t)(uintptr_t)(buf + (1 - w) * MI_EXT_LDS_STRIDE);
   u64* o = out + ((size_t)b * 2 + w) * N;
@@ -267,6 +255,29 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
                            [out_lo] "s"(o_lo), [out_hi] "s"(o_hi), [gown_lo] "s"(gown_lo), [gown_hi] "s"(gown_hi),
                            [gpar_lo] "s"(gpar_lo), [gpar_hi] "s"(gpar_hi), [tab_lo] "s"(tab_lo),
                            [tab_hi] "s"(tab_hi), [bl] "s"(base_log), [LW] "s"((uint32_t)(uintptr_t)lwtab));
+}
+
+template <bool CMUX, bool SOL = false>
+__global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
+                                                     const u64* __restrict__ ggsw_list, uint32_t batch, int base_log,
+                                                     const u64* __restrict__ tab, const uint32_t* __restrict__ gidx,
+                                                     uint32_t n_ggsw) {
+  __shared__ u64 buf[2 * MI_EXT_LDS_STRIDE];
+  __shared__ u64 lwtab[64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (blockIdx.x >= batch) return;
+  load_lane_pair_tables(lwtab, tab, threadIdx.x);
+  // r5: a grid smaller than the batch loops over items b = blockIdx.x, + gridDim.x, ... (launch_ext_tw's persistent
+  // form, MI_EXT_PERSIST): the workgroups stay resident instead of being relaunched per item
+  for (uint32_t b = blockIdx.x; b < batch; b += gridDim.x) {
+    // per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one shared GGSW
+    const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
+    if (gi >= n_ggsw) continue;  // uniform per workgroup
+    ext_tw_item<CMUX, SOL>(out, glwe, ggsw_list + (size_t)gi * 4 * N, b, base_log, tab, buf, lwtab, lane, w);
+    // the item's row stores drain before the next item's loads (the body's vmcnt waits count only its own loads)
+    if (b + gridDim.x < batch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 // The blind-rotation body keeps the NTT-domain data in the forward's W1' register layout through the MAC
@@ -303,6 +314,14 @@ hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_po
 
 bool ext_tw_reads_w1p() { return MI_EXT_W1P != 0; }
 
+static bool ext_persist() {
+  static const bool on = [] {
+    const char* v = getenv("MI_EXT_PERSIST");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                          int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw,
                          bool prepared) {
@@ -319,7 +338,16 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
     }
     ggsw = perm;
   }
-  const dim3 g((unsigned)batch), blk(128);
+  // MI_EXT_PERSIST=1 (r5 A/B): at most 4 resident two-wave workgroups per CU (the bodies' 256 VGPRs allow 2 waves per
+  // SIMD), each looping over items; default: one workgroup per item
+  size_t wgs = batch;
+  if (ext_persist()) {
+    int dev = 0, cus = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    wgs = std::min<size_t>(batch, (size_t)cus * 4);
+  }
+  const dim3 g((unsigned)wgs), blk(128);
   if (sol && cmux)
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else if (sol)

@@ -20,7 +20,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import gen_tw_kernel as T  # noqa: E402
-from gen_tw_kernel import MulSlot, Seg, Slot, ct, gmul, pv  # noqa: E402
+from gen_tw_kernel import MulSlot, Seg, Slot, canon, ct, gmul, gs, pv  # noqa: E402
 
 XB = 64          # x[k] at v[XB + 2k : XB + 2k + 1]
 TB_K5 = 80      # the twist values tw[k] (ONLY passes)
@@ -33,9 +33,11 @@ def bitrev5(i):
     return int(format(i, "05b")[::-1], 2)
 
 
-def tower_exp(s, g):
-    """ntt64 mi_arith.hpp tower_exp(true, s, g): stage s, group g of the first five forward stages -> 2^(3 bitrev5)."""
-    return 3 * bitrev5((1 << s) + g)
+def tower_exp(s, g, fwd=True):
+    """mi_arith.hpp tower_exp(fwd, s, g): stage s, group g of the first five stages -> 2^(3 bitrev5) (forward) or its
+    inverse 2^(192 - 3 bitrev5)."""
+    r = 3 * bitrev5((1 << s) + g)
+    return r if fwd else (192 - r) % 192
 
 
 def X(k):
@@ -90,6 +92,43 @@ def tile5_stages(W, phase):
     return out
 
 
+def gs_stages_text(pairs_by_stage, scratch, canon_in=True, canon_out=True):
+    """GS stages (a, b) -> (a + b, (a - b) 2^e) on canonical inputs (the generator's gs keeps both outputs canonical
+    then); with canon_out every output is canonical at the end."""
+    slots = [Slot(scratch + 8 * i, SG + 6 * i) for i in range(3)]
+    flags = {}
+    lines = []
+    for st in pairs_by_stage:
+        sg = Seg()
+        for i, (a, b, e) in enumerate(st):
+            flags[a], flags[b] = gs(sg, slots[i % 3], X(a), X(b), e, flags.get(a, canon_in), flags.get(b, canon_in))
+        lines += sched(sg)
+    if canon_out and not all(flags.values()):
+        sg = Seg()
+        for i, r in enumerate(r for r, f in flags.items() if not f):
+            canon(sg, slots[i % 3], X(r))
+        lines += sched(sg)
+    return lines
+
+
+def tile5_inv_stages(W, phase):
+    """The inverse K = 5 tile (ntt64_tile.hpp phase_b<5, false> then phase_a<5, false>): phase B stages 4, 3 on rows
+    8 W + k (distance d), phase A stages 2, 1, 0 on rows W + 4 k (distance d / 4); GS with the inverse tower twiddles."""
+    K, RPT = 5, 8
+    out = []
+    for S in ((4, 3) if phase == "b" else (2, 1, 0)):
+        d = 1 << (K - 1 - S)
+        dk = d if phase == "b" else d // 4
+        st = []
+        for k in range(RPT):
+            if k & dk:
+                continue
+            row = (RPT * W + k) if phase == "b" else (W + 4 * k)
+            st.append((k, k + dk, tower_exp(S, row >> (K - S), fwd=False)))
+        out.append(st)
+    return out
+
+
 def emit_fn(name, lines, n_x, tb, scratch, n_scratch):
     xs = ", ".join(f'"+{{v[{XB + 2 * k}:{XB + 2 * k + 1}]}}"(x[{k}])' for k in range(n_x))
     ins = ", ".join(f'"{{v[{tb + 2 * k}:{tb + 2 * k + 1}]}}"(tw[{k}])' for k in range(n_x)) if tb else ""
@@ -112,6 +151,11 @@ def main():
         out.append(emit_fn(f"k5_fwd_a_w{W}", stages_text(tile5_stages(W, "a"), SC_K5), 8, None, SC_K5, 24))
         lines = stages_text(tile5_stages(W, "b"), SC_K5) + twist_text(8, TB_K5, SC_K5)
         out.append(emit_fn(f"k5_fwd_b_tw_w{W}", lines, 8, TB_K5, SC_K5, 24))
+        # the inverse tile of the accumulating last top pass (ntt64_kernels.hip top_tile_body<5, false, 2, ACC>): the
+        # block untwist on load, phase B; LDS exchange (C++); phase A, canonical outputs for the accumulation
+        lines = twist_text(8, TB_K5, SC_K5) + gs_stages_text(tile5_inv_stages(W, "b"), SC_K5)
+        out.append(emit_fn(f"k5_inv_tw_b_w{W}", lines, 8, TB_K5, SC_K5, 24))
+        out.append(emit_fn(f"k5_inv_a_w{W}", gs_stages_text(tile5_inv_stages(W, "a"), SC_K5), 8, None, SC_K5, 24))
     out += ["}  // namespace tile_asm", "}  // namespace mi"]
     print("\n".join(out))
 
