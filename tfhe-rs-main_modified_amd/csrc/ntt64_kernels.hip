@@ -183,7 +183,7 @@ __device__ __forceinline__ void tile5_inv_a(u64 (&x)[8]) {
 
 // The stage-0 pass of the split transform at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): the same function as
 // ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true> at s0 = 0.  Grid: x = column tiles of 64, y = polynomials.
-template <int K, bool FWD, int TWIST, int ACC, int W>
+template <int K, bool FWD, int TWIST, int ACC, int W, bool ASM = true>
 __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t cols, uint64_t col, uint32_t c,
                                               const u64* __restrict__ twist, u64* __restrict__ accp, u64* lds) {
   using Rw = tile::Rows<K>;
@@ -201,7 +201,7 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
       poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : Goldilocks::canon(x[k]);  // lazy stages
     }
   } else {
-    if constexpr (K == 5 && TWIST == 2) {  // r5: untwist + stages as generated asm (tools/gen_tile_asm.py)
+    if constexpr (K == 5 && TWIST == 2 && ASM) {  // r5: untwist + stages as generated asm (tools/gen_tile_asm.py)
       u64 tw[RPT];
 #pragma unroll
       for (int k = 0; k < RPT; ++k) {
@@ -232,7 +232,7 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
   }
 }
 
-template <int K, bool FWD, int TWIST, int ACC>
+template <int K, bool FWD, int TWIST, int ACC, bool ASM = true>
 __global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ data, uint64_t stride, uint32_t logn,
                                                            const u64* __restrict__ twist, u64* __restrict__ acc) {
   __shared__ u64 lds[(1 << K) * 64];
@@ -242,10 +242,10 @@ __global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ dat
   u64* poly = data + (uint64_t)blockIdx.y * stride;
   u64* accp = ACC ? acc + (uint64_t)blockIdx.y * stride : nullptr;
   switch (w) {
-    case 0: top_tile_body<K, FWD, TWIST, ACC, 0>(poly, cols, col, c, twist, accp, lds); break;
-    case 1: top_tile_body<K, FWD, TWIST, ACC, 1>(poly, cols, col, c, twist, accp, lds); break;
-    case 2: top_tile_body<K, FWD, TWIST, ACC, 2>(poly, cols, col, c, twist, accp, lds); break;
-    default: top_tile_body<K, FWD, TWIST, ACC, 3>(poly, cols, col, c, twist, accp, lds); break;
+    case 0: top_tile_body<K, FWD, TWIST, ACC, 0, ASM>(poly, cols, col, c, twist, accp, lds); break;
+    case 1: top_tile_body<K, FWD, TWIST, ACC, 1, ASM>(poly, cols, col, c, twist, accp, lds); break;
+    case 2: top_tile_body<K, FWD, TWIST, ACC, 2, ASM>(poly, cols, col, c, twist, accp, lds); break;
+    default: top_tile_body<K, FWD, TWIST, ACC, 3, ASM>(poly, cols, col, c, twist, accp, lds); break;
   }
 }
 
@@ -358,8 +358,12 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
   if constexpr (K >= 4) {
     if (s0 == 0 && logn >= K + 6) {
       const dim3 tgrid((unsigned)(((uint64_t)1 << (logn - K)) / 64), (unsigned)batch);
-      hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
-                         (uint32_t)logn, twist, acc);
+      if (tile_asm_enabled())
+        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
+                           (uint32_t)logn, twist, acc);
+      else  // MI_TILE_ASM=0: the compiled stages (A/B)
+        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, false>), tgrid, dim3(256), 0, s, data,
+                           (uint64_t)stride, (uint32_t)logn, twist, acc);
       return hipGetLastError();
     }
   }
@@ -383,6 +387,14 @@ static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int log
     case 5: return launch_top_tw<5, FWD, TWIST, ACC>(data, batch, stride, logn, s0, tw, twist, acc, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+bool tile_asm_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("MI_TILE_ASM");
+    return !(v && v[0] == '0');
+  }();
+  return on;
 }
 
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,

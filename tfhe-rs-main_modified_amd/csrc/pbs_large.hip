@@ -214,7 +214,7 @@ __device__ __forceinline__ void tile5_fwd_b_tw(u64 (&x)[8], const u64 (&tw)[8]) 
 // The same step at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): lane (wave W, column c) forms ct1 and the
 // decomposition state of its phase-A rows, then per level runs the phase-A stages, the LDS exchange and the phase-B
 // stages and stores the digit polynomial from its phase-B rows.  Grid: x = column tiles of 64, y = GLWE polynomials.
-template <int K, bool BNF, bool ONLY, int W>
+template <int K, bool BNF, bool ONLY, int W, bool ASM = true>
 __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64* __restrict__ ap, uint32_t full,
                                                  uint32_t rem, uint64_t cols, uint64_t col, uint32_t c, uint64_t per,
                                                  const LargeShape& sh, const u64* __restrict__ twist, u64* lds) {
@@ -252,7 +252,7 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
       x[k] = ((int64_t)term < 0) ? term + P : term;
     }
     u64* o = dp + (uint64_t)li * per;
-    if constexpr (K == 5 && ONLY) {  // r5: phase A, phase B and the block twist as generated asm (gen_tile_asm.py)
+    if constexpr (K == 5 && ONLY && ASM) {  // r5: phase A, phase B and the block twist as generated asm (gen_tile_asm.py)
       tile5_fwd_a<W>(x);
       tile::exchange<K, W, true>(x, lds, c);
       tile5_fwd_b_tw<W>(x, tv);
@@ -273,7 +273,7 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
   }
 }
 
-template <int K, bool BNF, bool ONLY>
+template <int K, bool BNF, bool ONLY, bool ASM = true>
 __global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digits, const u64* __restrict__ acc,
                                                          const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
                                                          LargeShape sh, const u64* __restrict__ twist) {
@@ -292,10 +292,10 @@ __global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digit
   const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
   u64* dp = digits + (uint64_t)b * sh.level * per + (uint64_t)cc * sh.n;
   switch (w) {
-    case 0: rotdec_tile_body<K, BNF, ONLY, 0>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    case 1: rotdec_tile_body<K, BNF, ONLY, 1>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    case 2: rotdec_tile_body<K, BNF, ONLY, 2>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    default: rotdec_tile_body<K, BNF, ONLY, 3>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 0: rotdec_tile_body<K, BNF, ONLY, 0, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 1: rotdec_tile_body<K, BNF, ONLY, 1, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 2: rotdec_tile_body<K, BNF, ONLY, 2, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    default: rotdec_tile_body<K, BNF, ONLY, 3, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
   }
 }
 
@@ -306,9 +306,12 @@ static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, cons
   if constexpr (K >= 4) {
     if ((sh.n >> K) >= 64) {  // the cooperative tile (>= one 64-column tile)
       const dim3 tgrid((unsigned)(((uint64_t)sh.n >> K) / 64), nb * (sh.k + 1));
-      if (only)
+      if (only && tile_asm_enabled())
         hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
                            sh, twist);
+      else if (only)  // MI_TILE_ASM=0: the compiled stages (A/B)
+        hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true, false>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe,
+                           step, sh, twist);
       else
         hipLaunchKernelGGL((large_rotdec_tile<K, BNF, false>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
                            sh, twist);
