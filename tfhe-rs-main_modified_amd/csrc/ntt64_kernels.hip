@@ -358,7 +358,7 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
   if constexpr (K >= 4) {
     if (s0 == 0 && logn >= K + 6) {
       const dim3 tgrid((unsigned)(((uint64_t)1 << (logn - K)) / 64), (unsigned)batch);
-      if (tile_asm_enabled())
+      if (tile_asm_enabled(2))
         hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
                            (uint32_t)logn, twist, acc);
       else  // MI_TILE_ASM=0: the compiled stages (A/B)
@@ -389,12 +389,12 @@ static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int log
   }
 }
 
-bool tile_asm_enabled() {
-  static const bool on = [] {
+bool tile_asm_enabled(int which) {
+  static const int mask = [] {
     const char* v = getenv("MI_TILE_ASM");
-    return !(v && v[0] == '0');
+    return v ? atoi(v) : 3;
   }();
-  return on;
+  return (mask & which) != 0;
 }
 
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,

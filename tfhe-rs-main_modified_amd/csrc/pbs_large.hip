@@ -306,7 +306,7 @@ static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, cons
   if constexpr (K >= 4) {
     if ((sh.n >> K) >= 64) {  // the cooperative tile (>= one 64-column tile)
       const dim3 tgrid((unsigned)(((uint64_t)sh.n >> K) / 64), nb * (sh.k + 1));
-      if (only && tile_asm_enabled())
+      if (only && tile_asm_enabled(1))
         hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
                            sh, twist);
       else if (only)  // MI_TILE_ASM=0: the compiled stages (A/B)
