@@ -174,6 +174,13 @@ __device__ __forceinline__ void tile5_inv_tw_b(u64 (&x)[8], const u64 (&tw)[8]) 
   else tile_asm::k5_inv_tw_b_w3(x, tw);
 }
 template <int W>
+__device__ __forceinline__ void tile5_inv_b(u64 (&x)[8]) {
+  if constexpr (W == 0) tile_asm::k5_inv_b_w0(x);
+  else if constexpr (W == 1) tile_asm::k5_inv_b_w1(x);
+  else if constexpr (W == 2) tile_asm::k5_inv_b_w2(x);
+  else tile_asm::k5_inv_b_w3(x);
+}
+template <int W>
 __device__ __forceinline__ void tile5_inv_a(u64 (&x)[8]) {
   if constexpr (W == 0) tile_asm::k5_inv_a_w0(x);
   else if constexpr (W == 1) tile_asm::k5_inv_a_w1(x);
@@ -183,7 +190,7 @@ __device__ __forceinline__ void tile5_inv_a(u64 (&x)[8]) {
 
 // The stage-0 pass of the split transform at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): the same function as
 // ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true> at s0 = 0.  Grid: x = column tiles of 64, y = polynomials.
-template <int K, bool FWD, int TWIST, int ACC, int W, bool ASM = true>
+template <int K, bool FWD, int TWIST, int ACC, int W, int ASM = 1>
 __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t cols, uint64_t col, uint32_t c,
                                               const u64* __restrict__ twist, u64* __restrict__ accp, u64* lds) {
   using Rw = tile::Rows<K>;
@@ -201,7 +208,16 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
       poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : Goldilocks::canon(x[k]);  // lazy stages
     }
   } else {
-    if constexpr (K == 5 && TWIST == 2 && ASM) {  // r5: untwist + stages as generated asm (tools/gen_tile_asm.py)
+    if constexpr (K == 5 && TWIST == 2 && ASM == 2) {  // r5: the compiled untwist on load, the stages as generated asm
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const uint64_t e = Rw::b(W, k) * cols + col;
+        x[k] = Goldilocks::mul(poly[e], twist[e]);
+      }
+      tile5_inv_b<W>(x);
+      tile::exchange<K, W, false>(x, lds, c);
+      tile5_inv_a<W>(x);
+    } else if constexpr (K == 5 && TWIST == 2 && ASM == 1) {  // r5: untwist + stages as generated asm (gen_tile_asm.py)
       u64 tw[RPT];
 #pragma unroll
       for (int k = 0; k < RPT; ++k) {
@@ -232,7 +248,7 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
   }
 }
 
-template <int K, bool FWD, int TWIST, int ACC, bool ASM = true>
+template <int K, bool FWD, int TWIST, int ACC, int ASM = 1>
 __global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ data, uint64_t stride, uint32_t logn,
                                                            const u64* __restrict__ twist, u64* __restrict__ acc) {
   __shared__ u64 lds[(1 << K) * 64];
@@ -359,10 +375,13 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
     if (s0 == 0 && logn >= K + 6) {
       const dim3 tgrid((unsigned)(((uint64_t)1 << (logn - K)) / 64), (unsigned)batch);
       if (tile_asm_enabled(2))
-        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
+        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 1>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
                            (uint32_t)logn, twist, acc);
-      else  // MI_TILE_ASM=0: the compiled stages (A/B)
-        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, false>), tgrid, dim3(256), 0, s, data,
+      else if (tile_asm_enabled(4))
+        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 2>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
+                           (uint32_t)logn, twist, acc);
+      else  // the compiled stages
+        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 0>), tgrid, dim3(256), 0, s, data,
                            (uint64_t)stride, (uint32_t)logn, twist, acc);
       return hipGetLastError();
     }

@@ -63,7 +63,8 @@ hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch,
                                   const uint64_t* body_tab, hipStream_t s);
 bool split_fused_enabled();  // MI_SPLIT_FUSED=0 in the environment: the two-launch form (A/B)
 // MI_TILE_ASM=<mask> in the environment (A/B, r5; default 1): bit 0 the rotation pass's forward K = 5 tile asm, bit 1
-// the accumulating inverse K = 5 top tile asm; a cleared bit runs the compiled stages
+// the accumulating inverse K = 5 top tile asm (untwist + stages), bit 2 its stages only (the untwist compiled); cleared
+// bits run the compiled stages
 bool tile_asm_enabled(int which);
 hipError_t launch_ntt_split(bool fwd, int logn, uint64_t* data, size_t batch, size_t stride, const uint64_t* tw,
                             const SplitTw& st, hipStream_t s, uint64_t* acc = nullptr, int acc_mode = 0,

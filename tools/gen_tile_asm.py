@@ -156,6 +156,8 @@ def main():
         lines = twist_text(8, TB_K5, SC_K5) + gs_stages_text(tile5_inv_stages(W, "b"), SC_K5)
         out.append(emit_fn(f"k5_inv_tw_b_w{W}", lines, 8, TB_K5, SC_K5, 24))
         out.append(emit_fn(f"k5_inv_a_w{W}", gs_stages_text(tile5_inv_stages(W, "a"), SC_K5), 8, None, SC_K5, 24))
+        # the same phase B without the untwist (the compiled multiply overlaps the row loads; MI_TILE_ASM bit 2)
+        out.append(emit_fn(f"k5_inv_b_w{W}", gs_stages_text(tile5_inv_stages(W, "b"), SC_K5), 8, None, SC_K5, 24))
     out += ["}  // namespace tile_asm", "}  // namespace mi"]
     print("\n".join(out))
 
