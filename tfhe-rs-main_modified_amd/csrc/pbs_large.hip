@@ -674,7 +674,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   // MI_PBS_WAVE_CAP=<waves per SIMD> (r5 A/B): the step's body launches hold at most that many waves per SIMD of the
   // device and loop over their units, so two lanes' launches can share every CU (one's memory phase beside the
   // other's issue-bound bodies) instead of filling the device one after the other; 0 / unset: full grids
-  const size_t wave_cap = (size_t)pbs_wave_cap() * (size_t)device_simds(s);
+  const size_t wave_cap = pbs_wave_cap() ? (size_t)pbs_wave_cap() * device_simds(s) : 0;
   // one lane's share of a chunk: ciphertexts [b0, b0 + nb) of the batch, its scratch slices, its stream
   struct Lane {
     size_t b0;
