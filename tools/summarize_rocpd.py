@@ -23,6 +23,11 @@ PEAK = 8.0e12
 HEAD_GRID = 8192 * 64  # lanes of the headline launches (both directions)
 
 
+def is_fwd(name):
+    """ntt_tw_body_kernel<true> / <true, false> (r5: the PERSIST parameter) or its mangled form."""
+    return "<true" in name or "ILb1E" in name
+
+
 def main():
     db, dst = sys.argv[1], sys.argv[2]
     line = json.load(open(sys.argv[3])) if len(sys.argv) > 3 else None
@@ -52,7 +57,7 @@ def main():
         if not ds:
             continue
         avg = sum(ds) / len(ds)
-        head["fwd" if "<true>" in name or "ILb1E" in name else "inv"] = {
+        head["fwd" if is_fwd(name) else "inv"] = {
             "kernel": name, "launches": len(ds), "average_ns": avg, "min_ns": min(ds),
             "achieved_GBps": ALG_BYTES / (avg * 1e-9) / 1e9, "frac": ALG_BYTES / (avg * 1e-9) / PEAK}
     out = {"source": os.path.basename(db), "headline_kernels": head}
@@ -65,7 +70,7 @@ def main():
         # >= 2 (W + K) launches is the cold start, the second the headline (then the steady-state loop)
         runs, cur = [], []
         for name, d, g, _ in rows:
-            kind = ("fwd" if "<true>" in name else "inv") if "ntt_tw_body_kernel" in name and g == HEAD_GRID else None
+            kind = ("fwd" if is_fwd(name) else "inv") if "ntt_tw_body_kernel" in name and g == HEAD_GRID else None
             if kind and (not cur or cur[-1][0] != kind):
                 cur.append((kind, d))
                 continue
