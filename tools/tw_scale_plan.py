@@ -65,6 +65,11 @@ def ct_network(kind):
         for q in range(5):
             d = 16 >> q
             st.append([(r, r + d, tabs["CYC_FWD"][q][r // (2 * d)]) for r in range(32) if not r & d])
+    elif kind == "inv_dit":  # the W1'' inverse's in-register DIT stages (gen_tw_kernel.dit_exps_pp, by register)
+        for q in range(5):
+            d = 1 << q
+            e = T.dit_exps_pp(q)
+            st.append([(r, r + d, e[r]) for r in range(32) if not r & d])
     elif kind == "inv_g1":
         for s in range(4, -1, -1):
             d = 16 >> s
@@ -170,6 +175,14 @@ def solve(iters=120000, seeds=4):
     best_c = min(anneal(fn_c, 80, True, iters, 10 + s) for s in range(seeds))
     assert best_c[0] < big, "forward CYC plan leaves a scaled output"
     plan["fwd_cyc"] = {"modes": best_c[2], "in_scales": best_c[1], "cost": best_c[0], "base": base_c}
+    # inverse DIT (the W1'' cyclic blocks, r5): inputs 0 (loaded, canonical), outputs free -> the untwist table; the
+    # lane-pair DIT stage between passes each register's scale through (its two inputs come from one register)
+    net_d = ct_network("inv_dit")
+    fn_d = lambda inp, m, x: eval_ct(net_d, [0] * 32, m, [True] * 32)[0]
+    base_d = fn_d(None, [0] * 80, None)
+    best_d = min(anneal(fn_d, 80, False, iters, 30 + s) for s in range(seeds))
+    out_d = eval_ct(net_d, [0] * 32, best_d[2], [True] * 32)[1]
+    plan["inv_dit"] = {"modes": best_d[2], "out_scales": out_d, "cost": best_d[0], "base": base_d}
     # inverse G1 (GS): inputs free (untwist), outputs 0
     net_g = ct_network("inv_g1")
     GS_START = [w for st in net_g for (_, _, w) in st]
