@@ -293,7 +293,7 @@ hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint
   if (sub_log < 1 || !inv_mac_supported(level, kp1)) return hipErrorInvalidValue;
   if (n_items == 0) return hipSuccess;
   const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
-  if (units > 0x7fffffffull * 4) return hipErrorInvalidValue;  // one launch (the callers' chunks are far below)
+  if (units > 0xffffffffull - 4 * 65536) return hipErrorInvalidValue;  // uint32 unit indices (the callers' chunks are far below)
   const uint64_t wgs = (units + 3) / 4, cap = wave_cap ? std::max<uint64_t>(1, wave_cap / 4) : wgs;
   const dim3 grid((unsigned)std::min(wgs, cap)), block(256);
   const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
