@@ -396,46 +396,7 @@ __global__ __launch_bounds__(256) void large_mac(u64* __restrict__ y, const u64*
 // takes two adjacent coefficients (16-byte accesses).  Grid: x over coefficient pairs, y over the items.
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-// The sum of a column's level (k + 1) products without a carry chain per product: each term's four 32 x 32 partial
-// products go straight into three 64-bit column accumulators (bits 0, 32 and 64 up) through v_mad_u64_u32's own
-// addend, their carries out of the accumulator counted apart: 8 VALU per term instead of a 128-bit product (4 mads plus
-// the limb assembly) and a 128-bit add (~19 VALU as compiled).  value() combines the columns and reduces once.
-struct Acc128 {
-  u64 a0 = 0, a32 = 0, a64 = 0;
-  uint32_t n0 = 0, n32 = 0, n64 = 0;
-  __device__ __forceinline__ void mac(u64 x, u64 w) {
-    const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
-    uint64_t c0, c1, c2, c3, junk;
-    // every carry is read >= 3 instructions after the mad that wrote it (VALU-written SGPR -> VALU read); not volatile:
-    // the block has no side effect beyond its outputs, so the compiler may schedule the loads around it
-    asm(
-        "v_mad_u64_u32 %[a0], %[c0], %[x0], %[w0], %[a0]\n\t"
-        "v_mad_u64_u32 %[a32], %[c1], %[x0], %[w1], %[a32]\n\t"
-        "v_mad_u64_u32 %[a64], %[c3], %[x1], %[w1], %[a64]\n\t"
-        "v_mad_u64_u32 %[a32], %[c2], %[x1], %[w0], %[a32]\n\t"
-        "v_addc_co_u32_e64 %[n0], %[j], %[n0], 0, %[c0]\n\t"
-        "v_addc_co_u32_e64 %[n32], %[j], %[n32], 0, %[c1]\n\t"
-        "v_addc_co_u32_e64 %[n64], %[j], %[n64], 0, %[c3]\n\t"
-        "v_addc_co_u32_e64 %[n32], %[j], %[n32], 0, %[c2]"
-        : [a0] "+v"(a0), [a32] "+v"(a32), [a64] "+v"(a64), [n0] "+v"(n0), [n32] "+v"(n32), [n64] "+v"(n64),
-          [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3), [j] "=&s"(junk)
-        : [x0] "v"(x0), [x1] "v"(x1), [w0] "v"(w0), [w1] "v"(w1));
-  }
-  // a0 + a32 2^32 + (a64 + n0) 2^64 + n32 2^96 + n64 2^128, with 2^128 = -2^32 mod p
-  __device__ __forceinline__ u64 value(u64 n_inv) const {
-    const u64 lo = a0 + (a32 << 32);
-    const u64 t = (a32 >> 32) + (lo < a0);
-    u64 hi = a64 + t;
-    uint32_t top = n64 + (hi < t);
-    hi += n0;
-    top += hi < (u64)n0;
-    const u64 h32 = (u64)n32 << 32;
-    hi += h32;
-    top += hi < h32;
-    const u64 v = Goldilocks::sub(Goldilocks::reduce128(lo, hi), (u64)top << 32);
-    return n_inv ? Goldilocks::mul(v, n_inv) : v;
-  }
-};
+// Acc128: the sum of a column's products with one reduction at the end (pbs_device.hpp)
 
 // LEVEL > 0: the level count is compile-time (the shortint shapes' 1 - 3), so the level loop unrolls and every load of
 // the item is issued before the first product; LEVEL = 0 reads it from sh
