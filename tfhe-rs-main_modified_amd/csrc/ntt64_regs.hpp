@@ -58,9 +58,12 @@ __host__ __device__ __forceinline__ constexpr int win_lo(int w) {
 // (entry m + g = 2^tower_exp(log2 m, g), every Goldilocks plan, prime64.rs:166-177); where the window also leaves the
 // group index compile-time (the lanes' bits lie below the window: lo >= LOGT, the first forward / last inverse
 // window) the multiply is a shift (Goldilocks::mul_pow2) instead of a table load and a four-limb product.
-template <class G, bool FWD, class Mod, bool SUB = false>
+// LAZY (forward, Goldilocks only, r5): the butterflies' outputs are any 64-bit representatives (Goldilocks::add_lazy /
+// sub_lazy against the canonical product), for consumers that reduce anyway (the shape kernels' MAC, pbs::Acc128)
+template <class G, bool FWD, class Mod, bool SUB = false, bool LAZY = false>
 __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w, const u64* __restrict__ tw,
                                                    const Mod& mod, uint32_t twc = 1) {
+  constexpr bool lazy = LAZY && FWD && std::is_same<Mod, Goldilocks>::value;
   const int lo = win_lo<G, FWD>(w);
   int rb_first, rb_last;  // r-bits of this window that still need a stage
   if (w < G::NFULL) { rb_first = 0; rb_last = G::LOGE - 1; }
@@ -82,7 +85,12 @@ __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w,
       if (std::is_same<Mod, Goldilocks>::value && !SUB && m < 32 && lo >= G::LOGT) {
         const int s_ref = G::LOGN - 1 - b, ex = tower_exp(FWD, s_ref, r0 >> (rb + 1));  // (t >> lo) == 0 here
         bool ng;
-        if (FWD) {
+        if (FWD && lazy) {
+          const u64 z = Goldilocks::mul_pow2(x[r1], ex, ng);
+          const u64 a = x[r0];
+          x[r0] = ng ? Goldilocks::sub_lazy(a, z) : Goldilocks::add_lazy(a, z);
+          x[r1] = ng ? Goldilocks::add_lazy(a, z) : Goldilocks::sub_lazy(a, z);
+        } else if (FWD) {
           const u64 z = Goldilocks::mul_pow2(x[r1], ex, ng);
           const u64 a = x[r0];
           x[r0] = ng ? Goldilocks::sub(a, z) : Goldilocks::add(a, z);
@@ -95,7 +103,12 @@ __device__ __forceinline__ void window_butterflies(u64 (&x)[G::E], int t, int w,
         continue;
       }
       const u64 wv = tw[(SUB ? m * twc : m) + (tpart | (r0 >> (rb + 1)))];
-      if (FWD) {
+      if constexpr (lazy) {
+        const u64 z1w = Goldilocks::mul(x[r1], wv);  // any x: a canonical product
+        const u64 a = x[r0];
+        x[r0] = Goldilocks::add_lazy(a, z1w);
+        x[r1] = Goldilocks::sub_lazy(a, z1w);
+      } else if (FWD) {
         const u64 z1w = mod.mul(x[r1], wv);
         const u64 a = x[r0];
         x[r0] = mod.add(a, z1w);
@@ -126,7 +139,7 @@ __device__ __forceinline__ void window_load(u64 (&x)[G::E], int t, int w, const 
 
 // Whole transform of NP polynomials (registers x[p]) sharing barriers; sh has NP * PADDED u64.
 // Entry: layout of window 0; exit: layout of the last window.  Contains __syncthreads().
-template <class G, bool FWD, int NP, class Mod>
+template <class G, bool FWD, int NP, class Mod, bool LAZY = false>
 __device__ __forceinline__ void ntt_regs(u64 (&x)[NP][G::E], int t, u64* sh, const u64* __restrict__ tw,
                                          const Mod& mod) {
 #pragma unroll
@@ -140,7 +153,7 @@ __device__ __forceinline__ void ntt_regs(u64 (&x)[NP][G::E], int t, u64* sh, con
       __syncthreads();
     }
 #pragma unroll
-    for (int p = 0; p < NP; ++p) window_butterflies<G, FWD>(x[p], t, w, tw, mod);
+    for (int p = 0; p < NP; ++p) window_butterflies<G, FWD, Mod, false, LAZY>(x[p], t, w, tw, mod);
   }
 }
 

@@ -123,7 +123,7 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
           x[c][r] = digit(state[c][r], sign[c][r]);
         }
       }
-    ntt_regs<G, true, K + 1>(x, t, sh, tw, gl);
+    ntt_regs<G, true, K + 1, Goldilocks, true>(x, t, sh, tw, gl);  // lazy: the MAC below reduces its sums anyway
     // the iterator yields DecompositionLevel(level_count) first (the least significant digit), the
     // GGSW stores that level first too (ggsw_encryption.rs:318-375): GGSW block li pairs with term li
     const u64* mat = ggsw + (size_t)li * (K + 1) * (K + 1) * N;
