@@ -225,10 +225,14 @@ template <int L>
 __global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
                                                              const u64* __restrict__ ggsw, uint32_t units,
                                                              uint32_t n_items, uint32_t sub_log, uint32_t kp1,
-                                                             const u64* __restrict__ twist) {
+                                                             const u64* __restrict__ twist, uint32_t stagger) {
   constexpr uint32_t W = 4;
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // MI_PBS_STAGGER (A/B, r5, with a capped looping grid): every other round of 256 workgroups starts later, so the
+  // waves sharing a CU run the MAC's memory phase and the inverse's issue-bound phase at different times
+  if (stagger && ((blockIdx.x >> 8) & 1))
+    for (uint32_t i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
   for (uint32_t u = blockIdx.x * W + wv; u < units; u += gridDim.x * W) {
     inv_mac_unit<L>(y, digits, ggsw, u, n_items, sub_log, kp1, twist, lds + wv * WAVE_LDS2, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as ntt_tw_body_kernel<PERSIST>
@@ -289,6 +293,10 @@ bool inv_mac_supported(int level, int kp1) {
 
 hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
                                  int level, int logn, const uint64_t* twist, hipStream_t s, size_t wave_cap) {
+  static const uint32_t stagger = [] {
+    const char* v = getenv("MI_PBS_STAGGER");
+    return v ? (uint32_t)std::max(0, atoi(v)) : 0u;
+  }();
   const int sub_log = logn - 11;
   if (sub_log < 1 || !inv_mac_supported(level, kp1)) return hipErrorInvalidValue;
   if (n_items == 0) return hipSuccess;
@@ -298,11 +306,11 @@ hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint
   const dim3 grid((unsigned)std::min(wgs, cap)), block(256);
   const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
   switch (level * kp1) {
-    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
-    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
-    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
-    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
-    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
+    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
+    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
+    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
+    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
   }
   return hipGetLastError();
 }
