@@ -239,6 +239,50 @@ __global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y
   }
 }
 
+// The wave-specialised form (r5, MI_PBS_WS; tools/gen_tw_kernel.py gen_macp / gen_invc): two-wave workgroups loop
+// over the units u = blockIdx.x, + gridDim.x, ...; wave 0 forms unit u's block of y row by row into the workgroup's
+// LDS hand-off buffer while wave 1 runs the inverse of the unit before (its transposes in a second LDS region), so each
+// SIMD overlaps the MAC's loads with the inverse's arithmetic.  Both waves run the same trip count and two s_barriers
+// per unit (inside the bodies), so the workgroup cannot deadlock; the consumer waits for its previous stores first.
+template <int L>
+__global__ __launch_bounds__(128) void ntt_tw_inv_mac_ws_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
+                                                                const u64* __restrict__ ggsw, uint32_t units,
+                                                                uint32_t n_items, uint32_t sub_log, uint32_t kp1,
+                                                                const u64* __restrict__ twist) {
+  __shared__ u64 lds[2048 + WAVE_LDS2];  // one block of y, then the consumer's transposes
+  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t yw = (uint32_t)(uintptr_t)lds + lane * 8, l8 = lane * 8, S = (uint32_t)(uintptr_t)(lds + 2048);
+  const uint64_t n = (uint64_t)2048 << sub_log;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t c = u % kp1, ib = u / kp1, b = ib % n_items, blk = ib / n_items;
+    if (wv == 0) {
+      const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
+      const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
+      const uint32_t dlo = (uint32_t)(uintptr_t)d, dhi = (uint32_t)((uintptr_t)d >> 32);
+      const uint32_t gglo = (uint32_t)(uintptr_t)g, gghi = (uint32_t)((uintptr_t)g >> 32);
+      const uint32_t dstep = (uint32_t)(n * 8), gstep = (uint32_t)(kp1 * n * 8);
+#define MI_MACP_OPS                                                                                              \
+  [d_lo] "s"(dlo), [d_hi] "s"(dhi), [dstep] "s"(dstep), [gg_lo] "s"(gglo), [gg_hi] "s"(gghi), [gstep] "s"(gstep), \
+      [l8] "v"(l8), [yw] "v"(yw)
+      if constexpr (L == 4) MI_TW_BODY_MACP4(MI_MACP_OPS);
+      else MI_TW_BODY_MACP6(MI_MACP_OPS);
+#undef MI_MACP_OPS
+    } else {
+      u64* p = y + ((uint64_t)b * kp1 + c) * n + (uint64_t)blk * 2048;
+      const uint32_t par = lane & 1, i = lane >> 1;
+      const uint32_t lwo = par * 128;
+      const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
+      const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
+      const u64* lw = twist + 2 * (2048 + 32);  // the last-DIT-stage table (tw_body<false>)
+      const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
+      const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
+      const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
+      MI_TW_BODY_INVC([g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw),
+                      [l8] "v"(l8), [t4w] "v"(t4w), [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo), [yw] "v"(yw));
+    }
+  }
+}
+
 }  // namespace tw
 
 hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
@@ -286,6 +330,12 @@ hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch,
   return hipGetLastError();
 }
 
+// MI_PBS_WS = two-wave workgroups per CU of the wave-specialised MAC-fused inverse (0: the four-wave fused kernel)
+static uint32_t inv_mac_ws_wgs_per_cu() {  // read per launch (tests switch it within one process)
+  const char* v = getenv("MI_PBS_WS");
+  return v ? (uint32_t)std::max(0, std::min(8, atoi(v))) : 0u;
+}
+
 bool inv_mac_supported(int level, int kp1) {
   const int L = level * kp1;
   return L == 2 || L == 3 || L == 4 || L == 6 || L == 8;
@@ -302,6 +352,18 @@ hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint
   if (n_items == 0) return hipSuccess;
   const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
   if (units > 0xffffffffull - 4 * 65536) return hipErrorInvalidValue;  // uint32 unit indices (the callers' chunks are far below)
+  if ((level * kp1 == 4 || level * kp1 == 6) && inv_mac_ws_wgs_per_cu() > 0) {  // MI_PBS_WS (r5 A/B)
+    int dev = 0, cus = 0;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const dim3 g((unsigned)std::min<uint64_t>(units, (uint64_t)cus * inv_mac_ws_wgs_per_cu())), blk(128);
+    const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
+    if (level * kp1 == 4)
+      hipLaunchKernelGGL(tw::ntt_tw_inv_mac_ws_kernel<4>, g, blk, 0, s, y, digits, ggsw, un, ni, sl, kp, twist);
+    else
+      hipLaunchKernelGGL(tw::ntt_tw_inv_mac_ws_kernel<6>, g, blk, 0, s, y, digits, ggsw, un, ni, sl, kp, twist);
+    return hipGetLastError();
+  }
   const uint64_t wgs = (units + 3) / 4, cap = wave_cap ? std::max<uint64_t>(1, wave_cap / 4) : wgs;
   const dim3 grid((unsigned)std::min(wgs, cap)), block(256);
   const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;

@@ -452,6 +452,54 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra
     return out if out_of_place else data
 
 
+def run_ws(hdr, L, twist_tab, mem_extra, ops_extra, units=1, producer_ops=None):
+    """Emulate the wave-specialised MAC-fused inverse's two-wave workgroup (gen_tw_kernel.gen_macp / gen_invc) over
+    `units` consecutive units: wave 0 runs macp{L} per unit, wave 1 invc, round-robin between s_barriers, one LDS
+    (the y buffer at 0, the consumer's transposes after it).  producer_ops(k) / ops_extra: per-unit term bases
+    (d_lo, d_hi, gg_lo, gg_hi, dstep, gstep) and the consumer's output base per unit (g_lo / g_hi via
+    ops_extra["out"](k) -> (lo, hi)).  Returns nothing: the outputs land in mem_extra's regions."""
+    tw = np.array(twist_tab, dtype=np.uint64)
+    TB = 0x200000000
+    mem = {TB: tw}
+    mem.update(mem_extra)
+    lds = np.zeros(8192, dtype=np.uint64)
+    lane = np.arange(LANES, dtype=np.uint64)
+    par, i = lane & np.uint64(1), lane >> np.uint64(1)
+    S = 16384  # the consumer's transposes after the 16 KiB hand-off buffer (ntt_tw_inv_mac_ws_kernel)
+    lw = TB + 2048 * 8
+    vin = {"l8": lane * 8, "lwo": par * 128, "t4w": S + ((i & 15) * 66 + par) * 8,
+           "t1x": S + (lane + (lane >> np.uint64(5))) * 8, "t1y": S + ((i & 15) * 66 + 33 * par) * 8,
+           "yw": lane * 8}
+
+    def wave(ops):
+        w = Wave(None, mem, lds=lds)
+        for k, (name_, val) in enumerate(vin.items()):
+            w.v[200 + k] = val.astype(np.uint64)
+            ops[name_] = f"v{200 + k}"
+        w.s[104], w.s[105] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
+        ops["lw"] = "s[104:105]"
+        ops["tw_lo"], ops["tw_hi"] = f"{TB & 0xFFFFFFFF}", f"{TB >> 32}"
+        w.ops = ops
+        return w
+
+    pl, cl = body_lines(hdr, f"macp{L}"), body_lines(hdr, "invc")
+
+    def run_wave(lines, ops_for):
+        for k in range(units):
+            w = wave(ops_for(k))
+            w.load(lines)
+            yield from w.steps()
+
+    gens = [run_wave(pl, producer_ops), run_wave(cl, lambda k: dict(zip(("g_lo", "g_hi"), ops_extra["out"](k))))]
+    live = list(gens)
+    while live:  # every live wave runs to its next barrier, then the next one
+        for g in list(live):
+            try:
+                next(g)
+            except StopIteration:
+                live.remove(g)
+
+
 def _lds_with_lane_pair_tables(tab, N, stride=None):
     """Workgroup LDS as pbs_tw.hip lays it out: 2 exchange buffers of `stride` u64 (default N), then the 32 forward
     lane-pair twiddles (tab[N:N+32]) and the W1'' inverse's 32 last-DIT-stage twiddles, entry m + 16 par =

@@ -1753,11 +1753,15 @@ def mac_row(sg, L, bufs_of_terms, slot, out):
     sg.add(f"v_cndmask_b32_e64 v{out + 1}, v{out + 1}, {a0h}, {f[9]}", [f"v{out + 1}", a0h, f[9]], [f"v{out + 1}"])
 
 
-def mac_phase(B, L, dmap, vhi=MAC_VHI):
+def mac_phase(B, L, dmap, vhi=MAC_VHI, bufs=None, after_row=None):
     """Rows 0..31 of y = sum_q d_q G_q into dmap (W0: lane j of row r = element 64 r + j of the block).  Term (r, q)
-    loads d_q row r from %[d] + q %[dstep] and G_q row r from %[gg] + q %[gstep] (bytes)."""
+    loads d_q row r from %[d] + q %[dstep] and G_q row r from %[gg] + q %[gstep] (bytes).  bufs / after_row (the
+    wave-specialised producer): another term ring, and lines emitted after each row (its hand-off write)."""
     assert 2 <= L <= 8 and S_MB + 4 * L <= 96
-    bufs, slot = mac_ring(vhi)
+    if bufs is None:
+        bufs, slot = mac_ring(vhi)
+    else:
+        slot = mac_ring(vhi)[1]
     ring = len(bufs)
     dq = lambda q: S_MB + 2 * q
     gq = lambda q: S_MB + 2 * L + 2 * q
@@ -1795,6 +1799,8 @@ def mac_phase(B, L, dmap, vhi=MAC_VHI):
         nxt = min(issued + L, total)
         B.raw(*[l for t in range(issued, nxt) for l in issue(t)])
         issued = nxt
+        if after_row:
+            B.raw(*after_row(r))
 
 
 def gen_inv_mac(tabs, L, vhi=MAC_VHI):
@@ -1802,6 +1808,51 @@ def gen_inv_mac(tabs, L, vhi=MAC_VHI):
     dmap = [64 + 2 * r for r in range(32)]
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     mac_phase(B, L, dmap, vhi)
+    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
+    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    assert INV_W1PP
+    dmap = inv_core(B, tabs, dmap, w1pp=True)
+    B.raw(*store_rows(dmap, S_GB))
+    return B
+
+
+# The wave-specialised form (r5, pbs_large.hip MI_PBS_WS): a two-wave workgroup loops over units; its producer wave
+# forms unit u's block of y (mac_phase) while its consumer wave runs the inverse of unit u - 1, so the MAC's memory
+# phase and the inverse's issue phase overlap inside every SIMD (the dispatcher puts two producers and two consumers on
+# each SIMD, tools/placement_probe.hip) instead of running in lockstep across the device.  Hand-off through the
+# workgroup's 16 KiB LDS buffer (row r, lane j at %[yw] + 512 r, %[yw] = buffer + 8 lane); the consumer's transposes
+# use a second region.  Per unit both waves execute two s_barriers: (1) the rows are written, (2) the consumer has read
+# them (the producer writes the next unit's rows only after it).
+WS_LS = (4, 6)   # l (k + 1) of the 3_3 and 4_4 shapes (k = 1, l = 2 / 3); other L keep ntt_tw_inv_mac_kernel
+
+
+WS_OUT = (124, 126)   # the producer's row results alternate between these pairs (each row's hand-off write reads one)
+
+
+def gen_macp(tabs, L):
+    """Producer half: y's block row by row, each row written to the LDS hand-off buffer as soon as it is reduced (the
+    buffer is free: the consumer read the previous unit's rows before the last barrier), so the data registers join the
+    term ring (26 terms ahead instead of 11); then (1) the rows are complete, (2) the consumer has read them."""
+    B = Body(tabs)
+    dmap = [WS_OUT[r % 2] for r in range(32)]
+    bufs = mac_ring(MAC_VHI)[0] + [64 + 4 * k for k in range(15)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
+    mac_phase(B, L, dmap, bufs=bufs,
+              after_row=lambda r: [f"ds_write_b64 %[yw], {pv(WS_OUT[r % 2])} offset:{512 * r}"])
+    B.raw("s_waitcnt lgkmcnt(0)", "s_barrier", "s_barrier")
+    return B
+
+
+def gen_invc(tabs):
+    """Consumer half: (1) the rows are complete (its previous unit's stores drain meanwhile), the rows from the LDS
+    buffer, (2) released to the producer, then the inverse body (gen_inv_mac's after its MAC; its transposes in the
+    workgroup's second LDS region) and the stores."""
+    B = Body(tabs)
+    dmap = [64 + 2 * r for r in range(32)]
+    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
+    B.raw("s_barrier", "s_waitcnt vmcnt(0)",
+          *[f"ds_read_b64 {pv(dmap[r])}, %[yw] offset:{512 * r}" for r in range(32)], "s_waitcnt lgkmcnt(0)",
+          "s_barrier")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
     B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
     assert INV_W1PP
@@ -1831,6 +1882,9 @@ def main():
     print(emit("fwd_ms64", gen_fwd_ms64(tabs), None, MS_SGPRS))
     for L in MAC_LS:
         print(emit(f"inv_mac{L}", gen_inv_mac(tabs, L), None, range(94, max(94, S_MB + 4 * L)), MAC_VHI))
+    for L in WS_LS:
+        print(emit(f"macp{L}", gen_macp(tabs, L), None, range(94, max(94, S_MB + 4 * L)), MAC_VHI))
+    print(emit("invc", gen_invc(tabs), None, (), MAC_VHI))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 

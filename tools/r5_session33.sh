@@ -1,0 +1,15 @@
+#!/bin/bash
+# r5 GPU session 33 (after the wave-specialised MAC-fused inverse went in as an A/B option, default off): the full GPU
+# suite (incl. test_large_pbs_wave_specialised), the driver's bench command, smoke, and the wave-placement probe
+source tools/gpu_session_lib.sh
+O=gpurun_out/r5final4
+mkdir -p $O
+step pytest_gpu 700 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread
+rc=$?
+[ $rc -le 1 ] || exit $rc
+step bench_driver_cmd 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+grep '"metric"' gpurun_out/bench_driver_cmd.txt | tail -1 > $O/bench_line_driver_cmd.json
+step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
+step placement 60 ./tools/placement_probe || exit 1
+cp gpurun_out/placement.txt $O/placement_probe.txt
+exit $rc
