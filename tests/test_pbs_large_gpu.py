@@ -34,11 +34,13 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-@pytest.mark.parametrize("n", [8192, 16384, 32768, 65536, 131072])
+@pytest.mark.parametrize("n,lazy", [(8192, "1"), (8192, "0"), (16384, "1"), (32768, "1"), (65536, "1"), (131072, "1")])
 @pytest.mark.parametrize("bnf", [True, False])
-def test_large_random_keys(engine, oracle, n, bnf):
+def test_large_random_keys(engine, oracle, n, lazy, bnf, monkeypatch):
     """Every N check_pbs_shape accepts past 8192: 32768 runs the K = 4 cooperative first top pass
-    (large_rotdec_tile), 131072 the two-pass split (large_rotdec_top<3> then the skip-first split) — ADVICE r4."""
+    (large_rotdec_tile), 131072 the two-pass split (large_rotdec_top<3> then the skip-first split) — ADVICE r4.
+    lazy "0": the rotation pass's top stages canonical (MI_ROTDEC_LAZY=0, the r5 A/B form) at 8192."""
+    monkeypatch.setenv("MI_ROTDEC_LAZY", lazy)
     q = 0 if bnf else P
     k = 1
     pl = engine.Plan.try_new(n, P)

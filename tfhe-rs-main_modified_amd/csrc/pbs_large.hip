@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void large_rotate_decompose(u64* __restrict__ 
 // (stage 0's twiddles are the tower's powers of two, Goldilocks::mul_pow2; the split tables exist only when they are)
 // in the layout of large_rotate_decompose.  Replaces that pass plus the transform's first pass: acc is read once and
 // the digits written once (not written, read and written again).
-template <int K, bool BNF, bool ONLY>
+template <int K, bool BNF, bool ONLY, bool LAZY = true>
 __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits, const u64* __restrict__ acc,
                                                         const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
                                                         LargeShape sh, const u64* __restrict__ tw,
@@ -175,10 +175,15 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
       for (int r = 0; r < R; ++r) {
         if (r & d) continue;
         bool ng;
-        const u64 z = Goldilocks::mul_pow2(x[r + d], tower_exp(true, s, r >> (K - s)), ng);
+        const u64 z = Goldilocks::mul_pow2(x[r + d], tower_exp(true, s, r >> (K - s)), ng);  // canonical, any input
         const u64 u = x[r];
-        x[r] = ng ? gl.sub(u, z) : gl.add(u, z);
-        x[r + d] = ng ? gl.add(u, z) : gl.sub(u, z);
+        if (ONLY && LAZY) {  // r5: any 64-bit representatives until the block twist's multiply (as the K = 5 tile)
+          x[r] = ng ? Goldilocks::sub_lazy(u, z) : Goldilocks::add_lazy(u, z);
+          x[r + d] = ng ? Goldilocks::add_lazy(u, z) : Goldilocks::sub_lazy(u, z);
+        } else {
+          x[r] = ng ? gl.sub(u, z) : gl.add(u, z);
+          x[r + d] = ng ? gl.add(u, z) : gl.sub(u, z);
+        }
       }
     }
     u64* o = dp + (uint64_t)li * per;
@@ -299,6 +304,11 @@ __global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digit
   }
 }
 
+static bool rotdec_lazy() {  // read per launch (A/B and tests in one process)
+  const char* v = getenv("MI_ROTDEC_LAZY");
+  return !(v && v[0] == '0');
+}
+
 template <int K, bool BNF>
 static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, const u64* lwe_in, uint32_t n_lwe,
                                     uint32_t step, uint32_t nb, const LargeShape& sh, const u64* tw, const u64* twist,
@@ -319,9 +329,12 @@ static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, cons
     }
   }
   const dim3 grid((unsigned)((((uint64_t)sh.n >> K) + 255) / 256), nb * (sh.k + 1));
-  if (only)
+  if (only && rotdec_lazy())
     hipLaunchKernelGGL((large_rotdec_top<K, BNF, true>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
                        tw, twist);
+  else if (only)  // MI_ROTDEC_LAZY=0 (A/B): canonical stages
+    hipLaunchKernelGGL((large_rotdec_top<K, BNF, true, false>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
+                       sh, tw, twist);
   else
     hipLaunchKernelGGL((large_rotdec_top<K, BNF, false>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
                        tw, twist);
