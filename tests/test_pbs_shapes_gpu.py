@@ -38,9 +38,11 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-@pytest.mark.parametrize("n,k", [(512, 1), (512, 4), (8192, 1)])
+# sb: N = 512, k = 4 level-1 PBS with the MAC's key loads one column at a time (r5 default) and without (MI_SHAPE_SB=0)
+@pytest.mark.parametrize("n,k,sb", [(512, 1, "1"), (512, 4, "1"), (512, 4, "0"), (8192, 1, "1")])
 @pytest.mark.parametrize("bnf", [True, False])
-def test_shape_ext_product_cmux_pbs_random_keys(engine, oracle, n, k, bnf):
+def test_shape_ext_product_cmux_pbs_random_keys(engine, oracle, n, k, sb, bnf, monkeypatch):
+    monkeypatch.setenv("MI_SHAPE_SB", sb)
     q = 0 if bnf else P
     pl = engine.Plan.try_new(n, P)
     c = oracle.NttContext(n)

@@ -66,7 +66,7 @@ struct Shape {
 // pre-normalised unless `normalize`.  L1: the level count is 1 at compile time (the shortint shapes' 1_1 / 2_2),
 // so no decomposition state stays live beside the digits (the register budget of 2 waves per SIMD); else the levels
 // are a runtime loop.
-template <int LOGN, int K, bool BNF, bool L1>
+template <int LOGN, int K, bool BNF, bool L1, bool SB = false>
 __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<LOGN, K>::E],
                                                  u64 (&y)[K + 1][Shape<LOGN, K>::E], const u64* __restrict__ ggsw,
                                                  int base_log, int level, int t, u64* sh,
@@ -139,6 +139,9 @@ __device__ __forceinline__ void ext_product_regs(const u64 (&ct1)[K + 1][Shape<L
 #pragma unroll
         for (int rr = 0; rr <= K; ++rr) acc.mac(x[rr][r], mat[(rr * (K + 1) + c) * N + pos]);
         y[c][r] = L1 ? acc.value(0) : gl.add(y[c][r], acc.value(0));
+        // SB (r5, the N = 512, k = 4 level-1 PBS): one column's key loads at a time, so fewer loaded values are live
+        // at once — 248 VGPRs and no spill instead of 256 + 18 spilled inside the step loop, +4 % PBS/s (session 41)
+        if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -208,7 +211,7 @@ void ext_product_kernel(u64* __restrict__ out, u64* __restrict__ glwe,
 // ---- programmable bootstrap batch (configs 4/5) -----------------------------------------------
 // lwe_in: batch x (n+1); lut: (K+1) x N shared; bsk: n x level x (K+1) x (K+1) x N (BNF: pre-normalised
 // copy); lwe_out: batch x (K N + 1).  Structure = programmable_bootstrap_ntt64[_bnf]_lwe_ciphertext_mem_optimized.
-template <int LOGN, int K, bool BNF, bool L1>
+template <int LOGN, int K, bool BNF, bool L1, bool SB = false>
 __global__ __launch_bounds__((Shape<LOGN, K>::T)) __attribute__((amdgpu_waves_per_eu(shape_waves<LOGN, K, L1, true>())))
 void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
                                                              PbsIo io, const u64* __restrict__ bsk,
@@ -285,7 +288,7 @@ void pbs_kernel(u64* __restrict__ lwe_out, const u64* __restrict__ lwe_in,
         ct1[c][r] = BNF ? v - acc[c][r] : sub_custom(v, acc[c][r]);  // cmux: ct1 - ct0
       }
     __syncthreads();
-    ext_product_regs<LOGN, K, BNF, L1>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, level, t, sh, tw, itw, false, 0);
+    ext_product_regs<LOGN, K, BNF, L1, SB>(ct1, y, bsk + (size_t)i * ggsw_len, base_log, level, t, sh, tw, itw, false, 0);
 #pragma unroll
     for (int c = 0; c <= K; ++c)
 #pragma unroll
@@ -517,6 +520,18 @@ static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* 
                             const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                             const uint64_t* itw, int centered, hipStream_t s) {
   const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN, K>::T);
+  if constexpr (K >= 3) {  // r5: the MAC's key loads one column at a time (MI_SHAPE_SB=0: the r4 schedule, A/B)
+    const char* v = getenv("MI_SHAPE_SB");
+    if (level == 1 && !(v && v[0] == '0')) {
+      if (bnf)
+        hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, true, true, true>), grid, block, 0, s, out, lwe_in, lut, bsk,
+                           (uint32_t)n_lwe, (uint32_t)batch, base_log, level, tw, itw, centered);
+      else
+        hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, false, true, true>), grid, block, 0, s, out, lwe_in, lut, bsk,
+                           (uint32_t)n_lwe, (uint32_t)batch, base_log, level, tw, itw, centered);
+      return hipGetLastError();
+    }
+  }
 #define MI_PBS_K(B, L)                                                                                             \
   hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, B, L>), grid, block, 0, s, out, lwe_in, lut, bsk, (uint32_t)n_lwe, \
                      (uint32_t)batch, base_log, level, tw, itw, centered)
