@@ -83,6 +83,39 @@ int mi_ntt64_mul_assign_normalize_batch(const mi_ntt64_plan *plan, uint64_t *lhs
 int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan *plan, uint64_t *acc, const uint64_t *lhs,
                                   const uint64_t *rhs, size_t batch, size_t stride, void *stream);
 
+/* ---- The Ntt64View layer (tfhe/src/core_crypto/commons/math/ntt/ntt64.rs:81-266), batched -------------------
+ * The per-polynomial helpers every tfhe-rs NTT consumer calls (ntt64_pbs.rs:600-663, ntt64_bnf_pbs.rs:596-681,
+ * lwe_bootstrap_key_conversion.rs:294-365), over `batch` polynomials of the plan's size `stride` u64 apart in both
+ * operands (device pointers, async on `stream`).  Any plan; the Solinas N = 2048 plan runs them as one fused launch
+ * each.  Results equal the reference's bit for bit, including what it leaves in its buffers.
+ *   forward             Ntt64View::forward (:89-95):            ntt = fwd(standard)
+ *   forward_normalized  Ntt64View::forward_normalized (:97-108): ntt = normalize(fwd(standard))
+ *   forward_from_power_of_two_modulus (:201-214): ntt = fwd(switch(standard)), switch x -> ((x >> (64 - w)) p
+ *                       + 2^(w-1)) >> w (modswitch_from_power_of_two_to_ntt_prime, :166-177), w in [1, 64]
+ *   forward_from_decomp (:221-240): ntt = fwd(d), d = x + p (wrapping) where x < 0 as an i64, else x
+ * For these four `ntt` may equal the input buffer (in place) or be disjoint from it.
+ *   add_backward (:110-131): ntt = inv(ntt) (in place, as Plan::inv), standard = wrapping_add_custom_mod(standard,
+ *                       ntt, p) (commons/numeric/unsigned.rs:174-187); standard canonical (< p)
+ *   add_backward_on_power_of_two_modulus (:244-266): ntt = switch(inv(ntt)) with switch v -> (((v << w) | p >> 1) / p)
+ *                       << (64 - w) (modswitch_from_ntt_prime_to_power_of_two, :184-196: an OR, not an add), then
+ *                       standard += ntt (wrapping), w in [1, 64]
+ * For these two `standard` and `ntt` must be disjoint.  A width outside [1, 64] (the reference's shifts overflow there)
+ * or overlapping operands are MI_ERR_INVALID_ARG. */
+int mi_ntt64_forward_batch(const mi_ntt64_plan *plan, uint64_t *ntt, const uint64_t *standard, size_t batch,
+                           size_t stride, void *stream);
+int mi_ntt64_forward_normalized_batch(const mi_ntt64_plan *plan, uint64_t *ntt, const uint64_t *standard, size_t batch,
+                                      size_t stride, void *stream);
+int mi_ntt64_forward_from_power_of_two_modulus_batch(const mi_ntt64_plan *plan, unsigned input_modulus_width,
+                                                     uint64_t *ntt, const uint64_t *standard, size_t batch,
+                                                     size_t stride, void *stream);
+int mi_ntt64_forward_from_decomp_batch(const mi_ntt64_plan *plan, uint64_t *ntt, const uint64_t *decomp, size_t batch,
+                                       size_t stride, void *stream);
+int mi_ntt64_add_backward_batch(const mi_ntt64_plan *plan, uint64_t *standard, uint64_t *ntt, size_t batch,
+                                size_t stride, void *stream);
+int mi_ntt64_add_backward_on_power_of_two_modulus_batch(const mi_ntt64_plan *plan, unsigned output_modulus_width,
+                                                        uint64_t *standard, uint64_t *ntt, size_t batch, size_t stride,
+                                                        void *stream);
+
 /* ---- Host-pointer convenience (copy in, run, copy out, synchronise) ---------------------
  * The single-polynomial `&mut [u64]` form of Plan::fwd / Plan::inv, batched; used by config 1
  * plumbing and the tests.  `buf` holds batch * n contiguous u64 on the host. */
@@ -518,6 +551,15 @@ int mi_lwe_keyswitch32_batch(const mi_lwe_ksk32 *key, uint32_t *lwe_out, const u
  * MI_MS_PRE_SWITCHED input of mi_blind_rotate_ntt64_batch / mi_pbs_ntt64_batch (log_modulus = log2(2N)). */
 int mi_lwe_modulus_switch32_batch(uint64_t *switched, const uint32_t *lwe_in, size_t lwe_dim, size_t batch,
                                   int log_modulus, int ms_mode, int device, void *stream);
+/* The same switch of u64 LWEs (the native 2^64 ciphertexts in front of every other blind rotation):
+ * lwe_ciphertext_modulus_switch / lwe_ciphertext_centered_binary_modulus_switch (algorithms/modulus_switch.rs:14-104)
+ * at Scalar = u64, materialised as the LazyStandardModulusSwitchedLweCiphertext reads them
+ * (entities/modulus_switched_lwe_ciphertext.rs:150-175) — what the HPU mockup runs before blind_rotate_ntt64_bnf_assign
+ * (mockups/tfhe-hpu-mockup/src/lib.rs:725-736).  Both forms: log_modulus in [1, BITS] for MI_MS_STANDARD (identity at
+ * BITS, fft_impl/common.rs:10-23) and [1, BITS - 1] for MI_MS_CENTERED, whose half_case shift (modulus_switch.rs:95)
+ * underflows at BITS in the reference; anything else is MI_ERR_INVALID_ARG.  BITS = 32 for the u32 call above. */
+int mi_lwe_modulus_switch_batch(uint64_t *switched, const uint64_t *lwe_in, size_t lwe_dim, size_t batch,
+                                int log_modulus, int ms_mode, int device, void *stream);
 
 #ifdef __cplusplus
 }

@@ -144,6 +144,45 @@ class Plan {
 // Layouts as in tfhe_ntt_amd.h.  Variants: MI_NTT64_SOLINAS / MI_NTT64_BNF.
 namespace core_crypto {
 
+// Ntt64View (commons/math/ntt/ntt64.rs:80-266): the per-polynomial helpers of every NTT consumer, over `batch`
+// polynomials `stride` u64 apart in both operands (device pointers).  Argument order as the reference's; add_backward*
+// leave `ntt` holding the inverse (switched for the power-of-two form), as Plan::inv in place does.
+class Ntt64View {
+ public:
+  explicit Ntt64View(const prime64::Plan& plan) : plan_(plan.raw()), n_(plan.ntt_size()), p_(plan.modulus()) {}
+  size_t polynomial_size() const noexcept { return n_; }
+  uint64_t custom_modulus() const noexcept { return p_; }
+  void forward(uint64_t* ntt, const uint64_t* standard, size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_forward_batch(plan_, ntt, standard, batch, stride, stream));
+  }
+  void forward_normalized(uint64_t* ntt, const uint64_t* standard, size_t batch, size_t stride,
+                          void* stream = nullptr) const {
+    check(mi_ntt64_forward_normalized_batch(plan_, ntt, standard, batch, stride, stream));
+  }
+  void add_backward(uint64_t* standard, uint64_t* ntt, size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_add_backward_batch(plan_, standard, ntt, batch, stride, stream));
+  }
+  void forward_from_power_of_two_modulus(unsigned input_modulus_width, uint64_t* ntt, const uint64_t* standard,
+                                         size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_forward_from_power_of_two_modulus_batch(plan_, input_modulus_width, ntt, standard, batch, stride,
+                                                           stream));
+  }
+  void forward_from_decomp(uint64_t* ntt, const uint64_t* decomp, size_t batch, size_t stride,
+                           void* stream = nullptr) const {
+    check(mi_ntt64_forward_from_decomp_batch(plan_, ntt, decomp, batch, stride, stream));
+  }
+  void add_backward_on_power_of_two_modulus(unsigned output_modulus_width, uint64_t* standard, uint64_t* ntt,
+                                            size_t batch, size_t stride, void* stream = nullptr) const {
+    check(mi_ntt64_add_backward_on_power_of_two_modulus_batch(plan_, output_modulus_width, standard, ntt, batch,
+                                                              stride, stream));
+  }
+
+ private:
+  const mi_ntt64_plan* plan_;
+  size_t n_;
+  uint64_t p_;
+};
+
 // algorithms/lwe_bootstrap_key_conversion.rs:294-365 (Raw: normalize = false)
 inline void convert_standard_lwe_bootstrap_key_to_ntt64(const prime64::Plan& plan, const uint64_t* bsk_std,
                                                         uint64_t* bsk_ntt, size_t n_polys, unsigned in_modulus_width,
@@ -302,6 +341,14 @@ inline void lwe_ciphertext_modulus_switch32(const uint32_t* lwe_in, uint64_t* sw
                                             void* stream = nullptr) {
   check(mi_lwe_modulus_switch32_batch(switched, lwe_in, lwe_dimension, batch, log_modulus,
                                       centered ? MI_MS_CENTERED : MI_MS_STANDARD, device, stream));
+}
+
+// the same switch of u64 LWEs (the native-modulus ciphertexts in front of every other blind rotation)
+inline void lwe_ciphertext_modulus_switch(const uint64_t* lwe_in, uint64_t* switched, size_t lwe_dimension,
+                                          size_t batch, int log_modulus, bool centered, int device = 0,
+                                          void* stream = nullptr) {
+  check(mi_lwe_modulus_switch_batch(switched, lwe_in, lwe_dimension, batch, log_modulus,
+                                    centered ? MI_MS_CENTERED : MI_MS_STANDARD, device, stream));
 }
 
 // On-disk NTT bootstrap key (entities/ntt_lwe_bootstrap_key.rs:26-33): plain bincode or the versioned

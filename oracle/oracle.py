@@ -233,6 +233,10 @@ _PBS_SIGS["ora_blind_rotate_bnf_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int
                                                 _sz, ctypes.c_int, ctypes.c_int])
 _PBS_SIGS["ora_blind_rotate_solinas_batch"] = (None, [_T, ctypes.c_int, ctypes.c_int, ctypes.c_int, _p64, _p64, _p64,
                                                     _sz, _sz, ctypes.c_int, ctypes.c_int])
+_PBS_SIGS["ora_ntt64_view_forward_batch"] = (None, [_T, ctypes.c_int, ctypes.c_uint, ctypes.c_int, _p64, _p64, _sz,
+                                                   _sz, ctypes.c_int])
+_PBS_SIGS["ora_ntt64_view_add_backward_batch"] = (None, [_T, ctypes.c_uint, _p64, _p64, _sz, _sz, ctypes.c_int])
+_PBS_SIGS["ora_lwe_ms64"] = (None, [_p64, _sz, ctypes.c_uint, ctypes.c_int, _p64])
 _pbs_ready = False
 
 
@@ -350,6 +354,40 @@ class NttContext:
         return dst
 
 
+    # ---- the Ntt64View layer (ntt64.rs:89-266), over a (batch, N) array (new arrays returned) ----
+    def _view_fwd(self, kind, width, normalize, standard, threads):
+        src = _u(standard).reshape(-1, self.n)
+        dst = np.zeros_like(src)
+        _plib().ora_ntt64_view_forward_batch(self.tables, kind, width, int(normalize), _ptr(dst), _ptr(src),
+                                             src.shape[0], self.n, threads)
+        return dst.reshape(np.shape(standard))
+
+    def forward(self, standard, threads=8):
+        return self._view_fwd(0, 0, False, standard, threads)
+
+    def forward_normalized(self, standard, threads=8):
+        return self._view_fwd(0, 0, True, standard, threads)
+
+    def forward_from_power_of_two_modulus(self, input_modulus_width, standard, threads=8):
+        return self._view_fwd(1, input_modulus_width, False, standard, threads)
+
+    def forward_from_decomp(self, decomp, threads=8):
+        return self._view_fwd(2, 0, False, decomp, threads)
+
+    def _view_add(self, width, standard, ntt, threads):
+        st = _u(standard).reshape(-1, self.n).copy()
+        y = _u(ntt).reshape(-1, self.n).copy()
+        _plib().ora_ntt64_view_add_backward_batch(self.tables, width, _ptr(st), _ptr(y), st.shape[0], self.n, threads)
+        return st.reshape(np.shape(standard)), y.reshape(np.shape(ntt))
+
+    def add_backward(self, standard, ntt, threads=8):
+        """-> (standard after the call, ntt after the call)"""
+        return self._view_add(0, standard, ntt, threads)
+
+    def add_backward_on_power_of_two_modulus(self, output_modulus_width, standard, ntt, threads=8):
+        return self._view_add(output_modulus_width, standard, ntt, threads)
+
+
 def pbs_set_fast_ntt(on: bool) -> None:
     """Route the PBS restatement's transforms through the AVX-512 restatement (CPU baseline only)."""
     _plib().ora_pbs_set_fast_ntt(int(on))
@@ -457,6 +495,21 @@ def lwe_keyswitch32(ksk, lwe_in, out_dim, base_log, level, out_mod_log, threads=
     out = np.zeros(x.shape[:-1] + (out_dim + 1,), np.uint32)
     _klib().ora_lwe_keyswitch32_batch(k.ctypes.data, in_dim, out_dim, base_log, level, out_mod_log, _ptr(x),
                                       out.ctypes.data, batch, threads)
+    return out
+
+
+def lwe_ms64(lwe, log_mod, centered):
+    """lwe_ciphertext_[centered_binary_]modulus_switch of u64 LWEs (modulus_switch.rs:14-104) -> u64 values in
+    [0, 2^log_mod), same shape."""
+    x = np.ascontiguousarray(lwe, dtype=np.uint64)
+    dim = x.shape[-1] - 1
+    out = np.zeros(x.shape, np.uint64)
+    flat, oflat = x.reshape(-1, dim + 1), out.reshape(-1, dim + 1)
+    for b in range(flat.shape[0]):
+        row = np.ascontiguousarray(flat[b])
+        orow = np.zeros(dim + 1, np.uint64)
+        _plib().ora_lwe_ms64(_ptr(row), dim, log_mod, 1 if centered else 0, _ptr(orow))
+        oflat[b] = orow
     return out
 
 

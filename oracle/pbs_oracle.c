@@ -405,3 +405,58 @@ void ora_ext_product_bnf_batch(const ora_ntt_tables *t, int k, int base_log, int
     for (b = 0; b < (long long)batch; ++b)
         ora_ext_product_bnf(t, k, base_log, level, out + (size_t)b * len, ggsw, glwe + (size_t)b * len);
 }
+
+/* ---- the Ntt64View layer (commons/math/ntt/ntt64.rs:89-266), one polynomial per call, batched with OpenMP ---- */
+/* u64::wrapping_add_custom_mod (commons/numeric/unsigned.rs:174-187) = self.wrapping_sub_custom_mod(
+ * other.wrapping_neg_custom_mod(m)) with wrapping_neg_custom_mod (:219-225) and wrapping_sub_custom_mod (:181-187) */
+static uint64_t wrapping_add_custom_mod(uint64_t a, uint64_t b, uint64_t m) {
+    const uint64_t nb = b == 0 ? 0 : m - b;
+    return a >= nb ? a - nb : a - nb + m;
+}
+
+/* kind 0 forward (:89-95) / forward_normalized (:97-108, normalize != 0), 1 forward_from_power_of_two_modulus
+ * (:201-214, modswitch_from_power_of_two_to_ntt_prime :166-177), 2 forward_from_decomp (:221-240) */
+void ora_ntt64_view_forward_batch(const ora_ntt_tables *t, int kind, unsigned width, int normalize, uint64_t *ntt,
+                                  const uint64_t *standard, size_t batch, size_t stride, int threads) {
+    const size_t n = t->n;
+#pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(static)
+    for (size_t b = 0; b < batch; ++b) {
+        uint64_t *dst = ntt + b * stride;
+        const uint64_t *src = standard + b * stride;
+        for (size_t j = 0; j < n; ++j) {
+            uint64_t x = src[j]; /* ntt.copy_from_slice(standard) */
+            if (kind == 1) x = ora_modswitch_p2_to_prime(x, width, t->p);
+            else if (kind == 2) x = (int64_t)x < 0 ? x + t->p : x; /* x.wrapping_add(custom_modulus) */
+            dst[j] = x;
+        }
+        ora_fwd(n, t->p, t->twid, dst);
+        if (normalize) ora_normalize(n, t->p, t->n_inv, dst);
+    }
+}
+
+/* width 0: add_backward (:110-131); else add_backward_on_power_of_two_modulus (:244-266) with
+ * modswitch_from_ntt_prime_to_power_of_two (:184-196).  ntt is left as the reference leaves it. */
+void ora_ntt64_view_add_backward_batch(const ora_ntt_tables *t, unsigned width, uint64_t *standard, uint64_t *ntt,
+                                       size_t batch, size_t stride, int threads) {
+    const size_t n = t->n;
+#pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(static)
+    for (size_t b = 0; b < batch; ++b) {
+        uint64_t *y = ntt + b * stride, *out = standard + b * stride;
+        ora_inv(n, t->p, t->inv_twid, y);
+        if (width) {
+            for (size_t j = 0; j < n; ++j) y[j] = ora_modswitch_prime_to_p2(y[j], width, t->p);
+            for (size_t j = 0; j < n; ++j) out[j] += y[j];
+        } else {
+            for (size_t j = 0; j < n; ++j) out[j] = wrapping_add_custom_mod(out[j], y[j], t->p);
+        }
+    }
+}
+
+/* lwe_ciphertext_[centered_binary_]modulus_switch at Scalar = u64 (algorithms/modulus_switch.rs:14-104), read out as
+ * the lazy switched ciphertext does (entities/modulus_switched_lwe_ciphertext.rs:150-172): out[i] = ms(a_i), out[dim]
+ * = ms(b + correction) */
+void ora_lwe_ms64(const uint64_t *lwe, size_t dim, unsigned log_mod, int centered, uint64_t *out) {
+    const uint64_t corr = centered ? ora_centered_ms_body_correction(lwe, dim, log_mod) : 0;
+    for (size_t i = 0; i < dim; ++i) out[i] = ora_modulus_switch(lwe[i], log_mod);
+    out[dim] = ora_modulus_switch(lwe[dim] + corr, log_mod);
+}

@@ -44,6 +44,17 @@ uint64_t ora_decompose_one_level(int base_log, uint64_t *state);
 uint64_t ora_modswitch_p2_to_prime(uint64_t v, unsigned width, uint64_t p);
 uint64_t ora_modswitch_prime_to_p2(uint64_t v, unsigned width, uint64_t p);
 
+/* the Ntt64View layer (ntt64.rs:89-266): kind 0 forward[_normalized], 1 forward_from_power_of_two_modulus(width),
+ * 2 forward_from_decomp; add_backward (width 0) / add_backward_on_power_of_two_modulus(width) */
+void ora_ntt64_view_forward_batch(const ora_ntt_tables *t, int kind, unsigned width, int normalize, uint64_t *ntt,
+                                  const uint64_t *standard, size_t batch, size_t stride, int threads);
+void ora_ntt64_view_add_backward_batch(const ora_ntt_tables *t, unsigned width, uint64_t *standard, uint64_t *ntt,
+                                       size_t batch, size_t stride, int threads);
+/* algorithms/modulus_switch.rs:14-104 at Scalar = u64, materialised (dim mask values, then the body) */
+void ora_lwe_ms64(const uint64_t *lwe, size_t dim, unsigned log_mod, int centered, uint64_t *out);
+uint64_t ora_centered_ms_body_correction(const uint64_t *mask, size_t n_lwe, unsigned log_modulus);
+uint64_t ora_modulus_switch(uint64_t input, unsigned log_modulus);
+
 /* ntt64_bnf_pbs.rs:541-681: out += GGSW (.) glwe  (native modulus) */
 void ora_ext_product_bnf(const ora_ntt_tables *t, int k, int base_log, int level, uint64_t *out,
                          const uint64_t *ggsw, const uint64_t *glwe);

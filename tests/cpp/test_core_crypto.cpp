@@ -6,7 +6,8 @@
 //   programmable_bootstrap_ntt64_lwe_ciphertext    ntt64_bnf_pbs.rs:469-540 (standard modulus switch)
 //   keyswitch_lwe_ciphertext                       lwe_keyswitch.rs:137-227 (2048 -> 918, B 2^4, L 4)
 //   keyswitch_lwe_ciphertext_with_scalar_change    lwe_keyswitch.rs:331-447 (KS32: 2048 -> 879, B 2^2, L 8, 2^21)
-//   lwe_ciphertext_centered_binary_modulus_switch  modulus_switch.rs:35-104 (u32 LWEs)
+//   lwe_ciphertext_centered_binary_modulus_switch  modulus_switch.rs:35-104 (u32 and u64 LWEs)
+//   Ntt64View (all six helpers)                    commons/math/ntt/ntt64.rs:89-266
 // and the f64-FFT mirror (namespace fft64) against exact integer arithmetic within the f64 error bound:
 //   forward_as_torus -> backward_as_torus round trip, add_external_product_assign vs the exact negacyclic product
 // Needs a HIP device.  Build: make -C tests/cpp.
@@ -153,6 +154,47 @@ int main() {
     EXPECT(d_sw.host() == want_sw);
     (void)hipFree(d_ksk);
     (void)hipFree(d_out);
+  }
+
+  // Ntt64View (ntt64.rs:89-266) over a batch of 5: forward_normalized, forward_from_power_of_two_modulus (w = 21),
+  // forward_from_decomp, add_backward, add_backward_on_power_of_two_modulus (w = 64); then the u64 centered switch
+  {
+    const size_t batch = 5;
+    cc::Ntt64View view(*plan);
+    EXPECT(view.polynomial_size() == N && view.custom_modulus() == P);
+    const auto x = uniform(130, P, batch * N), w = uniform(131, 0, batch * N), st = uniform(132, 0, batch * N);
+    std::vector<uint64_t> dg(batch * N);
+    for (size_t i = 0; i < dg.size(); ++i) dg[i] = (uint64_t)((int64_t)(w[i] % (1u << 23)) - (1 << 22));
+    std::vector<uint64_t> want(batch * N);
+    Dev d_x(x), d_w(w), d_dg(dg), d_out(batch * N);
+    ora_ntt64_view_forward_batch(&tabs, 0, 0, 1, want.data(), x.data(), batch, N, 4);
+    view.forward_normalized(d_out.p, d_x.p, batch, N);
+    EXPECT(d_out.host() == want);
+    ora_ntt64_view_forward_batch(&tabs, 1, 21, 0, want.data(), w.data(), batch, N, 4);
+    view.forward_from_power_of_two_modulus(21, d_out.p, d_w.p, batch, N);
+    EXPECT(d_out.host() == want);
+    ora_ntt64_view_forward_batch(&tabs, 2, 0, 0, want.data(), dg.data(), batch, N, 4);
+    view.forward_from_decomp(d_out.p, d_dg.p, batch, N);
+    EXPECT(d_out.host() == want);
+    std::vector<uint64_t> want_st(x), want_y(x);  // add_backward: standard mod p, ntt = x
+    ora_ntt64_view_add_backward_batch(&tabs, 0, want_st.data(), want_y.data(), batch, N, 4);
+    Dev d_st(x), d_y(x);
+    view.add_backward(d_st.p, d_y.p, batch, N);
+    EXPECT(d_st.host() == want_st);
+    EXPECT(d_y.host() == want_y);
+    std::vector<uint64_t> want_st2(st), want_y2(x);
+    ora_ntt64_view_add_backward_batch(&tabs, 64, want_st2.data(), want_y2.data(), batch, N, 4);
+    Dev d_st2(st), d_y2(x);
+    view.add_backward_on_power_of_two_modulus(64, d_st2.p, d_y2.p, batch, N);
+    EXPECT(d_st2.host() == want_st2);
+    EXPECT(d_y2.host() == want_y2);
+    const size_t dim = 918;
+    const auto lwe = uniform(133, 0, batch * (dim + 1));
+    std::vector<uint64_t> want_sw(lwe.size());
+    for (size_t b = 0; b < batch; ++b) ora_lwe_ms64(lwe.data() + b * (dim + 1), dim, 12, 1, want_sw.data() + b * (dim + 1));
+    Dev d_lwe(lwe), d_sw(lwe.size());
+    cc::lwe_ciphertext_modulus_switch(d_lwe.p, d_sw.p, dim, batch, 12, true);
+    EXPECT(d_sw.host() == want_sw);
   }
 
   // errors surface as tfhe_ntt_amd::Error with the C status (base_log * level >= 64)

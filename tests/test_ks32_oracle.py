@@ -99,6 +99,8 @@ def test_ks32_decrypts(oracle, w):
 @pytest.mark.parametrize("log_mod", [12, 1, 31, 32])
 @pytest.mark.parametrize("centered", [False, True])
 def test_ms32_oracle_matches_python_restatement(oracle, log_mod, centered):
+    if centered and log_mod == 32:
+        pytest.skip("outside the reference's domain: its half_case shift underflows at log_modulus = BITS")
     g = H.rng(log_mod * 2 + centered)
     dim = 879
     lwe = g.integers(0, M32, size=(3, dim + 1), dtype=np.uint64).astype(np.uint32)

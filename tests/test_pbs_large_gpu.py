@@ -34,13 +34,11 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-@pytest.mark.parametrize("n,lazy", [(8192, "1"), (8192, "0"), (16384, "1"), (32768, "1"), (65536, "1"), (131072, "1")])
+@pytest.mark.parametrize("n", [8192, 16384, 32768, 65536, 131072])
 @pytest.mark.parametrize("bnf", [True, False])
-def test_large_random_keys(engine, oracle, n, lazy, bnf, monkeypatch):
+def test_large_random_keys(engine, oracle, n, bnf):
     """Every N check_pbs_shape accepts past 8192: 32768 runs the K = 4 cooperative first top pass
-    (large_rotdec_tile), 131072 the two-pass split (large_rotdec_top<3> then the skip-first split) — ADVICE r4.
-    lazy "0": the rotation pass's top stages canonical (MI_ROTDEC_LAZY=0, the r5 A/B form) at 8192."""
-    monkeypatch.setenv("MI_ROTDEC_LAZY", lazy)
+    (large_rotdec_tile), 131072 the two-pass split (large_rotdec_top<3> then the skip-first split) — ADVICE r4."""
     q = 0 if bnf else P
     k = 1
     pl = engine.Plan.try_new(n, P)
@@ -211,33 +209,6 @@ def test_large_pbs_mac_fused_term_counts(engine, oracle, k, level, bnf):
     c = oracle.NttContext(n)
     M = engine.ntt64_pbs
     g = H.rng(900 + 10 * k + level + bnf)
-    bsk = rand_q(g, (n_lwe, level, k + 1, k + 1, n), P)
-    lut = rand_q(g, (k + 1, n), q)
-    lwe = rand_q(g, (batch, n_lwe + 1), q)
-    want = np.stack([c.pbs(lwe[b], lut.reshape(-1), bsk.reshape(-1), k, base_log, level, bnf=bnf)
-                     for b in range(batch)])
-    key = M.NttBootstrapKey(pl, dev(bsk), base_log, level, M.BNF if bnf else M.SOLINAS)
-    o = dev(np.zeros((batch, k * n + 1), np.uint64))
-    (M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized if bnf else
-     M.programmable_bootstrap_ntt64_lwe_ciphertext_mem_optimized)(dev(lwe), o, dev(lut), key)
-    assert np.array_equal(host(o), want)
-
-
-@pytest.mark.parametrize("n,level", [(8192, 2), (16384, 3)])
-@pytest.mark.parametrize("bnf", [True, False])
-def test_large_pbs_wave_specialised(engine, oracle, n, level, bnf, monkeypatch):
-    """The wave-specialised MAC-fused inverse (ntt64_tw.hip ntt_tw_inv_mac_ws_kernel, MI_PBS_WS, r5 A/B option: a
-    producer wave hands each unit's product block to a consumer wave through LDS) at the shortint term counts 4 (3_3's
-    l = 2) and 6 (4_4's l = 3): random-key PBS bit for bit vs the oracle, more units than workgroups (each loops)."""
-    monkeypatch.setenv("MI_PBS_WS", "1")  # one workgroup per CU: 320 units on 256 workgroups, some loop
-    k, n_lwe = 1, 2
-    batch = 40 if n == 8192 else 20
-    base_log = 23 // level
-    q = 0 if bnf else P
-    pl = engine.Plan.try_new(n, P)
-    c = oracle.NttContext(n)
-    M = engine.ntt64_pbs
-    g = H.rng(950 + n + level + bnf)
     bsk = rand_q(g, (n_lwe, level, k + 1, k + 1, n), P)
     lut = rand_q(g, (k + 1, n), q)
     lwe = rand_q(g, (batch, n_lwe + 1), q)

@@ -38,11 +38,10 @@ def rand_q(g, shape, q):
     return g.integers(0, q, size=shape, dtype=np.uint64) if q else H.uniform_u64(g, shape)
 
 
-# sb: N = 512, k = 4 level-1 PBS with the MAC's key loads one column at a time (r5 default) and without (MI_SHAPE_SB=0)
-@pytest.mark.parametrize("n,k,sb", [(512, 1, "1"), (512, 4, "1"), (512, 4, "0"), (8192, 1, "1")])
+# N = 512, k = 4 runs the level-1 PBS whose MAC loads its key one column at a time (the SB schedule, r5)
+@pytest.mark.parametrize("n,k", [(512, 1), (512, 4), (8192, 1)])
 @pytest.mark.parametrize("bnf", [True, False])
-def test_shape_ext_product_cmux_pbs_random_keys(engine, oracle, n, k, sb, bnf, monkeypatch):
-    monkeypatch.setenv("MI_SHAPE_SB", sb)
+def test_shape_ext_product_cmux_pbs_random_keys(engine, oracle, n, k, bnf):
     q = 0 if bnf else P
     pl = engine.Plan.try_new(n, P)
     c = oracle.NttContext(n)

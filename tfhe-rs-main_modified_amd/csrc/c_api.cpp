@@ -409,6 +409,95 @@ int mi_ntt64_mul_accumulate_batch(const mi_ntt64_plan* plan, uint64_t* acc, cons
   return run_pw(2, plan, acc, lhs, rhs, batch, stride, stream);
 }
 
+// ---- the Ntt64View layer (tfhe/src/core_crypto/commons/math/ntt/ntt64.rs:89-266), batched ------------------------
+// The Solinas N = 2048 plan runs the fused twisted bodies (ntt64_view.hip: one launch, conversions at load / store);
+// every other plan an elementwise pass around its own transform.  Two operands of one call are either the same buffer
+// (forward forms only) or disjoint.
+static bool view_overlap(const uint64_t* a, const uint64_t* b, size_t n, size_t batch, size_t stride) {
+  const size_t span = (batch - 1) * stride + n;
+  return a < b + span && b < a + span;
+}
+
+static int run_view_fwd(const mi_ntt64_plan* plan, int kind, unsigned width, bool normalized, uint64_t* ntt,
+                        const uint64_t* standard, size_t batch, size_t stride, void* stream) {
+  int st = check_batch(plan, ntt, batch, stride);
+  if (st != MI_OK || batch == 0) return st;
+  if (!standard) return fail(MI_ERR_INVALID_ARG, "standard buffer is NULL");
+  if (kind == 1 && (width < 1 || width > 64))
+    return fail(MI_ERR_INVALID_ARG, "input_modulus_width must be in [1, 64]");
+  if (ntt != standard && view_overlap(ntt, standard, plan->n, batch, stride))
+    return fail(MI_ERR_INVALID_ARG, "ntt and standard must be the same buffer or disjoint");
+  DeviceGuard g(plan->device);
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSuccess;
+  if (plan->twisted) {
+    e = mi::launch_view_fwd_tw(kind, ntt, standard, batch, stride, width,
+                               normalized ? plan->d_twist_fn : plan->d_twist_f, s);
+  } else {
+    if (kind != 0 || ntt != standard)
+      e = mi::launch_view_pre(kind, ntt, standard, plan->n, batch, stride, width, plan->p, s);
+    if (e == hipSuccess) e = launch_transform(true, plan, ntt, batch, stride, s);
+    if (e == hipSuccess && normalized)
+      e = mi::launch_pointwise(0, plan->goldilocks, plan->mp, ntt, nullptr, nullptr, plan->n, batch, stride,
+                               plan->c_normalize, s);
+  }
+  return e == hipSuccess ? MI_OK : hip_fail(e, "Ntt64View forward launch");
+}
+
+int mi_ntt64_forward_batch(const mi_ntt64_plan* plan, uint64_t* ntt, const uint64_t* standard, size_t batch,
+                           size_t stride, void* stream) {
+  return run_view_fwd(plan, 0, 0, false, ntt, standard, batch, stride, stream);
+}
+
+int mi_ntt64_forward_normalized_batch(const mi_ntt64_plan* plan, uint64_t* ntt, const uint64_t* standard, size_t batch,
+                                      size_t stride, void* stream) {
+  return run_view_fwd(plan, 0, 0, true, ntt, standard, batch, stride, stream);
+}
+
+int mi_ntt64_forward_from_power_of_two_modulus_batch(const mi_ntt64_plan* plan, unsigned input_modulus_width,
+                                                     uint64_t* ntt, const uint64_t* standard, size_t batch,
+                                                     size_t stride, void* stream) {
+  return run_view_fwd(plan, 1, input_modulus_width, false, ntt, standard, batch, stride, stream);
+}
+
+int mi_ntt64_forward_from_decomp_batch(const mi_ntt64_plan* plan, uint64_t* ntt, const uint64_t* decomp, size_t batch,
+                                       size_t stride, void* stream) {
+  return run_view_fwd(plan, 2, 0, false, ntt, decomp, batch, stride, stream);
+}
+
+// width 0: add_backward (custom modulus); else add_backward_on_power_of_two_modulus with that output width
+static int run_view_add(const mi_ntt64_plan* plan, unsigned width, uint64_t* standard, uint64_t* ntt, size_t batch,
+                        size_t stride, void* stream) {
+  int st = check_batch(plan, ntt, batch, stride);
+  if (st != MI_OK || batch == 0) return st;
+  if (!standard) return fail(MI_ERR_INVALID_ARG, "standard buffer is NULL");
+  if (view_overlap(ntt, standard, plan->n, batch, stride))
+    return fail(MI_ERR_INVALID_ARG, "standard and ntt must be disjoint");
+  DeviceGuard g(plan->device);
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (plan->twisted && (width == 0 || width == 64)) {
+    e = mi::launch_view_inv_tw(width == 64, standard, ntt, batch, stride, plan->d_twist_i, s);
+  } else {
+    e = launch_transform(false, plan, ntt, batch, stride, s);
+    if (e == hipSuccess) e = mi::launch_view_post(standard, ntt, plan->n, batch, stride, width, plan->p, s);
+  }
+  return e == hipSuccess ? MI_OK : hip_fail(e, "Ntt64View add_backward launch");
+}
+
+int mi_ntt64_add_backward_batch(const mi_ntt64_plan* plan, uint64_t* standard, uint64_t* ntt, size_t batch,
+                                size_t stride, void* stream) {
+  return run_view_add(plan, 0, standard, ntt, batch, stride, stream);
+}
+
+int mi_ntt64_add_backward_on_power_of_two_modulus_batch(const mi_ntt64_plan* plan, unsigned output_modulus_width,
+                                                        uint64_t* standard, uint64_t* ntt, size_t batch, size_t stride,
+                                                        void* stream) {
+  if (output_modulus_width < 1 || output_modulus_width > 64)
+    return fail(MI_ERR_INVALID_ARG, "output_modulus_width must be in [1, 64]");
+  return run_view_add(plan, output_modulus_width, standard, ntt, batch, stride, stream);
+}
+
 // The `&mut [u64]` host form (Plan::fwd / Plan::inv on a caller slice, as Ntt64View::forward / add_backward call
 // it per polynomial, ntt64.rs:89-137).  Each call borrows a staging slot of the plan's device from a process-wide
 // pool: a private non-blocking stream of the highest priority, a device buffer and a mapped, coherent pinned host buffer, all grown on
@@ -1366,18 +1455,42 @@ int mi_lwe_keyswitch32_batch(const mi_lwe_ksk32* key, uint32_t* lwe_out, const u
   return e == hipSuccess ? MI_OK : hip_fail(e, "keyswitch launch");
 }
 
-int mi_lwe_modulus_switch32_batch(uint64_t* switched, const uint32_t* lwe_in, size_t lwe_dim, size_t batch,
-                                  int log_modulus, int ms_mode, int device, void* stream) {
-  if (batch == 0) return MI_OK;
+// shared checks of the two LWE modulus switches: the standard switch is defined for 1 <= log_modulus <= BITS (identity at
+// BITS, fft_impl/common.rs:10-23); the centered one computes 1 << (BITS - log_modulus - 1) (modulus_switch.rs:95), so
+// it needs log_modulus < BITS (the reference's shift underflows there)
+static int check_lwe_ms(const void* switched, const void* lwe_in, size_t lwe_dim, size_t batch, int log_modulus,
+                        int ms_mode, int bits) {
   if (!switched || !lwe_in) return fail(MI_ERR_INVALID_ARG, "buffer is NULL");
   if (lwe_dim == 0 || lwe_dim > 0xFFFFFFull || batch > 0xFFFFFFFFull)
     return fail(MI_ERR_INVALID_ARG, "lwe dimension or batch out of range");
-  if (log_modulus < 1 || log_modulus > 32) return fail(MI_ERR_INVALID_ARG, "log_modulus must be in [1, 32]");
   if (ms_mode != MI_MS_STANDARD && ms_mode != MI_MS_CENTERED)
     return fail(MI_ERR_INVALID_ARG, "ms_mode must be MI_MS_STANDARD or MI_MS_CENTERED");
+  const int top = ms_mode == MI_MS_CENTERED ? bits - 1 : bits;
+  if (log_modulus < 1 || log_modulus > top)
+    return fail(MI_ERR_INVALID_ARG, "log_modulus must be in [1, " + std::to_string(top) + "] for this ms_mode");
+  return MI_OK;
+}
+
+int mi_lwe_modulus_switch32_batch(uint64_t* switched, const uint32_t* lwe_in, size_t lwe_dim, size_t batch,
+                                  int log_modulus, int ms_mode, int device, void* stream) {
+  if (batch == 0) return MI_OK;
+  int st = check_lwe_ms(switched, lwe_in, lwe_dim, batch, log_modulus, ms_mode, 32);
+  if (st != MI_OK) return st;
   DeviceGuard g(device);
   if (!g.ok) return fail(MI_ERR_INVALID_ARG, "bad device");
   hipError_t e = mi::launch_lwe_ms32(switched, lwe_in, lwe_dim, batch, log_modulus, ms_mode == MI_MS_CENTERED,
+                                     (hipStream_t)stream);
+  return e == hipSuccess ? MI_OK : hip_fail(e, "modulus switch launch");
+}
+
+int mi_lwe_modulus_switch_batch(uint64_t* switched, const uint64_t* lwe_in, size_t lwe_dim, size_t batch,
+                                int log_modulus, int ms_mode, int device, void* stream) {
+  if (batch == 0) return MI_OK;
+  int st = check_lwe_ms(switched, lwe_in, lwe_dim, batch, log_modulus, ms_mode, 64);
+  if (st != MI_OK) return st;
+  DeviceGuard g(device);
+  if (!g.ok) return fail(MI_ERR_INVALID_ARG, "bad device");
+  hipError_t e = mi::launch_lwe_ms64(switched, lwe_in, lwe_dim, batch, log_modulus, ms_mode == MI_MS_CENTERED,
                                      (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, "modulus switch launch");
 }

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ntt64_launch.hpp"
 #include "keyswitch_launch.hpp"
 
@@ -341,50 +343,63 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   }
 }
 
-// ---- the modulus switch of a u32 LWE (the KS32 bootstrap's input, mockups/tfhe-hpu-mockup/src/lib.rs:720-736) ----
-// modulus_switch (fft_impl/common.rs:10-23) at Scalar = u32
-__device__ __forceinline__ uint32_t ms32(uint32_t x, uint32_t log_mod) {
-  return log_mod >= 32 ? x : (uint32_t)(x + (1u << (32u - log_mod - 1u))) >> (32u - log_mod);
+// ---- the modulus switch of an LWE (lwe_ciphertext_modulus_switch / lwe_ciphertext_centered_binary_modulus_switch,
+// algorithms/modulus_switch.rs:14-104): u32 words for the KS32 bootstrap's input (mockups/tfhe-hpu-mockup/src/lib.rs:
+// 720-736), u64 words for the native-modulus ciphertexts of every other PBS ----
+// modulus_switch (fft_impl/common.rs:10-23) at Scalar = T: identity at log_mod == BITS
+template <typename T>
+__device__ __forceinline__ T ms_word(T x, uint32_t log_mod) {
+  constexpr uint32_t BITS = 8 * sizeof(T);
+  return log_mod >= BITS ? x : (T)(x + ((T)1 << (BITS - log_mod - 1u))) >> (BITS - log_mod);
 }
 
 // One wave per ciphertext: the switched mask (LazyStandardModulusSwitchedLweCiphertext::mask,
 // modulus_switched_lwe_ciphertext.rs:164-172) and, when `centered`, the body correction of
-// lwe_ciphertext_centered_binary_modulus_switch (modulus_switch.rs:35-104) at Scalar = u32 / Signed = i32: the wrapping
-// u32 sum of the halved rounding errors and the exact sum of the halving errors are order-free, so the lanes' partial
+// lwe_ciphertext_centered_binary_modulus_switch (modulus_switch.rs:56-102) at Scalar = T / Signed: the wrapping
+// sum of the halved rounding errors and the exact sum of the halving errors are order-free, so the lanes' partial
 // sums combine by a butterfly reduction; then body = modulus_switch(b + correction) (:150-162).  out: (dim + 1) u64 per
-// ciphertext, every value in [0, 2^log_mod) (the blind rotation's MI_MS_PRE_SWITCHED input).
-__global__ __launch_bounds__(256) void lwe_ms32_kernel(u64* __restrict__ out, const uint32_t* __restrict__ in,
-                                                       uint32_t dim, uint32_t batch, uint32_t log_mod, int centered) {
+// ciphertext, every value in [0, 2^log_mod) (the blind rotation's MI_MS_PRE_SWITCHED input).  The centered form is
+// called with log_mod < BITS only (the reference's half_case shift underflows at BITS).  The halving errors are each
+// in {-1, 0, 1}, so their sum fits an int32 for any dimension the callers accept (< 2^24).
+template <typename T>
+__global__ __launch_bounds__(256) void lwe_ms_kernel(u64* __restrict__ out, const T* __restrict__ in, uint32_t dim,
+                                                     uint32_t batch, uint32_t log_mod, int centered) {
+  using S = typename std::conditional<sizeof(T) == 4, int32_t, int64_t>::type;
+  constexpr uint32_t BITS = 8 * sizeof(T);
   const uint32_t lane = threadIdx.x & 63, item = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (item >= batch) return;
-  const uint32_t* x = in + (uint64_t)item * (dim + 1);
+  const T* x = in + (uint64_t)item * (dim + 1);
   u64* y = out + (uint64_t)item * (dim + 1);
-  uint32_t sum_half = 0;
+  T sum_half = 0;
   int32_t sum_hed = 0;
   for (uint32_t i = lane; i < dim; i += 64) {
-    const uint32_t a = x[i], sw = ms32(a, log_mod);
+    const T a = x[i], sw = ms_word<T>(a, log_mod);
     y[i] = sw;
     if (centered) {
-      const uint32_t round = log_mod >= 32 ? sw : sw << (32u - log_mod);
-      const int32_t err = (int32_t)(round - a), half = err / 2;  // i32 division truncates toward zero, as Rust's
-      sum_half += (uint32_t)half;
-      sum_hed += 2 * half - err;
+      const T round = log_mod >= BITS ? sw : (T)(sw << (BITS - log_mod));
+      const S err = (S)(T)(round - a), half = err / 2;  // signed division truncates toward zero, as Rust's
+      sum_half += (T)half;
+      sum_hed += (int32_t)(2 * half - err);
     }
   }
   if (centered) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-      sum_half += (uint32_t)__shfl_xor((int)sum_half, off, 64);
+      if constexpr (sizeof(T) == 4) {
+        sum_half += (T)__shfl_xor((int)sum_half, off, 64);
+      } else {
+        sum_half += (T)__shfl_xor((long long)sum_half, off, 64);
+      }
       sum_hed += __shfl_xor(sum_hed, off, 64);
     }
   }
   if (lane == 0) {
-    uint32_t corr = 0;
+    T corr = 0;
     if (centered) {
-      const uint32_t half_case = log_mod >= 32 ? 0u : 1u << (32u - log_mod - 1u);
-      corr = (sum_half - (uint32_t)(sum_hed / 2)) - half_case;
+      const T half_case = (T)1 << (BITS - log_mod - 1u);
+      corr = (T)(sum_half - (T)(S)(sum_hed / 2)) - half_case;
     }
-    y[dim] = ms32(x[dim] + corr, log_mod);
+    y[dim] = ms_word<T>((T)(x[dim] + corr), log_mod);
   }
 }
 
@@ -439,8 +454,17 @@ hipError_t launch_lwe_ms32(uint64_t* out, const uint32_t* in, size_t dim, size_t
                            hipStream_t st) {
   if (batch == 0) return hipSuccess;
   const unsigned grid = (unsigned)((batch + 3) / 4);
-  hipLaunchKernelGGL(ks::lwe_ms32_kernel, dim3(grid), dim3(256), 0, st, out, in, (uint32_t)dim, (uint32_t)batch,
-                     (uint32_t)log_mod, centered ? 1 : 0);
+  hipLaunchKernelGGL(ks::lwe_ms_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, out, in, (uint32_t)dim,
+                     (uint32_t)batch, (uint32_t)log_mod, centered ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_lwe_ms64(uint64_t* out, const uint64_t* in, size_t dim, size_t batch, int log_mod, bool centered,
+                           hipStream_t st) {
+  if (batch == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((batch + 3) / 4);
+  hipLaunchKernelGGL(ks::lwe_ms_kernel<uint64_t>, dim3(grid), dim3(256), 0, st, out, in, (uint32_t)dim,
+                     (uint32_t)batch, (uint32_t)log_mod, centered ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -24,5 +24,8 @@ hipError_t launch_keyswitch32(uint32_t* out, const uint64_t* lwe_in, const void*
 // the (centered binary) modulus switch of u32 LWEs of dimension dim to [0, 2^log_mod): (dim + 1) u64 per ciphertext
 hipError_t launch_lwe_ms32(uint64_t* out, const uint32_t* in, size_t dim, size_t batch, int log_mod, bool centered,
                            hipStream_t st);
+// the same for u64 LWEs (the native-modulus ciphertexts): (dim + 1) u64 per ciphertext in [0, 2^log_mod)
+hipError_t launch_lwe_ms64(uint64_t* out, const uint64_t* in, size_t dim, size_t batch, int log_mod, bool centered,
+                           hipStream_t st);
 
 }  // namespace mi

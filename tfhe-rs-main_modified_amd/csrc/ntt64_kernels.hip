@@ -165,32 +165,9 @@ __global__ __launch_bounds__(256) void ntt_top_kernel(IO* __restrict__ data, uin
   for (int i = 0; i < R; ++i) src[i * cols] = (IO)x[i];
 }
 
-// the generated inverse K = 5 blocks by wave index (tools/gen_tile_asm.py -> ntt64_tile_asm.hpp)
-template <int W>
-__device__ __forceinline__ void tile5_inv_tw_b(u64 (&x)[8], const u64 (&tw)[8]) {
-  if constexpr (W == 0) tile_asm::k5_inv_tw_b_w0(x, tw);
-  else if constexpr (W == 1) tile_asm::k5_inv_tw_b_w1(x, tw);
-  else if constexpr (W == 2) tile_asm::k5_inv_tw_b_w2(x, tw);
-  else tile_asm::k5_inv_tw_b_w3(x, tw);
-}
-template <int W>
-__device__ __forceinline__ void tile5_inv_b(u64 (&x)[8]) {
-  if constexpr (W == 0) tile_asm::k5_inv_b_w0(x);
-  else if constexpr (W == 1) tile_asm::k5_inv_b_w1(x);
-  else if constexpr (W == 2) tile_asm::k5_inv_b_w2(x);
-  else tile_asm::k5_inv_b_w3(x);
-}
-template <int W>
-__device__ __forceinline__ void tile5_inv_a(u64 (&x)[8]) {
-  if constexpr (W == 0) tile_asm::k5_inv_a_w0(x);
-  else if constexpr (W == 1) tile_asm::k5_inv_a_w1(x);
-  else if constexpr (W == 2) tile_asm::k5_inv_a_w2(x);
-  else tile_asm::k5_inv_a_w3(x);
-}
-
 // The stage-0 pass of the split transform at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): the same function as
 // ntt_top_kernel<K, FWD, Goldilocks, u64, TWIST, ACC, true> at s0 = 0.  Grid: x = column tiles of 64, y = polynomials.
-template <int K, bool FWD, int TWIST, int ACC, int W, int ASM = 1>
+template <int K, bool FWD, int TWIST, int ACC, int W>
 __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t cols, uint64_t col, uint32_t c,
                                               const u64* __restrict__ twist, u64* __restrict__ accp, u64* lds) {
   using Rw = tile::Rows<K>;
@@ -208,36 +185,14 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
       poly[e] = TWIST == 1 ? Goldilocks::mul(x[k], twist[e]) : Goldilocks::canon(x[k]);  // lazy stages
     }
   } else {
-    if constexpr (K == 5 && TWIST == 2 && ASM == 2) {  // r5: the compiled untwist on load, the stages as generated asm
 #pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const uint64_t e = Rw::b(W, k) * cols + col;
-        x[k] = Goldilocks::mul(poly[e], twist[e]);
-      }
-      tile5_inv_b<W>(x);
-      tile::exchange<K, W, false>(x, lds, c);
-      tile5_inv_a<W>(x);
-    } else if constexpr (K == 5 && TWIST == 2 && ASM == 1) {  // r5: untwist + stages as generated asm (gen_tile_asm.py)
-      u64 tw[RPT];
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const uint64_t e = Rw::b(W, k) * cols + col;
-        x[k] = poly[e];
-        tw[k] = twist[e];
-      }
-      tile5_inv_tw_b<W>(x, tw);
-      tile::exchange<K, W, false>(x, lds, c);
-      tile5_inv_a<W>(x);
-    } else {
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const uint64_t e = Rw::b(W, k) * cols + col;
-        x[k] = TWIST == 2 ? Goldilocks::mul(poly[e], twist[e]) : poly[e];
-      }
-      tile::phase_b<K, false, W>(x);
-      tile::exchange<K, W, false>(x, lds, c);
-      tile::phase_a<K, false, W>(x);
+    for (int k = 0; k < RPT; ++k) {
+      const uint64_t e = Rw::b(W, k) * cols + col;
+      x[k] = TWIST == 2 ? Goldilocks::mul(poly[e], twist[e]) : poly[e];
     }
+    tile::phase_b<K, false, W>(x);
+    tile::exchange<K, W, false>(x, lds, c);
+    tile::phase_a<K, false, W>(x);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint64_t e = Rw::a(W, k) * cols + col;
@@ -248,7 +203,7 @@ __device__ __forceinline__ void top_tile_body(u64* __restrict__ poly, uint64_t c
   }
 }
 
-template <int K, bool FWD, int TWIST, int ACC, int ASM = 1>
+template <int K, bool FWD, int TWIST, int ACC>
 __global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ data, uint64_t stride, uint32_t logn,
                                                            const u64* __restrict__ twist, u64* __restrict__ acc) {
   __shared__ u64 lds[(1 << K) * 64];
@@ -258,10 +213,10 @@ __global__ __launch_bounds__(256) void ntt_top_tile_kernel(u64* __restrict__ dat
   u64* poly = data + (uint64_t)blockIdx.y * stride;
   u64* accp = ACC ? acc + (uint64_t)blockIdx.y * stride : nullptr;
   switch (w) {
-    case 0: top_tile_body<K, FWD, TWIST, ACC, 0, ASM>(poly, cols, col, c, twist, accp, lds); break;
-    case 1: top_tile_body<K, FWD, TWIST, ACC, 1, ASM>(poly, cols, col, c, twist, accp, lds); break;
-    case 2: top_tile_body<K, FWD, TWIST, ACC, 2, ASM>(poly, cols, col, c, twist, accp, lds); break;
-    default: top_tile_body<K, FWD, TWIST, ACC, 3, ASM>(poly, cols, col, c, twist, accp, lds); break;
+    case 0: top_tile_body<K, FWD, TWIST, ACC, 0>(poly, cols, col, c, twist, accp, lds); break;
+    case 1: top_tile_body<K, FWD, TWIST, ACC, 1>(poly, cols, col, c, twist, accp, lds); break;
+    case 2: top_tile_body<K, FWD, TWIST, ACC, 2>(poly, cols, col, c, twist, accp, lds); break;
+    default: top_tile_body<K, FWD, TWIST, ACC, 3>(poly, cols, col, c, twist, accp, lds); break;
   }
 }
 
@@ -374,15 +329,10 @@ static hipError_t launch_top_tw(u64* data, size_t batch, size_t stride, int logn
   if constexpr (K >= 4) {
     if (s0 == 0 && logn >= K + 6) {
       const dim3 tgrid((unsigned)(((uint64_t)1 << (logn - K)) / 64), (unsigned)batch);
-      if (tile_asm_enabled(2))
-        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 1>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
-                           (uint32_t)logn, twist, acc);
-      else if (tile_asm_enabled(4))
-        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 2>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
-                           (uint32_t)logn, twist, acc);
-      else  // the compiled stages
-        hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC, 0>), tgrid, dim3(256), 0, s, data,
-                           (uint64_t)stride, (uint32_t)logn, twist, acc);
+      // the compiled stages: the inverse's K = 5 untwist + stages as generated asm measured slower (r5, a block that
+      // waits for all its row loads loses the overlap the compiled code keeps)
+      hipLaunchKernelGGL((ntt_top_tile_kernel<K, FWD, TWIST, ACC>), tgrid, dim3(256), 0, s, data, (uint64_t)stride,
+                         (uint32_t)logn, twist, acc);
       return hipGetLastError();
     }
   }
@@ -408,17 +358,8 @@ static hipError_t top_tw(int kk, u64* data, size_t batch, size_t stride, int log
   }
 }
 
-bool tile_asm_enabled(int which) {
-  static const int mask = [] {
-    const char* v = getenv("MI_TILE_ASM");
-    return v ? atoi(v) : 1;  // bit 1 measured slower (its loads must land before the block: session 19)
-  }();
-  return (mask & which) != 0;
-}
-
 hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t stride, const u64* tw,
-                            const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first,
-                            size_t wave_cap) {
+                            const SplitTw& st, hipStream_t s, u64* acc, int acc_mode, bool skip_first) {
   if (acc && fwd) return hipErrorInvalidValue;  // acc: inverse only
   const int t = logn - 11;
   if (t < 1 || t > 10) return hipErrorInvalidValue;
@@ -426,7 +367,7 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
   // t <= 3, the whole transform, no accumulation: top stages and bodies in one launch, one workgroup per polynomial.
   // Not inside the blind rotation (skip_first / acc): at its batch (one or two generations of workgroups) the fused
   // form's memory phase and body phase do not overlap across workgroups and measured slower.
-  if (t <= 3 && !skip_first && !acc && split_fused_enabled())
+  if (t <= 3 && !skip_first && !acc)
     return launch_ntt_split_fused(fwd, t, data, batch, stride, fwd ? st.blk_fwd : st.blk_inv,
                                   fwd ? st.body_fwd : st.body_inv, s);
   // the top passes put polynomials on grid.y (<= 65535 per launch); passes of <= 5 stages, balanced
@@ -462,8 +403,8 @@ hipError_t launch_ntt_split(bool fwd, int logn, u64* data, size_t batch, size_t 
     return hipSuccess;
   };
   hipError_t e = fwd ? all_tops()
-                     : (skip_first ? hipSuccess : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t, wave_cap));
-  if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t, wave_cap) : all_tops();
+                     : (skip_first ? hipSuccess : launch_ntt_tw(false, data, batch, stride, st.body_inv, s, t));
+  if (e == hipSuccess) e = fwd ? launch_ntt_tw(true, data, batch, stride, st.body_fwd, s, t) : all_tops();
   return e;
 }
 

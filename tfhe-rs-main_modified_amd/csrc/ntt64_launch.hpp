@@ -29,16 +29,29 @@ hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, con
 // key conversion of native-modulus polynomials (N = 2048 Solinas plan): dst = fwd(modswitch_{2^64 -> p}(src))
 hipError_t launch_ntt_tw_ms64(uint64_t* dst, const uint64_t* src, size_t n_polys, const uint64_t* twist,
                               hipStream_t s);
-// wave_cap > 0 (sub_log > 0, the blind rotation's launches): at most wave_cap waves, each looping over units
+// The Ntt64View layer (ntt64_view.hip, ntt64.rs:89-266).  Generic passes for any plan: view_pre writes
+// ntt = conv(standard) (kind 0 copy, 1 switch 2^width -> p, 2 negative decomposition digits + p) ahead of the plan's
+// forward; view_post follows its inverse (width > 0: ntt = switch p -> 2^width, standard += ntt wrapping; width 0:
+// standard = wrapping_add_custom_mod(standard, ntt, p)).  The fused twisted N = 2048 forms: view_fwd_tw (same kinds,
+// any width for kind 1; twist = the forward table or its N^-1 copy) and view_inv_tw (pow2_64: the width-64 switch;
+// else the custom-modulus add).
+hipError_t launch_view_pre(int kind, uint64_t* ntt, const uint64_t* standard, size_t n, size_t batch, size_t stride,
+                           unsigned width, uint64_t p, hipStream_t s);
+hipError_t launch_view_post(uint64_t* standard, uint64_t* ntt, size_t n, size_t batch, size_t stride, unsigned width,
+                            uint64_t p, hipStream_t s);
+hipError_t launch_view_fwd_tw(int kind, uint64_t* ntt, const uint64_t* standard, size_t batch, size_t stride,
+                              unsigned width, const uint64_t* twist, hipStream_t s);
+hipError_t launch_view_inv_tw(bool pow2_64, uint64_t* standard, uint64_t* ntt, size_t batch, size_t stride,
+                              const uint64_t* twist, hipStream_t s);
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist,
-                         hipStream_t s, int sub_log = 0, size_t wave_cap = 0);
+                         hipStream_t s, int sub_log = 0);
 // The MAC-fused inverse bodies of the large-N blind rotation (ntt64_tw.hip): for n_items ciphertexts, every 2048-block
 // of the k + 1 products y[b][c] = sum_{li, r} digits[b][li][r] . ggsw[li][r][c] (NTT domain, the step's GGSW with any
 // normalisation folded in) formed on load and run through the inverse body (the split inverse's first phase);
 // twist = the 2048 plan's inverse body table (SplitTw body_inv).  l (k + 1) in {2, 3, 4, 6, 8} (inv_mac_supported).
 bool inv_mac_supported(int level, int kp1);
 hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
-                                 int level, int logn, const uint64_t* twist, hipStream_t s, size_t wave_cap = 0);
+                                 int level, int logn, const uint64_t* twist, hipStream_t s);
 
 // The split transform of a Solinas plan with 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN = 2^20 (ntt64_kernels.hip; GPU parity:
 // tests/test_ntt_gpu.py test_fwd_inv_all_sizes_solinas 2^12 .. 2^18, test_fwd_inv_beyond_2_18 2^19 / 2^20 — the
@@ -61,14 +74,9 @@ struct SplitTw {
 // twist (SplitTw blk_fwd / blk_inv), body_tab = the 2048 body's table (body_fwd / body_inv)
 hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch, size_t stride, const uint64_t* blk,
                                   const uint64_t* body_tab, hipStream_t s);
-bool split_fused_enabled();  // MI_SPLIT_FUSED=0 in the environment: the two-launch form (A/B)
-// MI_TILE_ASM=<mask> in the environment (A/B, r5; default 1): bit 0 the rotation pass's forward K = 5 tile asm, bit 1
-// the accumulating inverse K = 5 top tile asm (untwist + stages), bit 2 its stages only (the untwist compiled); cleared
-// bits run the compiled stages
-bool tile_asm_enabled(int which);
 hipError_t launch_ntt_split(bool fwd, int logn, uint64_t* data, size_t batch, size_t stride, const uint64_t* tw,
                             const SplitTw& st, hipStream_t s, uint64_t* acc = nullptr, int acc_mode = 0,
-                            bool skip_first = false, size_t wave_cap = 0);
+                            bool skip_first = false);
 // how launch_ntt_split cuts the t = log2 N - 11 top stages into passes: the first pass's stage count (the forward's
 // first pass, s0 = 0) and whether it is the only one (then it carries the block twist)
 inline void split_first_pass(int logn, int* k0, bool* only) {

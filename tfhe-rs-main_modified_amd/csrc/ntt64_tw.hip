@@ -51,9 +51,7 @@ constexpr uint32_t tw_waves() { return FWD ? 1u : 4u; }
 
 // sub_log > 0 (the split transform of N = 2^(11 + sub_log), ntt64_kernels.hip launch_ntt_split): unit `poly` is block
 // poly & (2^sub_log - 1) of polynomial poly >> sub_log, 2048 contiguous coefficients at that block's offset
-// PERSIST (the blind rotation's capped launches, r5): the grid holds fewer waves than units and each wave loops over
-// units poly, poly + grid waves, ... (launch_ntt_tw wave_cap)
-template <bool FWD, bool PERSIST = false>
+template <bool FWD>
 __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* __restrict__ data, uint32_t batch,
                                                                           uint64_t stride,
                                                                           const u64* __restrict__ twist,
@@ -62,14 +60,10 @@ __global__ __launch_bounds__(64 * tw_waves<FWD>()) void ntt_tw_body_kernel(u64* 
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = W == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint32_t poly = blockIdx.x * W + wv; poly < batch; poly += gridDim.x * W) {
-    u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
-    tw_body<FWD>(p, twist, (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2), lane);
-    if constexpr (!PERSIST) break;
-    // the body's stores drain before the next unit: its own vmcnt waits count only the loads it issues (loads and
-    // stores share vmcnt here and need not complete in order)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  const uint32_t poly = blockIdx.x * W + wv;
+  if (poly >= batch) return;
+  u64* p = data + (uint64_t)(poly >> sub_log) * stride + (uint64_t)(poly & ((1u << sub_log) - 1)) * 2048;
+  tw_body<FWD>(p, twist, (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2), lane);
 }
 
 // ---- the split transform of N = 2^(11 + T), T <= 3, in one launch ------------------------------------------------
@@ -225,62 +219,12 @@ template <int L>
 __global__ __launch_bounds__(256) void ntt_tw_inv_mac_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
                                                              const u64* __restrict__ ggsw, uint32_t units,
                                                              uint32_t n_items, uint32_t sub_log, uint32_t kp1,
-                                                             const u64* __restrict__ twist, uint32_t stagger) {
+                                                             const u64* __restrict__ twist) {
   constexpr uint32_t W = 4;
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // MI_PBS_STAGGER (A/B, r5, with a capped looping grid): every other round of 256 workgroups starts later, so the
-  // waves sharing a CU run the MAC's memory phase and the inverse's issue-bound phase at different times
-  if (stagger && ((blockIdx.x >> 8) & 1))
-    for (uint32_t i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  for (uint32_t u = blockIdx.x * W + wv; u < units; u += gridDim.x * W) {
-    inv_mac_unit<L>(y, digits, ggsw, u, n_items, sub_log, kp1, twist, lds + wv * WAVE_LDS2, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // as ntt_tw_body_kernel<PERSIST>
-  }
-}
-
-// The wave-specialised form (r5, MI_PBS_WS; tools/gen_tw_kernel.py gen_macp / gen_invc): two-wave workgroups loop
-// over the units u = blockIdx.x, + gridDim.x, ...; wave 0 forms unit u's block of y row by row into the workgroup's
-// LDS hand-off buffer while wave 1 runs the inverse of the unit before (its transposes in a second LDS region), so each
-// SIMD overlaps the MAC's loads with the inverse's arithmetic.  Both waves run the same trip count and two s_barriers
-// per unit (inside the bodies), so the workgroup cannot deadlock; the consumer waits for its previous stores first.
-template <int L>
-__global__ __launch_bounds__(128) void ntt_tw_inv_mac_ws_kernel(u64* __restrict__ y, const u64* __restrict__ digits,
-                                                                const u64* __restrict__ ggsw, uint32_t units,
-                                                                uint32_t n_items, uint32_t sub_log, uint32_t kp1,
-                                                                const u64* __restrict__ twist) {
-  __shared__ u64 lds[2048 + WAVE_LDS2];  // one block of y, then the consumer's transposes
-  const uint32_t lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t yw = (uint32_t)(uintptr_t)lds + lane * 8, l8 = lane * 8, S = (uint32_t)(uintptr_t)(lds + 2048);
-  const uint64_t n = (uint64_t)2048 << sub_log;
-  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const uint32_t c = u % kp1, ib = u / kp1, b = ib % n_items, blk = ib / n_items;
-    if (wv == 0) {
-      const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
-      const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
-      const uint32_t dlo = (uint32_t)(uintptr_t)d, dhi = (uint32_t)((uintptr_t)d >> 32);
-      const uint32_t gglo = (uint32_t)(uintptr_t)g, gghi = (uint32_t)((uintptr_t)g >> 32);
-      const uint32_t dstep = (uint32_t)(n * 8), gstep = (uint32_t)(kp1 * n * 8);
-#define MI_MACP_OPS                                                                                              \
-  [d_lo] "s"(dlo), [d_hi] "s"(dhi), [dstep] "s"(dstep), [gg_lo] "s"(gglo), [gg_hi] "s"(gghi), [gstep] "s"(gstep), \
-      [l8] "v"(l8), [yw] "v"(yw)
-      if constexpr (L == 4) MI_TW_BODY_MACP4(MI_MACP_OPS);
-      else MI_TW_BODY_MACP6(MI_MACP_OPS);
-#undef MI_MACP_OPS
-    } else {
-      u64* p = y + ((uint64_t)b * kp1 + c) * n + (uint64_t)blk * 2048;
-      const uint32_t par = lane & 1, i = lane >> 1;
-      const uint32_t lwo = par * 128;
-      const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
-      const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
-      const u64* lw = twist + 2 * (2048 + 32);  // the last-DIT-stage table (tw_body<false>)
-      const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
-      const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
-      const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
-      MI_TW_BODY_INVC([g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw),
-                      [l8] "v"(l8), [t4w] "v"(t4w), [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo), [yw] "v"(yw));
-    }
-  }
+  const uint32_t u = blockIdx.x * W + wv;
+  if (u < units) inv_mac_unit<L>(y, digits, ggsw, u, n_items, sub_log, kp1, twist, lds + wv * WAVE_LDS2, lane);
 }
 
 }  // namespace tw
@@ -306,14 +250,6 @@ static void fused_launch(bool fwd, uint64_t* d, uint32_t n, size_t stride, const
                        body_tab);
 }
 
-bool split_fused_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("MI_SPLIT_FUSED");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch, size_t stride, const uint64_t* blk,
                                   const uint64_t* body_tab, hipStream_t s) {
   if (t < 1 || t > 3) return hipErrorInvalidValue;
@@ -330,71 +266,33 @@ hipError_t launch_ntt_split_fused(bool fwd, int t, uint64_t* data, size_t batch,
   return hipGetLastError();
 }
 
-// MI_PBS_WS = two-wave workgroups per CU of the wave-specialised MAC-fused inverse (0: the four-wave fused kernel)
-static uint32_t inv_mac_ws_wgs_per_cu() {  // read per launch (tests switch it within one process)
-  const char* v = getenv("MI_PBS_WS");
-  return v ? (uint32_t)std::max(0, std::min(8, atoi(v))) : 0u;
-}
-
 bool inv_mac_supported(int level, int kp1) {
   const int L = level * kp1;
   return L == 2 || L == 3 || L == 4 || L == 6 || L == 8;
 }
 
 hipError_t launch_ntt_tw_inv_mac(uint64_t* y, const uint64_t* digits, const uint64_t* ggsw, size_t n_items, int kp1,
-                                 int level, int logn, const uint64_t* twist, hipStream_t s, size_t wave_cap) {
-  static const uint32_t stagger = [] {
-    const char* v = getenv("MI_PBS_STAGGER");
-    return v ? (uint32_t)std::max(0, atoi(v)) : 0u;
-  }();
+                                 int level, int logn, const uint64_t* twist, hipStream_t s) {
   const int sub_log = logn - 11;
   if (sub_log < 1 || !inv_mac_supported(level, kp1)) return hipErrorInvalidValue;
   if (n_items == 0) return hipSuccess;
   const uint64_t units = (uint64_t)n_items * kp1 << sub_log;
   if (units > 0xffffffffull - 4 * 65536) return hipErrorInvalidValue;  // uint32 unit indices (the callers' chunks are far below)
-  if ((level * kp1 == 4 || level * kp1 == 6) && inv_mac_ws_wgs_per_cu() > 0) {  // MI_PBS_WS (r5 A/B)
-    int dev = 0, cus = 0;
-    if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const dim3 g((unsigned)std::min<uint64_t>(units, (uint64_t)cus * inv_mac_ws_wgs_per_cu())), blk(128);
-    const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
-    if (level * kp1 == 4)
-      hipLaunchKernelGGL(tw::ntt_tw_inv_mac_ws_kernel<4>, g, blk, 0, s, y, digits, ggsw, un, ni, sl, kp, twist);
-    else
-      hipLaunchKernelGGL(tw::ntt_tw_inv_mac_ws_kernel<6>, g, blk, 0, s, y, digits, ggsw, un, ni, sl, kp, twist);
-    return hipGetLastError();
-  }
-  const uint64_t wgs = (units + 3) / 4, cap = wave_cap ? std::max<uint64_t>(1, wave_cap / 4) : wgs;
-  const dim3 grid((unsigned)std::min(wgs, cap)), block(256);
+  const dim3 grid((unsigned)((units + 3) / 4)), block(256);
   const uint32_t un = (uint32_t)units, ni = (uint32_t)n_items, sl = (uint32_t)sub_log, kp = (uint32_t)kp1;
   switch (level * kp1) {
-    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
-    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
-    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
-    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
-    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist, stagger); break;
+    case 2: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<2>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 3: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<3>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 4: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<4>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    case 6: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<6>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
+    default: hipLaunchKernelGGL(tw::ntt_tw_inv_mac_kernel<8>, grid, block, 0, s, y, digits, ggsw, un, ni, sl, kp, twist); break;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_ntt_tw(bool fwd, uint64_t* data, size_t batch, size_t stride, const uint64_t* twist, hipStream_t s,
-                         int sub_log, size_t wave_cap) {
+                         int sub_log) {
   if (batch == 0) return hipSuccess;
-  if (wave_cap && sub_log > 0 && (batch << sub_log) <= 0xffffffffull) {  // one capped, looping launch
-    const uint32_t n = (uint32_t)(batch << sub_log);
-    if (fwd) {
-      constexpr uint32_t W = tw::tw_waves<true>();
-      const uint32_t g = (uint32_t)std::min<size_t>((n + W - 1) / W, std::max<size_t>(1, wave_cap / W));
-      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<true, true>), dim3(g), dim3(64 * W), 0, s, data, n, (uint64_t)stride,
-                         twist, (uint32_t)sub_log);
-    } else {
-      constexpr uint32_t W = tw::tw_waves<false>();
-      const uint32_t g = (uint32_t)std::min<size_t>((n + W - 1) / W, std::max<size_t>(1, wave_cap / W));
-      hipLaunchKernelGGL((tw::ntt_tw_body_kernel<false, true>), dim3(g), dim3(64 * W), 0, s, data, n,
-                         (uint64_t)stride, twist, (uint32_t)sub_log);
-    }
-    return hipGetLastError();
-  }
   // grid.x limit 2^31 - 1 (a whole chunk is 16 TiB of polynomials); a chunk of units holds whole polynomials
   const size_t CHUNK = (size_t(1) << 30) >> sub_log << sub_log;
   const size_t units = batch << sub_log;

@@ -520,9 +520,8 @@ static hipError_t pbs_shape(bool bnf, int level, uint64_t* out, const uint64_t* 
                             const uint64_t* bsk, size_t n_lwe, size_t batch, int base_log, const uint64_t* tw,
                             const uint64_t* itw, int centered, hipStream_t s) {
   const dim3 grid((unsigned)batch), block(pbs::Shape<LOGN, K>::T);
-  if constexpr (K >= 3) {  // r5: the MAC's key loads one column at a time (MI_SHAPE_SB=0: the r4 schedule, A/B)
-    const char* v = getenv("MI_SHAPE_SB");
-    if (level == 1 && !(v && v[0] == '0')) {
+  if constexpr (LOGN == 9 && K == 4) {  // r5, the measured shape (1_1): the MAC's key loads one column at a time
+    if (level == 1) {
       if (bnf)
         hipLaunchKernelGGL((pbs::pbs_kernel<LOGN, K, true, true, true>), grid, block, 0, s, out, lwe_in, lut, bsk,
                            (uint32_t)n_lwe, (uint32_t)batch, base_log, level, tw, itw, centered);

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void large_rotate_decompose(u64* __restrict__ 
 // (stage 0's twiddles are the tower's powers of two, Goldilocks::mul_pow2; the split tables exist only when they are)
 // in the layout of large_rotate_decompose.  Replaces that pass plus the transform's first pass: acc is read once and
 // the digits written once (not written, read and written again).
-template <int K, bool BNF, bool ONLY, bool LAZY = true>
+template <int K, bool BNF, bool ONLY>
 __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits, const u64* __restrict__ acc,
                                                         const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
                                                         LargeShape sh, const u64* __restrict__ tw,
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void large_rotdec_top(u64* __restrict__ digits
         bool ng;
         const u64 z = Goldilocks::mul_pow2(x[r + d], tower_exp(true, s, r >> (K - s)), ng);  // canonical, any input
         const u64 u = x[r];
-        if (ONLY && LAZY) {  // r5: any 64-bit representatives until the block twist's multiply (as the K = 5 tile)
+        if (ONLY) {  // r5: any 64-bit representatives until the block twist's multiply (as the K = 5 tile)
           x[r] = ng ? Goldilocks::sub_lazy(u, z) : Goldilocks::add_lazy(u, z);
           x[r + d] = ng ? Goldilocks::add_lazy(u, z) : Goldilocks::sub_lazy(u, z);
         } else {
@@ -219,7 +219,7 @@ __device__ __forceinline__ void tile5_fwd_b_tw(u64 (&x)[8], const u64 (&tw)[8]) 
 // The same step at K = 4 / 5 as a cooperative tile (ntt64_tile.hpp): lane (wave W, column c) forms ct1 and the
 // decomposition state of its phase-A rows, then per level runs the phase-A stages, the LDS exchange and the phase-B
 // stages and stores the digit polynomial from its phase-B rows.  Grid: x = column tiles of 64, y = GLWE polynomials.
-template <int K, bool BNF, bool ONLY, int W, bool ASM = true>
+template <int K, bool BNF, bool ONLY, int W>
 __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64* __restrict__ ap, uint32_t full,
                                                  uint32_t rem, uint64_t cols, uint64_t col, uint32_t c, uint64_t per,
                                                  const LargeShape& sh, const u64* __restrict__ twist, u64* lds) {
@@ -257,7 +257,7 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
       x[k] = ((int64_t)term < 0) ? term + P : term;
     }
     u64* o = dp + (uint64_t)li * per;
-    if constexpr (K == 5 && ONLY && ASM) {  // r5: phase A, phase B and the block twist as generated asm (gen_tile_asm.py)
+    if constexpr (K == 5 && ONLY) {  // r5: phase A, phase B and the block twist as generated asm (gen_tile_asm.py)
       tile5_fwd_a<W>(x);
       tile::exchange<K, W, true>(x, lds, c);
       tile5_fwd_b_tw<W>(x, tv);
@@ -278,7 +278,7 @@ __device__ __forceinline__ void rotdec_tile_body(u64* __restrict__ dp, const u64
   }
 }
 
-template <int K, bool BNF, bool ONLY, bool ASM = true>
+template <int K, bool BNF, bool ONLY>
 __global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digits, const u64* __restrict__ acc,
                                                          const u64* __restrict__ lwe_in, uint32_t n_lwe, uint32_t step,
                                                          LargeShape sh, const u64* __restrict__ twist) {
@@ -297,16 +297,11 @@ __global__ __launch_bounds__(256) void large_rotdec_tile(u64* __restrict__ digit
   const uint64_t per = (uint64_t)(sh.k + 1) * sh.n;
   u64* dp = digits + (uint64_t)b * sh.level * per + (uint64_t)cc * sh.n;
   switch (w) {
-    case 0: rotdec_tile_body<K, BNF, ONLY, 0, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    case 1: rotdec_tile_body<K, BNF, ONLY, 1, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    case 2: rotdec_tile_body<K, BNF, ONLY, 2, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
-    default: rotdec_tile_body<K, BNF, ONLY, 3, ASM>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 0: rotdec_tile_body<K, BNF, ONLY, 0>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 1: rotdec_tile_body<K, BNF, ONLY, 1>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    case 2: rotdec_tile_body<K, BNF, ONLY, 2>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
+    default: rotdec_tile_body<K, BNF, ONLY, 3>(dp, ap, full, rem, cols, col, c, per, sh, twist, lds); break;
   }
-}
-
-static bool rotdec_lazy() {  // read per launch (A/B and tests in one process)
-  const char* v = getenv("MI_ROTDEC_LAZY");
-  return !(v && v[0] == '0');
 }
 
 template <int K, bool BNF>
@@ -316,12 +311,9 @@ static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, cons
   if constexpr (K >= 4) {
     if ((sh.n >> K) >= 64) {  // the cooperative tile (>= one 64-column tile)
       const dim3 tgrid((unsigned)(((uint64_t)sh.n >> K) / 64), nb * (sh.k + 1));
-      if (only && tile_asm_enabled(1))
+      if (only)
         hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
                            sh, twist);
-      else if (only)  // MI_TILE_ASM=0: the compiled stages (A/B)
-        hipLaunchKernelGGL((large_rotdec_tile<K, BNF, true, false>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe,
-                           step, sh, twist);
       else
         hipLaunchKernelGGL((large_rotdec_tile<K, BNF, false>), tgrid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
                            sh, twist);
@@ -329,12 +321,9 @@ static hipError_t rotdec_top_launch(bool only, u64* digits, const u64* acc, cons
     }
   }
   const dim3 grid((unsigned)((((uint64_t)sh.n >> K) + 255) / 256), nb * (sh.k + 1));
-  if (only && rotdec_lazy())
+  if (only)
     hipLaunchKernelGGL((large_rotdec_top<K, BNF, true>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
                        tw, twist);
-  else if (only)  // MI_ROTDEC_LAZY=0 (A/B): canonical stages
-    hipLaunchKernelGGL((large_rotdec_top<K, BNF, true, false>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step,
-                       sh, tw, twist);
   else
     hipLaunchKernelGGL((large_rotdec_top<K, BNF, false>), grid, dim3(256), 0, s, digits, acc, lwe_in, n_lwe, step, sh,
                        tw, twist);
@@ -596,29 +585,6 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 
 }  // namespace pbs
 
-static int pbs_wave_cap() {
-  static const int v = [] {
-    const char* e = getenv("MI_PBS_WAVE_CAP");
-    return e ? std::max(0, atoi(e)) : 0;
-  }();
-  return v;
-}
-
-static size_t device_simds(hipStream_t s) {
-  int dev = 0, cus = 0;
-  if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  return (size_t)cus * 4;
-}
-
-static bool mac_fused_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("MI_PBS_MAC_FUSED");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 // Lanes: a chunk of >= PBS_LANE_MIN ciphertexts is split into mi::pbs_lane_count() parts (default 2, >= 16 ciphertexts
 // each), the first on the caller's stream and the others on pooled side streams (mi::StreamFork), their launches
 // interleaved step by step.  Each ciphertext's blind rotation is independent, so the parts share nothing but the key,
@@ -642,13 +608,9 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
   int k0 = 0;
   bool only = false;
   if (split) split_first_pass(logn, &k0, &only);
-  // r5: the MAC fused into the inverse's bodies (ntt64_tw.hip ntt_tw_inv_mac_kernel) where generated; 16-byte aligned
-  // key; MI_PBS_MAC_FUSED=0 in the environment keeps the separate MAC pass (A/B)
-  const bool mac_fused = split && inv_mac_supported(level, k + 1) && mac_fused_enabled();
-  // MI_PBS_WAVE_CAP=<waves per SIMD> (r5 A/B): the step's body launches hold at most that many waves per SIMD of the
-  // device and loop over their units, so two lanes' launches can share every CU (one's memory phase beside the
-  // other's issue-bound bodies) instead of filling the device one after the other; 0 / unset: full grids
-  const size_t wave_cap = pbs_wave_cap() ? (size_t)pbs_wave_cap() * device_simds(s) : 0;
+  // r5: the MAC fused into the inverse's bodies (ntt64_tw.hip ntt_tw_inv_mac_kernel) where generated (l (k + 1) in
+  // {2, 3, 4, 6, 8}); other shapes run the separate MAC pass
+  const bool mac_fused = split && inv_mac_supported(level, k + 1);
   // one lane's share of a chunk: ciphertexts [b0, b0 + nb) of the batch, its scratch slices, its stream
   struct Lane {
     size_t b0;
@@ -676,7 +638,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
               : rotdec_top<false>(k0, only, L.digits, L.acc, L.in, (uint32_t)n_lwe, i, nb, sh, tw, split->blk_fwd, L.st);
       if (e == hipSuccess)
         e = launch_ntt_split(true, logn, L.digits, (size_t)nb * level * (k + 1), sh.n, tw, *split, L.st, nullptr, 0,
-                             true, wave_cap);
+                             true);
     } else {
       if (bnf)
         hipLaunchKernelGGL(large_rotate_decompose<true>, dim3(blocks_for(elems)), dim3(256), 0, L.st, L.digits, L.acc,
@@ -689,7 +651,7 @@ hipError_t launch_pbs_large(int logn, int k, bool bnf, int level, uint64_t* out,
     if (e != hipSuccess) return e;
     if (mac_fused)  // the MAC formed on load by the inverse's 2048-block bodies, then the inverse's top passes
       return (e = launch_ntt_tw_inv_mac(L.y, L.digits, bsk + (size_t)i * ggsw_len, nb, k + 1, level, logn,
-                                         split->body_inv, L.st, wave_cap)) != hipSuccess
+                                         split->body_inv, L.st)) != hipSuccess
                  ? e
                  : launch_ntt_split(false, logn, L.y, (size_t)nb * (k + 1), sh.n, itw, *split, L.st, L.acc,
                                     bnf ? 1 : 2, true);

@@ -268,16 +268,12 @@ __global__ __launch_bounds__(128) void ext_tw_kernel(u64* __restrict__ out, u64*
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x >= batch) return;
   load_lane_pair_tables(lwtab, tab, threadIdx.x);
-  // r5: a grid smaller than the batch loops over items b = blockIdx.x, + gridDim.x, ... (launch_ext_tw's persistent
-  // form, MI_EXT_PERSIST): the workgroups stay resident instead of being relaunched per item
-  for (uint32_t b = blockIdx.x; b < batch; b += gridDim.x) {
-    // per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one shared GGSW
-    const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
-    if (gi >= n_ggsw) continue;  // uniform per workgroup
-    ext_tw_item<CMUX, SOL>(out, glwe, ggsw_list + (size_t)gi * 4 * N, b, base_log, tab, buf, lwtab, lane, w);
-    // the item's row stores drain before the next item's loads (the body's vmcnt waits count only its own loads)
-    if (b + gridDim.x < batch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // one item per workgroup; per-item GGSW (gidx[b] < n_ggsw; an out-of-range index leaves the item untouched) or one
+  // shared GGSW
+  const uint32_t b = blockIdx.x;
+  const uint32_t gi = gidx ? __builtin_amdgcn_readfirstlane(gidx[b]) : 0u;
+  if (gi >= n_ggsw) return;  // uniform per workgroup
+  ext_tw_item<CMUX, SOL>(out, glwe, ggsw_list + (size_t)gi * 4 * N, b, base_log, tab, buf, lwtab, lane, w);
 }
 
 // The blind-rotation body keeps the NTT-domain data in the forward's W1' register layout through the MAC
@@ -314,14 +310,6 @@ hipError_t launch_prepare_tw_key(uint64_t* dst, const uint64_t* src, size_t n_po
 
 bool ext_tw_reads_w1p() { return MI_EXT_W1P != 0; }
 
-static bool ext_persist() {
-  static const bool on = [] {
-    const char* v = getenv("MI_EXT_PERSIST");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
 hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, const uint64_t* ggsw, size_t batch,
                          int base_log, const uint64_t* tab, hipStream_t s, const uint32_t* gidx, uint32_t n_ggsw,
                          bool prepared) {
@@ -338,16 +326,7 @@ hipError_t launch_ext_tw(bool cmux, bool sol, uint64_t* out, uint64_t* glwe, con
     }
     ggsw = perm;
   }
-  // MI_EXT_PERSIST=1 (r5 A/B): at most 4 resident two-wave workgroups per CU (the bodies' 256 VGPRs allow 2 waves per
-  // SIMD), each looping over items; default: one workgroup per item
-  size_t wgs = batch;
-  if (ext_persist()) {
-    int dev = 0, cus = 0;
-    if (hipStreamGetDevice(s, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    wgs = std::min<size_t>(batch, (size_t)cus * 4);
-  }
-  const dim3 g((unsigned)wgs), blk(128);
+  const dim3 g((unsigned)batch), blk(128);  // one workgroup per item (a looping persistent grid measured slower, r5)
   if (sol && cmux)
     hipLaunchKernelGGL((pbstw::ext_tw_kernel<true, true>), g, blk, 0, s, out, glwe, ggsw, (uint32_t)batch, base_log, tab, gidx, n_ggsw);
   else if (sol)

@@ -9,9 +9,9 @@ from .prime64 import SOLINAS_P, Plan, fill_uniform
 
 _load_lib()
 
-from . import fft64, fourier_bsk_format, lwe_keyswitch, multi_gpu, ntt64_pbs, ntt_bsk_format, prime32  # noqa: E402,E501  (core_crypto consumers; key formats; batch sharding; u32 plans)
+from . import fft64, fourier_bsk_format, lwe_keyswitch, multi_gpu, ntt64, ntt64_pbs, ntt_bsk_format, prime32  # noqa: E402,E501  (core_crypto consumers; key formats; batch sharding; u32 plans)
 from .native import (native32, native64, native128, native_binary32, native_binary64,  # noqa: E402
                      native_binary128)
 
-__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform", "fft64", "ntt64_pbs", "lwe_keyswitch", "multi_gpu", "prime32", "native32",
+__all__ = ["Plan", "SOLINAS_P", "MiError", "fill_uniform", "fft64", "ntt64", "ntt64_pbs", "lwe_keyswitch", "multi_gpu", "prime32", "native32",
            "native64", "native128", "native_binary32", "native_binary64", "native_binary128"]

@@ -50,6 +50,12 @@ _SIGS = {
     "mi_ntt64_normalize_batch": (_int, [_vp, _vp, _sz, _sz, _vp]),
     "mi_ntt64_mul_assign_normalize_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
     "mi_ntt64_mul_accumulate_batch": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_forward_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_forward_normalized_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_forward_from_power_of_two_modulus_batch": (_int, [_vp, ctypes.c_uint, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_forward_from_decomp_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_add_backward_batch": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "mi_ntt64_add_backward_on_power_of_two_modulus_batch": (_int, [_vp, ctypes.c_uint, _vp, _vp, _sz, _sz, _vp]),
     "mi_ntt64_fwd_host": (_int, [_vp, _p64, _sz]),
     "mi_ntt64_inv_host": (_int, [_vp, _p64, _sz]),
     "mi_ntt64_normalize_host": (_int, [_vp, _p64, _sz]),
@@ -140,6 +146,7 @@ _SIGS = {
                                  ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     "mi_lwe_keyswitch32_batch": (_int, [_vp, _vp, _vp, _sz, _vp]),
     "mi_lwe_modulus_switch32_batch": (_int, [_vp, _vp, _sz, _sz, _int, _int, _int, _vp]),
+    "mi_lwe_modulus_switch_batch": (_int, [_vp, _vp, _sz, _sz, _int, _int, _int, _vp]),
 }
 
 

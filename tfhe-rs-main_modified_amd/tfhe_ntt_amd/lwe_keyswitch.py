@@ -6,8 +6,9 @@ Reference (paths relative to /root/reference/tfhe/src/core_crypto):
 * ``keyswitch_lwe_ciphertext``   algorithms/lwe_keyswitch.rs:103-227 (native 2^64 modulus)
 * ``keyswitch_lwe_ciphertext_with_scalar_change``  algorithms/lwe_keyswitch.rs:331-447 (u64 -> u32 LWEs, the HPU
   KS32 parameter sets, shortint/parameters/v1_5/hpu.rs:57-76)
-* ``lwe_ciphertext_modulus_switch`` / ``lwe_ciphertext_centered_binary_modulus_switch`` of u32 LWEs
-  algorithms/modulus_switch.rs:14-104 (the KS32 bootstrap's input, mockups/tfhe-hpu-mockup/src/lib.rs:720-736)
+* ``lwe_ciphertext_modulus_switch`` / ``lwe_ciphertext_centered_binary_modulus_switch`` of u32 LWEs (the KS32
+  bootstrap's input, mockups/tfhe-hpu-mockup/src/lib.rs:720-736) and of u64 LWEs (the native-modulus ciphertexts in
+  front of every other blind rotation), algorithms/modulus_switch.rs:14-104
 
 The reference keyswitches one ciphertext per call; here a leading batch dimension is allowed (one
 launch on the int8 matrix cores, csrc/keyswitch.hip).  Shape mismatches raise ``ValueError`` where
@@ -151,6 +152,25 @@ def lwe_ciphertext_centered_binary_modulus_switch32(lwe_in, switched_out, log_mo
     lwe_ciphertext_modulus_switch32(lwe_in, switched_out, log_modulus, centered=True)
 
 
+def lwe_ciphertext_modulus_switch(lwe_in, switched_out, log_modulus: int, centered: bool = False) -> None:
+    """The (centered binary) modulus switch of u64 LWEs (modulus_switch.rs:14-104 at Scalar = u64), materialised as
+    the LazyStandardModulusSwitchedLweCiphertext reads it (modulus_switched_lwe_ciphertext.rs:150-175): switched_out
+    (same shape as lwe_in) gets every value in [0, 2^log_modulus), the MI_MS_PRE_SWITCHED input of the blind rotation
+    / PBS.  log_modulus in [1, 64] (standard) or [1, 63] (centered: the reference's half_case shift underflows at 64)."""
+    if tuple(switched_out.shape) != tuple(lwe_in.shape):
+        raise ValueError(f"assertion failed: shapes {tuple(lwe_in.shape)} != {tuple(switched_out.shape)}")
+    size = lwe_in.shape[-1]
+    batch = lwe_in.numel() // size
+    check(lib().mi_lwe_modulus_switch_batch(_dev(switched_out, "switched_out"), _dev(lwe_in, "lwe_in"), size - 1,
+                                            batch, log_modulus, MS_CENTERED if centered else MS_STANDARD,
+                                            lwe_in.device.index or 0, _stream(lwe_in)))
+
+
+def lwe_ciphertext_centered_binary_modulus_switch(lwe_in, switched_out, log_modulus: int) -> None:
+    lwe_ciphertext_modulus_switch(lwe_in, switched_out, log_modulus, centered=True)
+
+
 __all__ = ["LweKeyswitchKey", "keyswitch_lwe_ciphertext", "LweKeyswitchKey32",
            "keyswitch_lwe_ciphertext_with_scalar_change", "lwe_ciphertext_modulus_switch32",
-           "lwe_ciphertext_centered_binary_modulus_switch32"]
+           "lwe_ciphertext_centered_binary_modulus_switch32", "lwe_ciphertext_modulus_switch",
+           "lwe_ciphertext_centered_binary_modulus_switch"]

@@ -417,14 +417,16 @@ def body_lines(hdr, name, prefix="MI_TW_BODY_"):
     return [m.group(1) for m in re.finditer(r'"(.*?)\\n"', txt[start:end])]
 
 
-def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra=None, ops_extra=None):
+def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra=None, ops_extra=None, out_init=None):
     """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial.  out_of_place: the body
     writes another buffer (%[o_lo] / %[o_hi], the key-conversion body), which is returned.  mem_extra / ops_extra:
-    more memory regions (base address -> u64 array) and operand bindings (the MAC-fused inverse's term bases)."""
+    more memory regions (base address -> u64 array) and operand bindings (the MAC-fused inverse's term bases).
+    out_init: the %[o_*] buffer's initial contents (the Ntt64View add_backward bodies read and write it); the call then
+    returns (data, out)."""
     data = np.array(poly, dtype=np.uint64).copy()
     tw = np.array(twist_tab, dtype=np.uint64)
     GB, TB, OB = 0x100000000, 0x200000000, 0x300000000
-    out = np.zeros_like(data)
+    out = np.zeros_like(data) if out_init is None else np.array(out_init, dtype=np.uint64).copy()
     mem = {GB: data, TB: tw, OB: out}
     lane = np.arange(LANES, dtype=np.uint64)
     par, i = lane & np.uint64(1), lane >> np.uint64(1)
@@ -449,6 +451,8 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra
         ops.update(ops_extra)
     w.ops = ops
     w.run(body_lines(hdr, name))
+    if out_init is not None:
+        return data, out
     return out if out_of_place else data
 
 

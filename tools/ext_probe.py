@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time bench.py's config-3 external-product leg alone (diagnostic; A/B of launch forms via the environment, e.g.
-MI_EXT_PERSIST=1).   python tools/ext_probe.py [batch]"""
+r5; the persistent form it compared is gone).   python tools/ext_probe.py [batch]"""
 import argparse
 import json
 import os

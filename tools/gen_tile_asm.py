@@ -151,13 +151,8 @@ def main():
         out.append(emit_fn(f"k5_fwd_a_w{W}", stages_text(tile5_stages(W, "a"), SC_K5), 8, None, SC_K5, 24))
         lines = stages_text(tile5_stages(W, "b"), SC_K5) + twist_text(8, TB_K5, SC_K5)
         out.append(emit_fn(f"k5_fwd_b_tw_w{W}", lines, 8, TB_K5, SC_K5, 24))
-        # the inverse tile of the accumulating last top pass (ntt64_kernels.hip top_tile_body<5, false, 2, ACC>): the
-        # block untwist on load, phase B; LDS exchange (C++); phase A, canonical outputs for the accumulation
-        lines = twist_text(8, TB_K5, SC_K5) + gs_stages_text(tile5_inv_stages(W, "b"), SC_K5)
-        out.append(emit_fn(f"k5_inv_tw_b_w{W}", lines, 8, TB_K5, SC_K5, 24))
-        out.append(emit_fn(f"k5_inv_a_w{W}", gs_stages_text(tile5_inv_stages(W, "a"), SC_K5), 8, None, SC_K5, 24))
-        # the same phase B without the untwist (the compiled multiply overlaps the row loads; MI_TILE_ASM bit 2)
-        out.append(emit_fn(f"k5_inv_b_w{W}", gs_stages_text(tile5_inv_stages(W, "b"), SC_K5), 8, None, SC_K5, 24))
+        # (the inverse tile of the accumulating last top pass as asm, tile5_inv_stages / gs_stages_text, measured
+        # slower in r5 and is not emitted: the library runs the compiled stages there)
     out += ["}  // namespace tile_asm", "}  // namespace mi"]
     print("\n".join(out))
 

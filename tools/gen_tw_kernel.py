@@ -1816,7 +1816,7 @@ def gen_inv_mac(tabs, L, vhi=MAC_VHI):
     return B
 
 
-# The wave-specialised form (r5, pbs_large.hip MI_PBS_WS): a two-wave workgroup loops over units; its producer wave
+# The wave-specialised form (r5 probe, not emitted into the library: measured 2-5 % slower than the fused kernel): a two-wave workgroup loops over units; its producer wave
 # forms unit u's block of y (mac_phase) while its consumer wave runs the inverse of unit u - 1, so the MAC's memory
 # phase and the inverse's issue phase overlap inside every SIMD (the dispatcher puts two producers and two consumers on
 # each SIMD, tools/placement_probe.hip) instead of running in lockstep across the device.  Hand-off through the
@@ -1882,9 +1882,6 @@ def main():
     print(emit("fwd_ms64", gen_fwd_ms64(tabs), None, MS_SGPRS))
     for L in MAC_LS:
         print(emit(f"inv_mac{L}", gen_inv_mac(tabs, L), None, range(94, max(94, S_MB + 4 * L)), MAC_VHI))
-    for L in WS_LS:
-        print(emit(f"macp{L}", gen_macp(tabs, L), None, range(94, max(94, S_MB + 4 * L)), MAC_VHI))
-    print(emit("invc", gen_invc(tabs), None, (), MAC_VHI))
     print(f"// fwd {f.nvalu} VALU, inv {i.nvalu} VALU", file=sys.stderr)
 
 
