@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Integer-VALU issue model of the generated bodies (tools/valu_cost.py: instruction mix x the issue
 # costs measured by tools/valu_probe.hip; tests/test_bench_contract.py keeps these in sync), and the
 # MI355X peak engine clock it is priced at.
-VALU_CYCLES = {"fwd": 13919.9, "inv": 14447.5, "pbs_step": 35057.4, "pbs_sol_step": 35378.7, "ext_bnf": 33868.5}
+VALU_CYCLES = {"fwd": 13631.3, "inv": 14158.8, "pbs_step": 35057.4, "pbs_sol_step": 35378.7, "ext_bnf": 33868.5}
 SIMDS, PEAK_CLOCK_HZ = 256 * 4, 2.4e9
 # PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
 PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096
@@ -332,7 +332,7 @@ def bench_pbs_shape(name, args, eng, torch, dev, world, barrier, dist):
     eng.fill_uniform(lwe, SEED + 92, 0)
     out = torch.empty((batch, k * n + 1), dtype=torch.int64, device=dev)
     run = lambda: M.programmable_bootstrap_ntt64_bnf_lwe_ciphertext_mem_optimized(lwe, out, lut, key)
-    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=1)
+    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=3)
     del key
     ntts = n_lwe * (level + 1) * (k + 1)  # forward (level x (k+1)) + inverse (k+1) transforms per CMUX step
     return {"metric": f"PBS/sec, BNF NTT PBS at the {name.upper()} shape", "value": world * batch * K / el,
@@ -394,7 +394,7 @@ def bench_pbs_shape_fft(name, args, eng, torch, dev, world, barrier, dist):
     eng.fill_uniform(lwe, SEED + 95, 0)
     out = torch.empty((batch, k * n + 1), dtype=torch.int64, device=dev)
     run = lambda: F.programmable_bootstrap_lwe_ciphertext(lwe, out, lut, key, F.MS_CENTERED)
-    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=1)
+    K, el, kernel_ms = timed_leg(run, torch, barrier, dist, dev, min_steps=3)
     del key, fbsk
     return {"metric": f"PBS/sec, f64-FFT PBS at the {name.upper()} shape", "value": world * batch * K / el,
             "unit": "PBS/s", "steps": K, "ms_per_step": el / K * 1e3, "kernel_ms": kernel_ms, "dtype": "f64",
@@ -526,6 +526,7 @@ def bench_pbs_sharded(args, eng, torch, dev, rank, world, barrier, pbs, bsk):
             "value": G * K / times[False], "unit": "PBS/s", "scaling": "strong",
             "value_with_scatter_gather": G * K / times[True],
             "ms_per_step": times[False] / K * 1e3, "ms_per_step_with_scatter_gather": times[True] / K * 1e3,
+            "steps": K,
             "key_broadcast_ms": bcast_s * 1e3,
             "config": {"global_batch": G, "n_gpus": world, "shard": [a, b],
                        "transfer": "gloo via host (rehearsal)" if gloo else
@@ -1279,11 +1280,17 @@ def compact_line(out, full_path=None):
         line["config"]["build_matches_tree"] = build.get("match")
     roof = out.get("roofline") or {}
     line["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                "algorithmic_bytes_per_launch", "kernel")}
+                                                "traffic_source", "algorithmic_bytes_per_launch", "kernel")}
     line["cpu_baseline"] = out.get("cpu_baseline")
     kern = out.get("kernels") or {}
     line["kernels"] = {k: kern.get(k) for k in ("timed_launch_ms", "fwd_ms", "inv_ms")}
     line["valu_bound_frac"] = {k: v.get("frac") for k, v in (out.get("valu_bound") or {}).items()}
+    # the sustained rate beside the K-step burst: the >= 1 s loop right after the timed region, and
+    # the same K steps from an idle GPU
+    for key in ("steady_state", "cold_start"):
+        d = out.get(key) or {}
+        if d:
+            line[key] = {k: d.get(k) for k in ("value", "roofline_frac", "seconds", "steps") if d.get(k) is not None}
     line["legs_summary"] = legs_summary(out)
     line["full_record"] = full_path
     return line
@@ -1313,8 +1320,15 @@ def legs_summary(out):
             continue
         if "value" in d:
             rows[name] = row(d)
-        else:
-            rows.update({f"{name}.{k}": row(v) for k, v in d.items() if isinstance(v, dict) and "value" in v})
+        # nested legs with their own value: the shape legs' entries, and config 5 under pbs.sharded / pbs_fft.sharded
+        # (N > 1 ranks) with and without the scatter / gather transfers
+        for k, v in d.items():
+            if isinstance(v, dict) and "value" in v:
+                r = row(v)
+                for extra in ("value_with_scatter_gather", "ms_per_step_with_scatter_gather", "scaling"):
+                    if v.get(extra) is not None:
+                        r[extra] = v[extra]
+                rows[f"{name}.{k}"] = r
     return rows
 
 

@@ -82,6 +82,15 @@ def test_compact_line_fits_driver_tail():
            "host_path": {"blob": "b" * 20000}, "default_stream": {"blob": "b" * 5000}}
     for i, name in enumerate(bench.LEG_ORDER):
         out[name] = _stub_leg(i, nested=name.startswith("pbs_shapes"))
+    # config 5 at world 8: the sharded legs nested under pbs / pbs_fft reach the summary
+    for name in ("pbs", "pbs_fft"):
+        out[name]["sharded"] = dict(_stub_leg(90), scaling="strong", value_with_scatter_gather=2.5e5,
+                                    ms_per_step_with_scatter_gather=300.123456, key_broadcast_ms=12.3,
+                                    config={"global_batch": 65536, "n_gpus": 8, "transfer": "t" * 100})
+    out["steady_state"] = {"value": 6.9e7, "steps": 8600, "seconds": 1.0012, "timed_launch_ms": 0.058,
+                           "roofline_frac": 0.567, "note": "n" * 200}
+    out["cold_start"] = {"value": 6.1e7, "ms_per_step": 0.13, "timed_launch_ms": 0.065, "roofline_frac": 0.51,
+                         "note": "n" * 200}
     line = bench.compact_line(out, bench.FULL_RECORD)
     text = json.dumps(line)
     assert len(text.encode()) <= bench.LINE_MAX_BYTES, len(text)
@@ -94,6 +103,13 @@ def test_compact_line_fits_driver_tail():
         row = line["legs_summary"][name]
         assert {"value", "ms_per_step", "steps", "frac", "alg_frac"} <= set(row), row
     assert "host_path" not in line and "hip_runtime" not in line["config"]
+    for name in ("pbs.sharded", "pbs_fft.sharded"):
+        row = line["legs_summary"][name]
+        assert {"value", "value_with_scatter_gather", "ms_per_step", "ms_per_step_with_scatter_gather", "steps",
+                "scaling"} <= set(row), row
+    assert line["steady_state"]["roofline_frac"] == 0.567 and line["steady_state"]["seconds"] == 1.0012
+    assert line["cold_start"]["value"] == 6.1e7
+    assert line["roofline"]["traffic_source"]
 
 
 def test_compact_line_of_last_rounds_full_record():

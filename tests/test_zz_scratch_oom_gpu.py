@@ -1,0 +1,60 @@
+"""The scratch pool under device-memory pressure (`-m gpu`; named to run last: it fills the card).
+
+ADVICE r5: since the pool keeps a large idle block for the large requests it was made for, a small request allocates
+a new block; when that hipMalloc fails the request must still be served — from the large idle block, or after the
+pool frees its idle blocks — instead of returning OOM where the pre-r5 pool succeeded (csrc/scratch.cpp
+scratch_alloc).  The keyswitch's digit buffer is the scratch request here (batch 131,072: a 1 GiB block; batch 16:
+128 KiB), its output checked against the same call made before the card was full.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _fill_device(torch, dev, floor_bytes=1 << 20):
+    """Allocate device memory in halving chunk sizes until even `floor_bytes` fails; returns the tensors held."""
+    held, size = [], 8 << 30
+    while size >= floor_bytes:
+        try:
+            held.append(torch.empty(size, dtype=torch.uint8, device=dev))
+        except torch.cuda.OutOfMemoryError:
+            size //= 2
+    return held
+
+
+def test_small_request_served_when_device_memory_is_full(engine, oracle):
+    import torch
+    KS = engine.lwe_keyswitch
+    M = engine.ntt64_pbs
+    dev = torch.device("cuda:0")
+    in_dim, out_dim, base_log, level = 2048, 918, 4, 4
+    g = np.random.Generator(np.random.PCG64(0x5C))
+    ksk = torch.from_numpy(g.integers(0, 2**64, size=(in_dim, level, out_dim + 1), dtype=np.uint64).view(np.int64)).to(dev)
+    key = KS.LweKeyswitchKey(ksk, base_log, level)
+    del ksk
+    small_in = torch.from_numpy(g.integers(0, 2**64, size=(16, in_dim + 1), dtype=np.uint64).view(np.int64)).to(dev)
+    small_out = torch.zeros((16, out_dim + 1), dtype=torch.int64, device=dev)
+    KS.keyswitch_lwe_ciphertext(key, small_in, small_out)
+    torch.cuda.synchronize()
+    want = small_out.clone()
+    M.scratch_trim(0)
+    # a large call leaves a 1 GiB idle block behind
+    big_in = torch.zeros((131072, in_dim + 1), dtype=torch.int64, device=dev)
+    big_out = torch.zeros((131072, out_dim + 1), dtype=torch.int64, device=dev)
+    KS.keyswitch_lwe_ciphertext(key, big_in, big_out)
+    torch.cuda.synchronize()
+    del big_in, big_out
+    torch.cuda.empty_cache()
+    assert M.scratch_bytes(0) >= 1 << 30
+    held = []
+    try:
+        held = _fill_device(torch, dev)
+        small_out.zero_()
+        KS.keyswitch_lwe_ciphertext(key, small_in, small_out)  # its new 1 MiB block cannot be allocated
+        torch.cuda.synchronize()
+        assert torch.equal(small_out, want)
+    finally:
+        del held
+        torch.cuda.empty_cache()
+        M.scratch_trim(0)

@@ -154,21 +154,15 @@ __global__ __launch_bounds__(64) void ntt_tw_ms64_kernel(u64* dst, const u64* sr
   const u64* p = src + (uint64_t)poly * 2048;
   u64* q = dst + (uint64_t)poly * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)lds;
-  const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
-  const uint32_t t1w = S + (lane & 31) * 8;
-  const uint32_t t1r = S + (i * 34 + par) * 8;
-  const uint32_t lwo = par * 128;
+  const FwdAddrs a(S, lane);
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t olo = (uint32_t)(uintptr_t)q, ohi = (uint32_t)((uintptr_t)q >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
   const u64* lw = twist + 2048;
-  const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
-  const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
-  const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
   MI_TW_BODY_FWD_MS64([g_lo] "s"(glo), [g_hi] "s"(ghi), [o_lo] "s"(olo), [o_hi] "s"(ohi), [tw_lo] "s"(twlo),
-                      [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t1w] "v"(t1w), [t1r] "v"(t1r),
-                      [t2wl] "v"(t2wl), [t2wh] "v"(t2wh), [t2r] "v"(t2r), [lwo] "v"(lwo));
+                      [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t1w] "v"(a.t1w), [t1r] "v"(a.t1r),
+                      [t2wl] "v"(a.t2wl), [t2wh] "v"(a.t2wh), [t2r] "v"(a.t2r), [lwo] "v"(a.lwo));
 }
 
 
@@ -191,21 +185,17 @@ __device__ __forceinline__ void inv_mac_unit(u64* __restrict__ y, const u64* __r
   const u64* d = digits + (uint64_t)b * L * n + (uint64_t)blk * 2048;
   const u64* g = ggsw + (uint64_t)c * n + (uint64_t)blk * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)wl;
-  const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
-  const uint32_t lwo = par * 128;
+  const tw::InvAddrs a(S, lane);
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
   const u64* lw = twist + 2 * (2048 + 32);  // the last-DIT-stage table (tw_body<false>)
-  const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
-  const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
-  const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
   const uint32_t dlo = (uint32_t)(uintptr_t)d, dhi = (uint32_t)((uintptr_t)d >> 32);
   const uint32_t gglo = (uint32_t)(uintptr_t)g, gghi = (uint32_t)((uintptr_t)g >> 32);
   const uint32_t dstep = (uint32_t)(n * 8), gstep = (uint32_t)(kp1 * n * 8);
 #define MI_INV_MAC_OPS                                                                                             \
-  [g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t4w] "v"(t4w), \
-      [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo), [d_lo] "s"(dlo), [d_hi] "s"(dhi), [dstep] "s"(dstep),           \
+  [g_lo] "s"(glo), [g_hi] "s"(ghi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi), [lw] "s"(lw), [l8] "v"(l8), [t4w] "v"(a.t4w), \
+      [t1x] "v"(a.t1x), [t1y] "v"(a.t1y), [lwo] "v"(a.lwo), [d_lo] "s"(dlo), [d_hi] "s"(dhi), [dstep] "s"(dstep),           \
       [gg_lo] "s"(gglo), [gg_hi] "s"(gghi), [gstep] "s"(gstep)
   if constexpr (L == 2) MI_TW_BODY_INV_MAC2(MI_INV_MAC_OPS);
   else if constexpr (L == 3) MI_TW_BODY_INV_MAC3(MI_INV_MAC_OPS);

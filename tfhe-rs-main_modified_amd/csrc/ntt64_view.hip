@@ -103,22 +103,16 @@ __global__ __launch_bounds__(64) void view_fwd_kernel(u64* ntt, const u64* stand
   const u64* p = standard + (uint64_t)poly * stride;
   u64* q = ntt + (uint64_t)poly * stride;
   const uint32_t S = (uint32_t)(uintptr_t)lds;
-  const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
-  const uint32_t t1w = S + (lane & 31) * 8;
-  const uint32_t t1r = S + (i * 34 + par) * 8;
-  const uint32_t lwo = par * 128;
+  const tw::FwdAddrs a(S, lane);  // the forward body's W1x transposes (ntt64_tw_device.hpp)
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t olo = (uint32_t)(uintptr_t)q, ohi = (uint32_t)((uintptr_t)q >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
   const u64* lw = twist + 2048;
-  const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
-  const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
-  const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
 #define MI_VIEW_FWD_OPS                                                                                           \
   [g_lo] "s"(glo), [g_hi] "s"(ghi), [o_lo] "s"(olo), [o_hi] "s"(ohi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi),    \
-      [lw] "s"(lw), [l8] "v"(l8), [t1w] "v"(t1w), [t1r] "v"(t1r), [t2wl] "v"(t2wl), [t2wh] "v"(t2wh),          \
-      [t2r] "v"(t2r), [lwo] "v"(lwo)
+      [lw] "s"(lw), [l8] "v"(l8), [t1w] "v"(a.t1w), [t1r] "v"(a.t1r), [t2wl] "v"(a.t2wl), [t2wh] "v"(a.t2wh),  \
+      [t2r] "v"(a.t2r), [lwo] "v"(a.lwo)
   if constexpr (KIND == PRE_COPY) {
     MI_TW_BODY_FWD_COPY(MI_VIEW_FWD_OPS);
   } else if constexpr (KIND == PRE_POW2) {
@@ -141,19 +135,15 @@ __global__ __launch_bounds__(256) void view_inv_kernel(u64* standard, u64* ntt, 
   u64* p = ntt + (uint64_t)poly * stride;
   u64* q = standard + (uint64_t)poly * stride;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * tw::WAVE_LDS2);
-  const uint32_t par = lane & 1, i = lane >> 1;
   const uint32_t l8 = lane * 8;
-  const uint32_t lwo = par * 128;
+  const tw::InvAddrs a(S, lane);
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t olo = (uint32_t)(uintptr_t)q, ohi = (uint32_t)((uintptr_t)q >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
   const u64* lw = twist + 2 * (2048 + 32);  // the last-DIT-stage table (tw_body<false>)
-  const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
-  const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
-  const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
 #define MI_VIEW_INV_OPS                                                                                          \
   [g_lo] "s"(glo), [g_hi] "s"(ghi), [o_lo] "s"(olo), [o_hi] "s"(ohi), [tw_lo] "s"(twlo), [tw_hi] "s"(twhi),   \
-      [lw] "s"(lw), [l8] "v"(l8), [t4w] "v"(t4w), [t1x] "v"(t1x), [t1y] "v"(t1y), [lwo] "v"(lwo)
+      [lw] "s"(lw), [l8] "v"(l8), [t4w] "v"(a.t4w), [t1x] "v"(a.t1x), [t1y] "v"(a.t1y), [lwo] "v"(a.lwo)
   if constexpr (POW2_64) {
     MI_TW_BODY_INV_ADD64(MI_VIEW_INV_OPS);
   } else {

@@ -92,6 +92,31 @@ void release(std::vector<Block>& blocks) {
   (void)hipSetDevice(cur);
 }
 
+// takes the smallest idle block of `dev` that holds `bytes` (snug ones only when `snug`) into the busy map
+bool take_idle(Pool& P, int dev, size_t bytes, bool snug, Block* out) {
+  auto best = P.idle.end();
+  for (auto it = P.idle.begin(); it != P.idle.end(); ++it)
+    if (it->device == dev && it->bytes >= bytes && (!snug || fits_snugly(it->bytes, bytes)) &&
+        (best == P.idle.end() || it->bytes < best->bytes))
+      best = it;
+  if (best == P.idle.end()) return false;
+  *out = *best;
+  P.idle.erase(best);
+  P.busy[out->p] = *out;
+  return true;
+}
+
+// hands a reused block to the caller: its stream waits for the block's last user
+hipError_t issue_reused(const Block& blk, void** out, hipStream_t s) {
+  hipError_t e;
+  if (blk.recorded && (e = hipStreamWaitEvent(s, blk.last_use, 0)) != hipSuccess) {
+    (void)scratch_free(blk.p, nullptr);
+    return e;
+  }
+  *out = blk.p;
+  return hipSuccess;
+}
+
 }  // namespace
 
 hipError_t scratch_alloc(void** out, size_t bytes, hipStream_t s) {
@@ -106,17 +131,8 @@ hipError_t scratch_alloc(void** out, size_t bytes, hipStream_t s) {
   std::vector<Block> smaller;  // idle blocks a new, larger block supersedes
   {
     std::lock_guard<std::mutex> lk(P.mu);
-    auto best = P.idle.end();
-    for (auto it = P.idle.begin(); it != P.idle.end(); ++it)
-      if (it->device == dev && it->bytes >= bytes && fits_snugly(it->bytes, bytes) &&
-          (best == P.idle.end() || it->bytes < best->bytes))
-        best = it;
-    if (best != P.idle.end()) {
-      blk = *best;
-      P.idle.erase(best);
-      P.busy[blk.p] = blk;
-      found = true;
-    } else {
+    found = take_idle(P, dev, bytes, true, &blk);
+    if (!found) {
       // only the idle blocks too small for this request are superseded; a much larger idle block stays for the
       // large requests it was made for (a small request no longer takes the 4 GiB PBS block)
       auto keep = std::partition(P.idle.begin(), P.idle.end(),
@@ -125,21 +141,29 @@ hipError_t scratch_alloc(void** out, size_t bytes, hipStream_t s) {
       P.idle.erase(keep, P.idle.end());
     }
   }
-  if (found) {
-    if (blk.recorded && (e = hipStreamWaitEvent(s, blk.last_use, 0)) != hipSuccess) {
-      (void)scratch_free(blk.p, nullptr);
-      return e;
-    }
-    *out = blk.p;
-    return hipSuccess;
-  }
+  if (found) return issue_reused(blk, out, s);
   release(smaller);
   blk = Block{};
   blk.device = dev;
   blk.bytes = (bytes + GRAIN - 1) / GRAIN * GRAIN;
   if ((e = hipMalloc(&blk.p, blk.bytes)) != hipSuccess) {
     (void)hipGetLastError();
-    return e;
+    // out of device memory: serve the request from any idle block of this device that holds it, snug or
+    // not (before the snug rule this request would have taken it); failing that, free every idle block of the device
+    // once its last user has retired and try the allocation again
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      found = take_idle(P, dev, bytes, false, &blk);
+    }
+    if (found) return issue_reused(blk, out, s);
+    (void)scratch_trim(dev);
+    blk = Block{};
+    blk.device = dev;
+    blk.bytes = (bytes + GRAIN - 1) / GRAIN * GRAIN;
+    if ((e = hipMalloc(&blk.p, blk.bytes)) != hipSuccess) {
+      (void)hipGetLastError();
+      return e;
+    }
   }
   if ((e = hipEventCreateWithFlags(&blk.last_use, hipEventDisableTiming)) != hipSuccess) {
     (void)hipFree(blk.p);

@@ -246,6 +246,13 @@ class Wave:
         idx = np.array([(l & ~3) + perm[l & 3] for l in range(LANES)])
         self.wv(self.vreg(a[0]), np.where(self.mask("vcc"), self.src32(a[2]), src[idx]))
 
+    def op_v_permlane32_swap_b32(self, a):
+        # half-wave exchange: lanes 32-63 of vdst <-> lanes 0-31 of vsrc (whole registers, EXEC all ones)
+        d, s_ = self.vreg(a[0]), self.vreg(a[1])
+        lo = self.v[s_][:32].copy()
+        self.v[s_][:32] = self.v[d][32:]
+        self.v[d][32:] = lo
+
     def op_v_cndmask_b32_e64(self, a):
         m = self.mask(a[3])
         self.wv(self.vreg(a[0]), np.where(m, self.src32(a[2]), self.src32(a[1])))
@@ -417,12 +424,14 @@ def body_lines(hdr, name, prefix="MI_TW_BODY_"):
     return [m.group(1) for m in re.finditer(r'"(.*?)\\n"', txt[start:end])]
 
 
-def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra=None, ops_extra=None, out_init=None):
+def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra=None, ops_extra=None, out_init=None,
+             w1x=None):
     """Emulate one wave (wave 0 of a workgroup) of the transform body on one polynomial.  out_of_place: the body
     writes another buffer (%[o_lo] / %[o_hi], the key-conversion body), which is returned.  mem_extra / ops_extra:
     more memory regions (base address -> u64 array) and operand bindings (the MAC-fused inverse's term bases).
     out_init: the %[o_*] buffer's initial contents (the Ntt64View add_backward bodies read and write it); the call then
-    returns (data, out)."""
+    returns (data, out).  w1x (default: the generator's FWD_W1X for forward bodies, i.e. names starting "fwd"): the
+    forward's W1x lane-pair layout (lane = i + 32 j0) and its transpose addresses, as ntt64_tw_device.hpp computes them."""
     data = np.array(poly, dtype=np.uint64).copy()
     tw = np.array(twist_tab, dtype=np.uint64)
     GB, TB, OB = 0x100000000, 0x200000000, 0x300000000
@@ -438,6 +447,14 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra
            "t2wl": S + ((i & 15) * 66 + 33 * par) * 8, "t2wh": S + ((i & 15) * 66 + 31 * par + 1) * 8,
            "t2r": S + (lane ^ (lane >> np.uint64(5))) * 8, "t4w": S + ((i & 15) * 66 + par) * 8, "t4r": S + lane * 8,
            "t1x": S + (lane + (lane >> np.uint64(5))) * 8, "t1y": S + ((i & 15) * 66 + 33 * par) * 8}
+    if w1x is None:
+        import gen_tw_kernel as _T
+        w1x = (_T.FWD_W1X and name.startswith("fwd")) or (_T.INV_W1X and name.startswith("inv"))
+    if w1x:  # lane = i + 32 j0 (gen_tw_kernel NTT_ADDR_W1X; the inverse's W1'' pair bit j5 likewise)
+        par, i = lane >> np.uint64(5), lane & np.uint64(31)
+        vin.update({"t1r": S + (i * 33 + par) * 8, "lwo": par * 128,
+                    "t2wl": S + ((i & 15) * 65 + 33 * par) * 8, "t2wh": S + ((i & 15) * 65 + 31 * par + 1) * 8,
+                    "t4w": S + ((i & 15) * 65 + par) * 8, "t1y": S + ((i & 15) * 66 + 33 * par) * 8})
     for k, (name_, val) in enumerate(vin.items()):
         w.v[200 + k] = val.astype(np.uint64)   # outside the body's v8..v127
         ops[name_] = f"v{200 + k}"
@@ -454,54 +471,6 @@ def run_body(hdr, name, poly, twist_tab, fwd=True, out_of_place=False, mem_extra
     if out_init is not None:
         return data, out
     return out if out_of_place else data
-
-
-def run_ws(hdr, L, twist_tab, mem_extra, ops_extra, units=1, producer_ops=None):
-    """Emulate the wave-specialised MAC-fused inverse's two-wave workgroup (gen_tw_kernel.gen_macp / gen_invc) over
-    `units` consecutive units: wave 0 runs macp{L} per unit, wave 1 invc, round-robin between s_barriers, one LDS
-    (the y buffer at 0, the consumer's transposes after it).  producer_ops(k) / ops_extra: per-unit term bases
-    (d_lo, d_hi, gg_lo, gg_hi, dstep, gstep) and the consumer's output base per unit (g_lo / g_hi via
-    ops_extra["out"](k) -> (lo, hi)).  Returns nothing: the outputs land in mem_extra's regions."""
-    tw = np.array(twist_tab, dtype=np.uint64)
-    TB = 0x200000000
-    mem = {TB: tw}
-    mem.update(mem_extra)
-    lds = np.zeros(8192, dtype=np.uint64)
-    lane = np.arange(LANES, dtype=np.uint64)
-    par, i = lane & np.uint64(1), lane >> np.uint64(1)
-    S = 16384  # the consumer's transposes after the 16 KiB hand-off buffer (ntt_tw_inv_mac_ws_kernel)
-    lw = TB + 2048 * 8
-    vin = {"l8": lane * 8, "lwo": par * 128, "t4w": S + ((i & 15) * 66 + par) * 8,
-           "t1x": S + (lane + (lane >> np.uint64(5))) * 8, "t1y": S + ((i & 15) * 66 + 33 * par) * 8,
-           "yw": lane * 8}
-
-    def wave(ops):
-        w = Wave(None, mem, lds=lds)
-        for k, (name_, val) in enumerate(vin.items()):
-            w.v[200 + k] = val.astype(np.uint64)
-            ops[name_] = f"v{200 + k}"
-        w.s[104], w.s[105] = np.uint64(lw & 0xFFFFFFFF), np.uint64(lw >> 32)
-        ops["lw"] = "s[104:105]"
-        ops["tw_lo"], ops["tw_hi"] = f"{TB & 0xFFFFFFFF}", f"{TB >> 32}"
-        w.ops = ops
-        return w
-
-    pl, cl = body_lines(hdr, f"macp{L}"), body_lines(hdr, "invc")
-
-    def run_wave(lines, ops_for):
-        for k in range(units):
-            w = wave(ops_for(k))
-            w.load(lines)
-            yield from w.steps()
-
-    gens = [run_wave(pl, producer_ops), run_wave(cl, lambda k: dict(zip(("g_lo", "g_hi"), ops_extra["out"](k))))]
-    live = list(gens)
-    while live:  # every live wave runs to its next barrier, then the next one
-        for g in list(live):
-            try:
-                next(g)
-            except StopIteration:
-                live.remove(g)
 
 
 def _lds_with_lane_pair_tables(tab, N, stride=None):

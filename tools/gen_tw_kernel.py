@@ -729,10 +729,15 @@ class Body:
         self.tabs = tabs
         self.lines = []
         self.nvalu = 0
+        # the per-block tally (tools/valu_cost.py --blocks): `tag` names the block being emitted; blocks[tag] holds its
+        # lines, bfly[(tag, exponent mod 192)] the lines of each butterfly of a stage before scheduling
+        self.tag = "setup"
+        self.blocks, self.bfly = {}, {}
 
     def out(self, lines):
         self.lines += lines
         self.nvalu += sum(1 for l in lines if l.startswith("v_"))
+        self.blocks.setdefault(self.tag, []).extend(lines)
 
     def raw(self, *lines):
         self.out(list(lines))
@@ -770,6 +775,7 @@ class Body:
             S = exps[r] if by_reg else exps[r // (2 * dist)]
             sl = slots[bf % len(slots)]
             a, b = X(dmap, r), X(dmap, r + dist)
+            n0 = len(sg.ops)
             if kind == "ct" and modes is not None:
                 scaled_ct(sg, sl, dmap, r, r + dist, S, modes[bf], scales, canon)
             elif kind == "ct":
@@ -780,6 +786,8 @@ class Body:
                 canon[r] = canon[r + dist] = False
             else:
                 canon[r], canon[r + dist] = gs(sg, sl, a, b, S, canon[r], canon[r + dist])
+            self.bfly.setdefault((self.tag, S % 192), []).append(
+                [t for op in sg.ops[n0:] for t in (op.text if isinstance(op.text, list) else [op.text])])
             bf += 1
         for i, op in enumerate(sg.ops):
             op.idx = i
@@ -877,6 +885,15 @@ def store_rows(dmap, base):
 
 EXEC_LO = [f"s_mov_b32 exec_hi, 0"]          # lanes 0..31 (assumes exec was all ones)
 EXEC_HI = [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
+
+
+def exec_block_half(ad, h):
+    """EXEC = the lanes of blocks i in [16 h, 16 h + 16): lanes 32 h .. 32 h + 31 in the lane-pair layouts 2 i + par,
+    lanes 16 h .. 16 h + 15 and 32 + 16 h .. 47 + 16 h in the W1x layouts i + 32 par (assumes exec was all ones)."""
+    if getattr(ad, "w1x", False):
+        m = "0xffff" if h == 0 else "0xffff0000"
+        return [f"s_mov_b32 exec_lo, {m}", f"s_mov_b32 exec_hi, {m}"]
+    return EXEC_LO if h == 0 else EXEC_HI
 EXEC_ALL = [f"s_mov_b64 exec, s[{S_EXE}:{S_EXE + 1}]"]
 
 
@@ -897,6 +914,24 @@ class Addr:
 NTT_ADDR = Addr(lambda bt, k, dst: f"global_load_dwordx2 {pv(dst)}, %[l8], s[{S_TB + 2 * bt}:{S_TB + 2 * bt + 1}] "
                                    f"offset:{512 * k}",
                 **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw", "t1x", "t1y")})
+
+# The forward's W1x layout (r6): the lane pair of block i is lanes i and i + 32 (lane = i + 32 j0) instead of 2 i and
+# 2 i + 1, so the lane-pair stage's regroup is two v_permlane32_swap_b32 per register pair (a half-wave exchange,
+# 8.2 cycles each) instead of four DPP moves and four selects (34.8 cycles).  Its transposes: T1 with row stride 33
+# (reads at (i 33 + j0 + 2 q) 8: conflict-free for both 32-lane groups), T2 with row stride 65 and the halves split by
+# i < 16 (lanes 0-15 and 32-47).  The per-lane addresses come from the kernel wrapper (ntt64_tw_device.hpp tw_body:
+# i = lane & 31, j0 = lane >> 5); the odd-lane mask s[S_PAR] becomes the upper half-wave.
+FWD_W1X = True
+INV_W1X = True   # the standalone inverse bodies' W1'' blocks in the same half-wave pairing (lane = i + 32 j5)
+NTT_ADDR_W1X = Addr(NTT_ADDR.tw_load, w1x=True,
+                    **{n: f"%[{n}]" for n in ("t1w", "t1r", "t2wl", "t2wh", "t2r", "t4w", "t4r", "lwo", "lw", "t1x", "t1y")})
+
+
+def par_mask(ad):
+    """s[S_PAR:S_PAR+1] = the lanes holding the odd member of each lane pair."""
+    if getattr(ad, "w1x", False):
+        return [f"s_mov_b32 s{S_PAR}, 0", f"s_mov_b32 s{S_PAR + 1}, -1"]
+    return [f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa"]
 
 
 FULL_STRIDE = 66  # row stride (u64) of the one-pass transposes of a wave with a 16.5 KiB LDS buffer (ad.full_t)
@@ -936,17 +971,18 @@ def t1(body, dmap, ybase, newhi, ad=NTT_ADDR, row_waits=None):
         assert row_waits is None
         return t1_full(body, dmap, ad)
     L = []
+    st = 33 if getattr(ad, "w1x", False) else 34  # row stride (u64): conflict-free reads in either lane-pair layout
     L += [f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"]
     for r in range(32):
         if row_waits:
             L.append(row_waits[r])
-        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * 34 * 8}")
+        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * st * 8}")
     L += EXEC_ALL
     for q in range(16):
         L.append(f"ds_read_b64 {pv(ybase + 2 * q)}, {ad.t1r} offset:{2 * q * 8}")
     L += [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"]
     for r in range(32):
-        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * 34 * 8}")
+        L.append(f"ds_write_b64 {ad.t1w}, {pv(dmap[r])} offset:{r * st * 8}")
     L += EXEC_ALL
     L.append("s_waitcnt lgkmcnt(0)")
     for q in range(16):
@@ -965,9 +1001,15 @@ def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
         assert len(free) >= 16, free
         ydst = free[:16]
     L = []
+    w1x = getattr(ad, "w1x", False)
+    rs = 65 if w1x else 66  # row stride (u64) of the W0 side
     for h in range(2):
-        L += ([f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"] if h == 0 else
-              [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"])
+        if w1x:  # the half of blocks i < 16 (h = 0) is lanes 0-15 and 32-47
+            m = "0xffff" if h == 0 else "0xffff0000"
+            L += [f"s_mov_b32 exec_lo, {m}", f"s_mov_b32 exec_hi, {m}"]
+        else:
+            L += ([f"s_mov_b32 exec_lo, -1", f"s_mov_b32 exec_hi, 0"] if h == 0 else
+                  [f"s_mov_b32 exec_lo, 0", f"s_mov_b32 exec_hi, -1"])
         for k in range(32):
             if pairs:
                 if k < 16:
@@ -982,7 +1024,7 @@ def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
         dst = ydst if h == 0 else [newhi + 2 * r for r in range(16)]
         rb = ad.t2r if pairs else ad.t4r
         for r in range(16):
-            L.append(f"ds_read_b64 {pv(dst[r])}, {rb} offset:{r * 66 * 8}")
+            L.append(f"ds_read_b64 {pv(dst[r])}, {rb} offset:{r * rs * 8}")
     L.append("s_waitcnt lgkmcnt(0)")
     body.raw(*L)
     return ydst + [newhi + 2 * r for r in range(16)]
@@ -994,7 +1036,7 @@ def t_iw0(body, dmap, pairs, ybase, newhi, ad=NTT_ADDR):
 REGROUP_DPP_SELECT = False
 
 
-def regroup(sg, dmap, k, tmp, to_pairs, k2=None):
+def regroup(sg, dmap, k, tmp, to_pairs, k2=None, w1x=False):
     """W1 <-> W1' for register pair (k, k2 = k+16) of this lane and its partner (lane ^ 1).
     to_pairs: even lane ends with (a_k, b_k), odd lane with (a_{k2}, b_{k2}).
     back:     even lane ends with (a_k, a_{k2}), odd lane with (b_k, b_{k2}).
@@ -1003,6 +1045,12 @@ def regroup(sg, dmap, k, tmp, to_pairs, k2=None):
     kk2 = k + 16 if k2 is None else k2
     lo0, hi0, p0 = X(dmap, k)
     lo1, hi1, p1 = X(dmap, kk2)
+    if w1x:
+        # W1x (lane = i + 32 par): one half-wave exchange per word moves the lower lanes' x[k2] up and the upper
+        # lanes' x[k] down — the same permutation in both directions (it is an involution)
+        sg.add(f"v_permlane32_swap_b32 {lo0}, {lo1}", [lo0, lo1], [lo0, lo1], "dpp")
+        sg.add(f"v_permlane32_swap_b32 {hi0}, {hi1}", [hi0, hi1], [hi0, hi1], "dpp")
+        return None
     T0, T1, U0, U1 = tmp
     par = f"s[{S_PAR}:{S_PAR + 1}]"
     dpp = "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
@@ -1209,7 +1257,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
             wlo, whi = f"v{wb[2 * i]}", f"v{wb[2 * i] + 1}"
             if pre and k in pre:  # twiddle loaded earlier, latency hidden behind the previous stages
                 wlo, whi = f"v{pre[k]}", f"v{pre[k] + 1}"
-            freed = regroup(sg, dmap, k, tmp, True)
+            freed = regroup(sg, dmap, k, tmp, True, w1x=getattr(ad, "w1x", False))
             if freed is not None:
                 tmps[i % 2][0:2] = [freed, freed + 1]
             a, b = X(dmap, k), X(dmap, k + 16)
@@ -1243,7 +1291,7 @@ def pair_stage(B, dmap, fwd, ad=NTT_ADDR, tabs=None, pre=None, busy=()):
                     tmul_lane(sg, E[k], E[k + 16], b, sl, b[0], b[1], par3, (wlo, whi))
                 else:
                     gmul(sg, m, b, wlo, whi, b[0], b[1])
-                freed = regroup(sg, dmap, k, [f"v{r}" for r in tmps[i % 2]], False)
+                freed = regroup(sg, dmap, k, [f"v{r}" for r in tmps[i % 2]], False, w1x=getattr(ad, "w1x", False))
                 if freed is not None:
                     tmps[i % 2][0:2] = [freed, freed + 1]
         for j, op in enumerate(sg.ops):
@@ -1295,6 +1343,7 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
         if s == 0 and PROGRESSIVE and prefetch:  # rows issued as pairs (k, k + 16), then the 8 twist-row loads
             gw = [f"s_waitcnt vmcnt({40 - 8 * (g + 1)})" for g in range(4)]
         modes = plan["fwd_g1"]["modes"][16 * s:16 * s + 16] if plan else None
+        B.tag = f"G1 stage {s}"
         B.stage("ct", 16 >> s, tabs["G1_FWD"][s], dmap, fb, group_waits=gw, modes=modes,
                 scales=g1_scales if plan else None)
     if plan:
@@ -1305,10 +1354,12 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
     # loads while batch bt multiplies), 2 multiply slots in v24..v47
     prog = getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T
     after = (lambda bt: t1_full_writes(dmap, ad, range(8 * bt, 8 * bt + 8))) if prog else None
+    B.tag = "twist"
     twist_rows(B, dmap, ad, [8, 48], [MulSlot(24 + 12 * i, SG0 + 6 * i) for i in range(2)], first_loaded=prefetch,
                after_batch=after)
     if stop == "twist":
         return dmap
+    B.tag = "T1 transpose"
     dmap = t1_full(B, dmap, ad, written=True) if prog else t1(B, dmap, 8, 64, ad)
     if stop == "t1":
         return dmap
@@ -1323,16 +1374,21 @@ def fwd_core(B, tabs, dmap, ad=NTT_ADDR, stop=None, prefetch=False, first_stage=
     cf = [True] * 32  # twist outputs are canonical
     cyc_scales = list(plan["fwd_cyc"]["in_scales"]) if plan else None
     for q in range(5):
+        B.tag = f"cyclic stage {q}"
         B.stage("ct", 16 >> q, tabs["CYC_FWD"][q], dmap, fb, cf, modes=plan["fwd_cyc"]["modes"][16 * q:16 * q + 16]
                 if plan else None, scales=cyc_scales)
     if plan:
         assert all(v % 192 == 0 for v in cyc_scales), "the cyclic blocks' outputs must be unscaled"
     if stop == "cyc":
         return dmap
+    B.tag = "lane-pair stage"
     pair_stage(B, dmap, True, ad, tabs, pre, busy)
     if stop == "last":
         return dmap
-    return t_iw0(B, dmap, True, 96, 64, ad)
+    B.tag = "T2 transpose"
+    dmap = t_iw0(B, dmap, True, 96, 64, ad)
+    B.tag = "store"
+    return dmap
 
 
 def gen_fwd(tabs, stop=None):
@@ -1340,17 +1396,18 @@ def gen_fwd(tabs, stop=None):
     dmap = [64 + 2 * r for r in range(32)]
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    ad = NTT_ADDR_W1X if FWD_W1X else NTT_ADDR
+    B.raw(*par_mask(ad))
     if PROGRESSIVE and not stop:
         rows = load_rows(dmap, S_GB)
         B.raw(*[rows[r] for k in range(16) for r in (k, k + 16)])
     else:
         B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     if FWD_STORE != "t2" and not stop:
-        dmap = fwd_core(B, tabs, dmap, stop="last", prefetch=True)
+        dmap = fwd_core(B, tabs, dmap, ad, stop="last", prefetch=True)
         B.raw(*direct_stores(dmap, FWD_STORE))
         return B
-    dmap = fwd_core(B, tabs, dmap, stop=stop, prefetch=True)
+    dmap = fwd_core(B, tabs, dmap, ad, stop=stop, prefetch=True)
     if stop:
         B.raw(*store_raw(dmap))
         return B
@@ -1391,7 +1448,8 @@ def gen_fwd_ms64(tabs):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111",
           f"s_mov_b32 s{S_H31}, 0x80000000")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB), *gen_bases("o", S_OB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    ad = NTT_ADDR_W1X if FWD_W1X else NTT_ADDR
+    B.raw(*par_mask(ad))
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
     sg = Seg()
     sls = B.slots(free_blocks_except(dmap))
@@ -1400,7 +1458,7 @@ def gen_fwd_ms64(tabs):
     for i, op in enumerate(sg.ops):
         op.idx = i
     B.out(sg.schedule())
-    dmap = fwd_core(B, tabs, dmap, prefetch=True)
+    dmap = fwd_core(B, tabs, dmap, ad, prefetch=True)
     B.raw(*store_rows(dmap, S_OB))
     return B
 
@@ -1472,7 +1530,7 @@ def t1_w1pp(body, dmap, dst, ad=NTT_ADDR):
         for rho in range(16):
             L.append(f"ds_write_b64 {ad.t1x}, {pv(dmap[16 * h + rho])} offset:{rho * 66 * 8}")
         L.append("s_waitcnt lgkmcnt(0)")
-        L += EXEC_LO if h == 0 else EXEC_HI
+        L += exec_block_half(ad, h)
         for r in range(32):
             L.append(f"ds_read_b64 {pv(dst[r])}, {ad.t1y} offset:{r * 8}")
         L += EXEC_ALL
@@ -1504,8 +1562,9 @@ def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR, written=False, reads_pendin
         body.raw(*L)
         return list(dmap)
     L = []
+    rs = 65 if getattr(ad, "w1x", False) else 66  # W1x: an odd row stride keeps the 16-lane write groups conflict-free
     for h in range(2):
-        L += EXEC_LO if h == 0 else EXEC_HI
+        L += exec_block_half(ad, h)
         for R in range(32):
             off = 2 * (R >> 1) + 33 * (R & 1)
             L.append(f"ds_write_b64 {ad.t4w}, {pv(dmap[R])} offset:{off * 8}")
@@ -1513,7 +1572,7 @@ def t_w1pp_w0(body, dmap, ybase, newhi, ad=NTT_ADDR, written=False, reads_pendin
         L.append("s_waitcnt lgkmcnt(0)")
         dst = ybase if h == 0 else newhi
         for rho in range(16):
-            L.append(f"ds_read_b64 {pv(dst + 2 * rho)}, {ad.t1x} offset:{rho * 66 * 8}")
+            L.append(f"ds_read_b64 {pv(dst + 2 * rho)}, {ad.t1x} offset:{rho * rs * 8}")
         L.append("s_waitcnt lgkmcnt(0)")
     body.raw(*L)
     return [ybase + 2 * r for r in range(16)] + [newhi + 2 * r for r in range(16)]
@@ -1548,7 +1607,7 @@ def pair_stage_dit(B, dmap, ad, pre, busy, after_half=None):
             mm = msl[i % 2]
             sl = slot_view(mm, c23[i % 2])
             Se, So = inv_last_exp(2 * m), inv_last_exp(2 * m + 1)
-            freed = regroup(sg, dmap, 2 * m, tmp, True, k2=2 * m + 1)
+            freed = regroup(sg, dmap, 2 * m, tmp, True, k2=2 * m + 1, w1x=getattr(ad, "w1x", False))
             if freed is not None:
                 tmps[i % 2][0:2] = [freed, freed + 1]
             a, b = X(dmap, 2 * m), X(dmap, 2 * m + 1)
@@ -1587,6 +1646,7 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
         dmap = w1p_as_w1pp(dmap)
     else:
         assert not getattr(ad, "full_t", False)
+        B.tag = "T1'' transpose"
         dmap = t1_w1pp(B, dmap, dst or [8 + 2 * r for r in range(32)], ad)
     ms = pair_stage_dit_gmul_ms()
     pre = {m: pre_base + 2 * i for i, m in enumerate(ms)}
@@ -1597,11 +1657,14 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
     fb = free_blocks_except(dmap, busy)
     cf = [True] * 32  # loaded data is canonical
     for s in range(5):
+        B.tag = f"cyclic stage {s}"
         B.stage("ct", 1 << s, dit_exps_pp(s), dmap, fb, cf, by_reg=True)
     prog = getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T
     after = (lambda h: t_w1pp_w0_full_writes(dmap, ad, range(16 * h, 16 * h + 16))) if prog else None
+    B.tag = "lane-pair stage"
     pair_stage_dit(B, dmap, ad, pre, busy, after_half=after)
     assert getattr(ad, "full_t", False) or not set(range(ybase, ybase + 32)) & {r for b in dmap for r in (b, b + 1)}
+    B.tag = "T2'' transpose"
     return t_w1pp_w0(B, dmap, ybase, newhi, ad, written=prog, reads_pending=prog)
 
 
@@ -1631,6 +1694,7 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=Fa
                 B.stage("gs", 16 >> q, tabs["CYC_INV"][q], dmap, fb, cf)
         dmap = t_iw0(B, dmap, False, 96, 64, ad)
     # untwist: table rows and multiply slots in the registers the data does not occupy
+    B.tag = "untwist"
     free = free_blocks_except(dmap, busy)
     regs = []
     for b in free:
@@ -1648,7 +1712,9 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=Fa
     fb = free_blocks_except(dmap)
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
+        B.tag = f"G1 stage {s}"
         B.stage("gs", 16 >> s, tabs["G1_INV"][s], dmap, fb, cf)
+    B.tag = "canonicalise + store"
     sg = Seg()
     sls = B.slots(fb)
     for k, r in enumerate([r for r in range(32) if not cf[r]]):
@@ -1664,10 +1730,11 @@ def gen_inv(tabs, stop=None):
     dmap = [64 + 2 * r for r in range(32)]
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    ad = NTT_ADDR_W1X if INV_W1X and INV_W1PP else NTT_ADDR
+    B.raw(*par_mask(ad))
     if INV_W1PP:
         B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-        dmap = inv_core(B, tabs, dmap, w1pp=True)
+        dmap = inv_core(B, tabs, dmap, ad, w1pp=True)
         B.raw(*store_rows(dmap, S_GB))
         return B
     gks = pair_stage_gmul_ks(tabs, False)
@@ -1809,9 +1876,10 @@ def gen_inv_mac(tabs, L, vhi=MAC_VHI):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
     mac_phase(B, L, dmap, vhi)
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    ad = NTT_ADDR_W1X if INV_W1X else NTT_ADDR
+    B.raw(*par_mask(ad))
     assert INV_W1PP
-    dmap = inv_core(B, tabs, dmap, w1pp=True)
+    dmap = inv_core(B, tabs, dmap, ad, w1pp=True)
     B.raw(*store_rows(dmap, S_GB))
     return B
 
@@ -1827,38 +1895,6 @@ WS_LS = (4, 6)   # l (k + 1) of the 3_3 and 4_4 shapes (k = 1, l = 2 / 3); other
 
 
 WS_OUT = (124, 126)   # the producer's row results alternate between these pairs (each row's hand-off write reads one)
-
-
-def gen_macp(tabs, L):
-    """Producer half: y's block row by row, each row written to the LDS hand-off buffer as soon as it is reduced (the
-    buffer is free: the consumer read the previous unit's rows before the last barrier), so the data registers join the
-    term ring (26 terms ahead instead of 11); then (1) the rows are complete, (2) the consumer has read them."""
-    B = Body(tabs)
-    dmap = [WS_OUT[r % 2] for r in range(32)]
-    bufs = mac_ring(MAC_VHI)[0] + [64 + 4 * k for k in range(15)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
-    mac_phase(B, L, dmap, bufs=bufs,
-              after_row=lambda r: [f"ds_write_b64 %[yw], {pv(WS_OUT[r % 2])} offset:{512 * r}"])
-    B.raw("s_waitcnt lgkmcnt(0)", "s_barrier", "s_barrier")
-    return B
-
-
-def gen_invc(tabs):
-    """Consumer half: (1) the rows are complete (its previous unit's stores drain meanwhile), the rows from the LDS
-    buffer, (2) released to the producer, then the inverse body (gen_inv_mac's after its MAC; its transposes in the
-    workgroup's second LDS region) and the stores."""
-    B = Body(tabs)
-    dmap = [64 + 2 * r for r in range(32)]
-    B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111")
-    B.raw("s_barrier", "s_waitcnt vmcnt(0)",
-          *[f"ds_read_b64 {pv(dmap[r])}, %[yw] offset:{512 * r}" for r in range(32)], "s_waitcnt lgkmcnt(0)",
-          "s_barrier")
-    B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
-    assert INV_W1PP
-    dmap = inv_core(B, tabs, dmap, w1pp=True)
-    B.raw(*store_rows(dmap, S_GB))
-    return B
 
 
 def emit(name, body, ops_in, sgpr_extra=(), vhi=None):

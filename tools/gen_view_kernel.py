@@ -33,11 +33,11 @@ from gen_tw_kernel import (JUNK, MS_SGPRS, S_EXE, S_GB, S_H31, S_OB, S_PAR, S_TB
                            modswitch_native, pv, store_rows)
 
 
-def _prologue(B, extra=()):
+def _prologue(B, ad, extra=()):
     B.raw(f"s_mov_b64 s[{S_EXE}:{S_EXE + 1}], exec", f"s_mov_b32 s{S_X15}, 0x11111111",
           f"s_mov_b32 s{S_H31}, 0x80000000", *extra)
     B.raw(*gen_bases("g", S_GB), *gen_bases("tw", S_TB), *gen_bases("o", S_OB))
-    B.raw(f"s_mov_b32 s{S_PAR}, 0xaaaaaaaa", f"s_mov_b32 s{S_PAR + 1}, 0xaaaaaaaa")
+    B.raw(*T.par_mask(ad))
 
 
 def _sched(B, sg):
@@ -67,7 +67,8 @@ def gen_fwd_view(tabs, kind):
     """Standard rows (%[g_*]) -> conversion -> forward transform -> NTT rows (%[o_*])."""
     B = Body(tabs)
     dmap = [64 + 2 * r for r in range(32)]
-    _prologue(B)
+    ad = T.NTT_ADDR_W1X if T.FWD_W1X else T.NTT_ADDR
+    _prologue(B, ad)
     if kind == "copy" and T.PROGRESSIVE:  # as gen_fwd: stage 0 starts as the row pairs (k, k + 16) land
         rows = load_rows(dmap, S_GB)
         B.raw(*[rows[r] for k in range(16) for r in (k, k + 16)])
@@ -79,7 +80,7 @@ def gen_fwd_view(tabs, kind):
         for r in range(32):
             (conv_pow2 if kind == "pow2" else conv_decomp)(sg, sls[r % len(sls)], X(dmap, r))
         _sched(B, sg)
-    dmap = fwd_core(B, tabs, dmap, prefetch=True)
+    dmap = fwd_core(B, tabs, dmap, ad, prefetch=True)
     B.raw(*store_rows(dmap, S_OB))  # no final vmcnt wait: the wave may retire while its stores drain
     return B
 
@@ -140,9 +141,10 @@ def gen_inv_view(tabs, kind):
     standard rows (%[o_*])."""
     B = Body(tabs)
     dmap = [64 + 2 * r for r in range(32)]
-    _prologue(B)
+    ad = T.NTT_ADDR_W1X if T.INV_W1X else T.NTT_ADDR
+    _prologue(B, ad)
     B.raw(*load_rows(dmap, S_GB), "s_waitcnt vmcnt(0)")
-    dmap = inv_core(B, tabs, dmap, w1pp=True)
+    dmap = inv_core(B, tabs, dmap, ad, w1pp=True)
     busy = {r for b in dmap for r in (b, b + 1)}
     assert not busy & set(range(8, 64)), "the epilogue expects the inverse's output in v64..v127"
     slots = B.slots(list(EPI_SLOTS))

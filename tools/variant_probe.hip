@@ -38,17 +38,21 @@ __global__ __launch_bounds__(64 * W) void probe_kernel(u64* __restrict__ data, u
   if (poly >= batch) return;
   u64* p = data + (uint64_t)poly * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
-  const uint32_t par = lane & 1, i = lane >> 1;
+  constexpr int W1X[] = MI_VARIANT_W1X;
+  // the lane pair: lanes 2i, 2i + 1 (W1 / W1'') or i, i + 32 (W1x, r6)
+  const bool x = W1X[V];
+  const uint32_t par = x ? lane >> 5 : lane & 1, i = x ? lane & 31 : lane >> 1;
   const uint32_t l8 = lane * 8;
   const uint32_t t1w = S + (lane & 31) * 8;
-  const uint32_t t1r = S + (i * 34 + par) * 8;
+  const uint32_t t1r = S + (i * (x ? 33 : 34) + par) * 8;
   const uint32_t lwo = par * 128;
   const uint32_t glo = (uint32_t)(uintptr_t)p, ghi = (uint32_t)((uintptr_t)p >> 32);
   const uint32_t twlo = (uint32_t)(uintptr_t)twist, twhi = (uint32_t)((uintptr_t)twist >> 32);
   const u64* lw = twist + 2048;
   if constexpr (FWD) {
-    const uint32_t t2wl = S + ((i & 15) * 66 + 33 * par) * 8;
-    const uint32_t t2wh = S + ((i & 15) * 66 + 31 * par + 1) * 8;
+    const uint32_t rs = x ? 65 : 66;
+    const uint32_t t2wl = S + ((i & 15) * rs + 33 * par) * 8;
+    const uint32_t t2wh = S + ((i & 15) * rs + 31 * par + 1) * 8;
     const uint32_t t2r = S + (lane ^ (lane >> 5)) * 8;
     const uint32_t pso = i * 512 + par * 256;
     if constexpr (V == 0) MI_TW_BODY_FWD_V0(FWD_ARGS);
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(64 * W) void probe_kernel(u64* __restrict__ data, u
     if constexpr (V == 2) MI_TW_BODY_FWD_V2(FWD_ARGS);
     if constexpr (V == 3) MI_TW_BODY_FWD_V3(FWD_ARGS);
   } else {
-    const uint32_t t4w = S + ((i & 15) * 66 + par) * 8;
+    const uint32_t t4w = S + ((i & 15) * (x ? 65 : 66) + par) * 8;
     const uint32_t t4r = S + lane * 8;
     const uint32_t t1x = S + (lane + (lane >> 5)) * 8;
     const uint32_t t1y = S + ((i & 15) * 66 + 33 * par) * 8;
