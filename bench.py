@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # Integer-VALU issue model of the generated bodies (tools/valu_cost.py: instruction mix x the issue
 # costs measured by tools/valu_probe.hip; tests/test_bench_contract.py keeps these in sync), and the
 # MI355X peak engine clock it is priced at.
-VALU_CYCLES = {"fwd": 13631.3, "inv": 14158.8, "pbs_step": 35057.4, "pbs_sol_step": 35378.7, "ext_bnf": 33868.5}
+VALU_CYCLES = {"fwd": 13631.3, "inv": 14158.8, "pbs_step": 35057.4, "pbs_sol_step": 35378.7, "ext_bnf": 33859.1}
 SIMDS, PEAK_CLOCK_HZ = 256 * 4, 2.4e9
 # PARAM_MESSAGE_2_CARRY_2 shape (ks_pbs.rs:29-47)
 PBS_N_LWE, PBS_BASE_LOG, PBS_LEVEL, PBS_BATCH = 918, 23, 1, 4096

@@ -191,8 +191,9 @@ def test_view_strided_batch(engine, oracle):
     ctx = _ctx(oracle, n)
     x = _std_input(oracle, 0x5300, batch, n)
     buf = torch.full((batch, stride), 7, dtype=torch.int64, device="cuda")
-    src = dev(x)
-    view.forward(buf[:, :n], src)
+    src = torch.full((batch, stride), 5, dtype=torch.int64, device="cuda")  # both operands share one row stride
+    src[:, :n] = dev(x)
+    view.forward(buf[:, :n], src[:, :n])
     got = host(buf)
     assert np.array_equal(got[:, :n], ctx.forward(x)) and (got[:, n:] == 7).all()
     st = torch.full((batch, stride), 0, dtype=torch.int64, device="cuda")

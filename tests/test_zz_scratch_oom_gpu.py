@@ -48,13 +48,15 @@ def test_small_request_served_when_device_memory_is_full(engine, oracle):
     torch.cuda.empty_cache()
     assert M.scratch_bytes(0) >= 1 << 30
     held = []
+    small_out.zero_()
     try:
         held = _fill_device(torch, dev)
-        small_out.zero_()
         KS.keyswitch_lwe_ciphertext(key, small_in, small_out)  # its new 1 MiB block cannot be allocated
         torch.cuda.synchronize()
-        assert torch.equal(small_out, want)
     finally:
         del held
         torch.cuda.empty_cache()
         M.scratch_trim(0)
+    # compared once the card has room again: torch's own comparison kernel loads its code object lazily, which needs
+    # device memory
+    assert torch.equal(small_out, want)

@@ -219,7 +219,10 @@ __global__ __launch_bounds__(128) void pbs_tw_sol_kernel(u64* __restrict__ lwe_o
 }
 
 // external product / CMUX batch (config 3): one workgroup per GLWE pair, wave w on polynomial w;
-// SOL: GLWEs modulo p with a Normalize GGSW (ntt64_pbs.rs:553-702), else BNF (native GLWEs, Raw GGSW)
+// SOL: GLWEs modulo p with a Normalize GGSW (ntt64_pbs.rs:553-702), else BNF (native GLWEs, Raw GGSW).
+// r6: the bodies use v0..v167 (MI_EXT_VGPRS) and 8.5 KiB of LDS per wave (the half-wave transposes, the partner
+// exchange in two 16-row halves), so three waves fit per SIMD instead of the blind-rotation bodies' two
+// (tools/gen_pbs_kernel.py set_regmap / mac_ext).
 template <bool CMUX, bool SOL>
 __device__ __forceinline__ void ext_tw_item(u64* __restrict__ out, u64* __restrict__ glwe, const u64* __restrict__ ggsw,
                                             uint32_t b, int base_log, const u64* __restrict__ tab, u64* buf,

@@ -25,6 +25,9 @@ Register map (the body owns v8..v255, s20..s31, s36..s93):
   v8..v127 transform data + scratch, v128..v191 acc, v192..v195 lane*8 + 4096 m (row-group offsets),
   v196..v203 per-lane LDS addresses of the transposes, v204 S, v205 partner exchange address,
   v206 rotation offset, v207 0x7fffffff, v208..v239 GGSW prefetch, v240..v247 partner rows.
+The external-product / CMUX bodies (r6) use a second map below v168 (set_regmap / mac_ext): no accumulator held
+through the step, the fixed registers in v128..v163, the GGSW chunks in the forward's free scratch, the partner
+exchange in 16-row halves; three waves per SIMD.
 
 Usage: python tools/gen_pbs_kernel.py > tfhe-rs-main_modified_amd/csrc/pbs_tw_body.hpp
 """
@@ -64,26 +67,51 @@ def addr_for(tab):
                 t4w=f"v{V_T4W}", t4r=f"v{V_T4R}", lwo=f"v{V_LWO}", lw=sp(tab), t1x=f"v{V_T1X}", t1y=f"v{V_T2WL}")
 
 
-FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
 # The blind-rotation bodies own 16.5 KiB of LDS per wave (PBS_LDS_STRIDE u64): their forward T1 and inverse W1'' -> W0
 # transposes run in one pass through a 32 x 66 tile (gen_tw_kernel.t1_full) instead of two lane halves with exec flips
 # and three waits.  V_TB = S + 8 (66 (lane >> 1) + (lane & 1)); the tile's other address is V_T4R = S + 8 lane.
 PBS_FULL_T = True
 PBS_LDS_STRIDE = 32 * 66 if PBS_FULL_T else 2048   # u64 per wave buffer (pbs_tw.hip MI_PBS_LDS_STRIDE)
 V_TB = 250
-FWD_ADDR_P, INV_ADDR_P = addr_for(S_TWF), addr_for(S_TWI)
-for _a in (FWD_ADDR_P, INV_ADDR_P):
-    _a.full_t, _a.tfw, _a.tfb = PBS_FULL_T, f"v{V_T4R}", f"v{V_TB}"
 # the lane-pair twiddles (32 forward + the inverse's 32 last-DIT-stage twiddles of the W1'' layout) live in the
 # workgroup's LDS (copied by pbs_tw.hip at kernel start): lookups at LDS instead of L2 latency.
 # V_LWL = table base + 128 * (lane & 1).
 V_LWL = 248
-for _a in (FWD_ADDR, FWD_ADDR_P):
-    _a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
-for _a in (INV_ADDR, INV_ADDR_P):
-    _a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
-for _a in (FWD_ADDR, INV_ADDR, FWD_ADDR_P, INV_ADDR_P):
-    _a.lw_wait = "s_waitcnt lgkmcnt(0)"
+
+
+def build_addrs():
+    """The transform cores' address objects for the current register map (set_regmap)."""
+    global FWD_ADDR, INV_ADDR, FWD_ADDR_P, INV_ADDR_P
+    FWD_ADDR, INV_ADDR = addr_for(S_TWF), addr_for(S_TWI)
+    FWD_ADDR_P, INV_ADDR_P = addr_for(S_TWF), addr_for(S_TWI)
+    for a in (FWD_ADDR_P, INV_ADDR_P):
+        a.full_t, a.tfw, a.tfb = PBS_FULL_T, f"v{V_T4R}", f"v{V_TB}"
+    for a in (FWD_ADDR, FWD_ADDR_P):
+        a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{8 * k}"
+    for a in (INV_ADDR, INV_ADDR_P):
+        a.lw_load = lambda dst, k: f"ds_read_b64 {pv(dst)}, v{V_LWL} offset:{256 + 8 * k}"
+    for a in (FWD_ADDR, INV_ADDR, FWD_ADDR_P, INV_ADDR_P):
+        a.lw_wait = "s_waitcnt lgkmcnt(0)"
+
+
+build_addrs()
+
+# The external-product / CMUX bodies' register map (r6, EXT_VGPRS): everything below v168, so three waves fit per SIMD
+# (512 / 168) instead of two.  The 32 out rows are not held through the step (they are read at the end, 16 rows at a
+# time, into the registers the inverse leaves free), the GGSW chunks land in the scratch the forward leaves free (two
+# multiply slots instead of four), and the fixed registers pack into v128..v163.
+EXT_VGPRS = 168
+_PBS_MAP = dict(VOFF=192, V_T1W=196, V_T1R=197, V_LWO=198, V_T2WL=199, V_T2WH=200, V_T2R=201, V_T4W=202, V_T4R=203,
+                V_S=204, V_PX=205, V_U8=206, V_HHI=207, GBUF=208, PBUF=240, V_LWL=248, V_T1X=249, V_TB=250)
+_EXT_MAP = dict(VOFF=128, V_T1W=132, V_T1R=133, V_LWO=134, V_T2WL=135, V_T2WH=136, V_T2R=137, V_T4W=138, V_T4R=139,
+                V_S=140, V_PX=141, V_U8=142, V_HHI=143, V_LWL=144, V_T1X=145, V_TB=146, PBUF=148, GBUF=96)
+EXT_PBUF2 = 156   # the partner rows' second buffer (MAC_PARTNER_AHEAD) in the ext map
+EXT_LDS_STRIDE = 1088   # u64 per wave: the half-wave transposes (32 x 34, 16 x 66) and a 16-row exchange half
+
+
+def set_regmap(ext):
+    globals().update(_EXT_MAP if ext else _PBS_MAP)
+    build_addrs()
 
 
 def sched(B, sg):
@@ -144,6 +172,16 @@ def load_rows(dst, base):
 def store_rows(src, base):
     return [f"global_store_dwordx2 v{VOFF + r // 8}, {pv(src + 2 * r)}, {sp(base)} offset:{512 * (r % 8)}{T.STORE_POLICY}"
             for r in range(32)]
+
+
+def load_rows_sub(dst, base, rows):
+    return [f"global_load_dwordx2 {pv(dst + 2 * q)}, v{VOFF + r // 8}, {sp(base)} offset:{512 * (r % 8)}"
+            for q, r in enumerate(rows)]
+
+
+def store_rows_sub(src, base, rows):
+    return [f"global_store_dwordx2 v{VOFF + r // 8}, {pv(src + 2 * q)}, {sp(base)} offset:{512 * (r % 8)}{T.STORE_POLICY}"
+            for q, r in enumerate(rows)]
 
 
 def gload(c):
@@ -411,6 +449,42 @@ def mac(B, dmap):
     B.raw("s_barrier")
 
 
+def mac_ext(B, dmap):
+    """The MAC of the ext-map bodies (set_regmap(True)): the exchange with the partner wave in two halves of 16 rows
+    (8 KiB of LDS per wave instead of 16), the GGSW chunks double-buffered in the forward's free scratch (GBUF = v96),
+    two multiply slots in v40..v63, the partner rows in PBUF / EXT_PBUF2.  dmap: the forward's W1' output in
+    v8..v39 + v64..v95 (the non-full_t transposes)."""
+    assert dmap == [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)], dmap
+    ms = [MulSlot(40, SG0), MulSlot(52, SG0 + 6)]
+    B.raw(*gload(0), *gload(1))
+    B.raw(*[f"v_mov_b32 {m.v[z]}, 0" for m in ms for z in (9, 11)])
+    pbufs = [PBUF, EXT_PBUF2]
+    pread = lambda c: [f"ds_read_b64 {pv(pbufs[c % 2] + 2 * k)}, v{V_PX} offset:{512 * (4 * (c % 4) + k)}"
+                       for k in range(4)]
+    for h in range(2):
+        if h:  # the partner has read this wave's first half
+            B.raw("s_barrier")
+        B.raw(*[f"ds_write_b64 v{V_T4R}, {pv(dmap[16 * h + q])} offset:{512 * q}" for q in range(16)],
+              "s_waitcnt lgkmcnt(0)", "s_barrier", *pread(4 * h))
+        for c in range(4 * h, 4 * h + 4):
+            nxt = pread(c + 1) if c + 1 < 4 * h + 4 else []
+            B.raw(*nxt, f"s_waitcnt vmcnt({8 if c < 7 else 0}) lgkmcnt({len(nxt)})")
+            pb = pbufs[c % 2]
+            sg = Seg()
+            gb = GBUF + 16 * (c % 2)
+            for k in range(4):
+                r = 4 * c + k
+                m1, m2 = ms
+                x = X(dmap, r)
+                pl, ph = f"v{pb + 2 * k}", f"v{pb + 2 * k + 1}"
+                mac2(sg, m1, m2, x, (f"v{gb + 2 * k}", f"v{gb + 2 * k + 1}"), (pl, ph, pv(pb + 2 * k)),
+                     (f"v{gb + 8 + 2 * k}", f"v{gb + 9 + 2 * k}"))
+            sched(B, sg)
+            if c + 2 < 8:
+                B.raw(*gload(c + 2))
+    B.raw("s_barrier")
+
+
 def w1pp_regs(dmap):
     """Register plan of the W1'' inverse after the MAC (dmap: rows 0..15 at v96.., rows 16..31 at v64..): the
     transposed data in v8..v63 + the first four pairs of rows 0..15, the lane-pair twiddles in v64..v71 (rows
@@ -419,14 +493,16 @@ def w1pp_regs(dmap):
     return dict(dst=[8 + 2 * r for r in range(28)] + [96 + 2 * r for r in range(4)], pre_base=64, ybase=64, newhi=96)
 
 
-def modswitch_acc(B, dmap):
+def modswitch_acc(B, dmap, rows=range(32), acc=None, sls=None):
+    """acc += ms_{p -> 2^64}(y) for the rows of y (dmap); acc[r] at `acc` + 2 q for the q-th row (default ACC + 2 r)."""
     sg = Seg()
-    sls = B.slots(free_blocks_except(dmap))
-    for r in range(32):
-        sl = sls[r % len(sls)]
+    sls = sls or B.slots(free_blocks_except(dmap))
+    for q, r in enumerate(rows):
+        sl = sls[q % len(sls)]
         v, P, c = sl.v, sl.P, sl.c
         vl, vh, _ = X(dmap, r)
-        al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+        a = ACC + 2 * r if acc is None else acc + 2 * q
+        al, ah = f"v{a}", f"v{a + 1}"
         sg.add(f"v_sub_co_u32_e64 {v[0]}, {c[0]}, s{S_HLO}, {vh}", [vh], [v[0], c[0]])
         sg.add(f"v_subb_co_u32_e64 {v[1]}, {JUNK}, v{V_HHI}, 0, {c[0]}", [c[0]], [v[1], JUNK])
         sg.add(f"v_mad_u64_u32 {P[1]}, {c[1]}, {vl}, -1, {P[0]}", [vl, P[0]], [P[1], c[1]])
@@ -439,15 +515,16 @@ def modswitch_acc(B, dmap):
     sched(B, sg)
 
 
-def add_acc_sol(B, dmap):
+def add_acc_sol(B, dmap, rows=range(32), acc=None, sls=None):
     """acc <- acc + y mod p, canonical (both canonical): ntt64.rs:244-266 add_backward, custom modulus."""
     sg = Seg()
-    sls = B.slots(free_blocks_except(dmap))
-    for r in range(32):
-        sl = sls[r % len(sls)]
+    sls = sls or B.slots(free_blocks_except(dmap))
+    for q, r in enumerate(rows):
+        sl = sls[q % len(sls)]
         v, P, c = sl.v, sl.P, sl.c
         vl, vh, _ = X(dmap, r)
-        al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
+        a = ACC + 2 * r if acc is None else acc + 2 * q
+        al, ah = f"v{a}", f"v{a + 1}"
         sg.add(f"v_add_co_u32_e64 {v[0]}, {c[0]}, {al}, {vl}", [al, vl], [v[0], c[0]])
         sg.add(f"v_addc_co_u32_e64 {v[1]}, {c[0]}, {ah}, {vh}, {c[0]}", [ah, vh, c[0]], [v[1], c[0]])
         sg.add(f"v_mad_u64_u32 {P[1]}, {c[1]}, -1, 1, {P[0]}", [P[0]], [P[1], c[1]])
@@ -474,13 +551,14 @@ def tw_key_index(pos):
     return 64 * (L >> 1) + 32 * (L & 1) + 2 * (R & 15) + (R >> 4)
 
 
-def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False):
+def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False, ext=False):
     """Forward transform (its stage 0 already run), the MAC with the partner wave and the inverse; returns the output
-    dmap (W0, canonical).  w1p: the MAC and the inverse's input stay in the forward's W1' layout (PBS_W1P)."""
+    dmap (W0, canonical).  w1p: the MAC and the inverse's input stay in the forward's W1' layout (PBS_W1P).  ext: the
+    ext-map MAC (mac_ext)."""
     if w1p:
         fa, ia = (FWD_ADDR_P, INV_ADDR_P) if full_t else (FWD_ADDR, INV_ADDR)
         dmap = T.fwd_core(B, tabs, dmap0, fa, first_stage=1, stop="last")
-        mac(B, dmap)
+        (mac_ext if ext else mac)(B, dmap)
         assert dmap == ([64 + 2 * q for q in range(32)] if full_t else
                         [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)]), dmap
         return T.inv_core(B, tabs, dmap, ia, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64))
@@ -540,13 +618,21 @@ def gen_pbs(tabs, sol=False):
 # costs about what the two skipped transposes saved), with them 27.70 -> 28.02 M products/s, +1.2 %
 # (profiles/r3/ext_w1p_full_t_ab/)
 EXT_W1P = True
-EXT_PROGRESSIVE = True  # external product: decompose + first stage per group of rows as they arrive
 
 
 def gen_ext(tabs, cmux, sol=False):
     """One external product (cmux=False: out += GGSW . glwe) or CMUX (glwe -= out, then
     out += GGSW . glwe), level 1; wave w handles polynomial w of one GLWE pair.  BNF (native GLWEs, Raw
-    GGSW) or Solinas (sol: GLWEs mod p, Normalize GGSW, ntt64_pbs.rs:553-702)."""
+    GGSW) or Solinas (sol: GLWEs mod p, Normalize GGSW, ntt64_pbs.rs:553-702).  Built on the ext register map
+    (set_regmap(True): below v168, 8.5 KiB of LDS per wave)."""
+    set_regmap(True)
+    try:
+        return _gen_ext(tabs, cmux, sol)
+    finally:
+        set_regmap(False)
+
+
+def _gen_ext(tabs, cmux, sol):
     B = Body(tabs)
     prologue(B)
     S_GL, S_OUT = S_LWE, S_A
@@ -557,70 +643,61 @@ def gen_ext(tabs, cmux, sol=False):
         B.raw(f"s_add_u32 s{S_TWI}, %[tab_lo], {2 * 2080 * 8}", f"s_addc_u32 s{S_TWI + 1}, %[tab_hi], 0")
     B.raw(f"s_mov_b32 s{S_GL}, %[glwe_lo]", f"s_mov_b32 s{S_GL + 1}, %[glwe_hi]",
           f"s_mov_b32 s{S_OUT}, %[out_lo]", f"s_mov_b32 s{S_OUT + 1}, %[out_hi]")
-    if cmux:  # ct1 -= ct0 needs the out rows (ct0) first
-        B.raw(*load_rows(64, S_GL), *load_rows(ACC, S_OUT), *gload(0), *gload(1), "s_waitcnt vmcnt(16)")
-    elif EXT_PROGRESSIVE:
-        # the GLWE rows in butterfly-pair order (r, r + 16), then the first two GGSW chunks; the decomposition and
-        # the first forward stage run in 4 groups of 4 pairs as their rows arrive (loads return in issue order), and
-        # the out rows — read only by the final accumulate — are issued after them (the MAC's chunk waits
-        # over-cover them, which is safe)
+    dmap0 = [64 + 2 * r for r in range(32)]
+    sls7 = slots_at([8, 16, 24, 32, 40, 48, 56])
+    sls3 = slots_at([40, 48, 56])   # beside the glwe rows (v64..) and a 16-row half of the out rows (v8..v39)
+    dec = decompose_sol if sol else decompose
+    if cmux:  # ct1 -= ct0 (ntt64_bnf_pbs.rs:683-705 wrapping; ntt64_pbs.rs:669-680 mod p), the out rows 16 at a time
+        B.raw(*load_rows(64, S_GL))
+        for h in range(2):
+            rows = range(16 * h, 16 * h + 16)
+            B.raw(*load_rows_sub(8, S_OUT, rows), "s_waitcnt vmcnt(0)")
+            sg = Seg()
+            for q, r in enumerate(rows):
+                sl = sls3[q % len(sls3)]
+                xl, xh = f"v{64 + 2 * r}", f"v{65 + 2 * r}"
+                al, ah = f"v{8 + 2 * q}", f"v{9 + 2 * q}"
+                if sol:
+                    sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[0]}, {xl}, {al}", [xl, al], [xl, sl.c[0]])
+                    sg.add(f"v_subb_co_u32_e64 {xh}, {sl.c[1]}, {xh}, {ah}, {sl.c[0]}", [xh, ah, sl.c[0]],
+                           [xh, sl.c[1]])
+                    minus_eps(sg, sl.v[5], sl.c[1], pv(64 + 2 * r))
+                else:
+                    sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[1]}, {xl}, {al}", [xl, al], [xl, sl.c[1]])
+                    sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {sl.c[1]}", [xh, ah, sl.c[1]], [xh, JUNK])
+            sched(B, sg)
+        B.raw(*store_rows(64, S_GL))
+        sg = Seg()
+        for r in range(32):
+            dec(sg, sls7[r % len(sls7)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
+        sched(B, sg)
+        stage0_signed(B, tabs, dmap0)
+    else:
+        # the GLWE rows in butterfly-pair order (r, r + 16); the decomposition and the first forward stage run in 4
+        # groups of 4 pairs as their rows arrive (loads return in issue order)
         rows = load_rows(64, S_GL)
-        B.raw(*[rows[q] for k in range(16) for q in (k, k + 16)], *gload(0), *gload(1))
-        sls = slots_at([8, 16, 24, 32, 40, 48, 56])
-        dmap0 = [64 + 2 * r for r in range(32)]
+        B.raw(*[rows[q] for k in range(16) for q in (k, k + 16)])
         for g in range(4):
-            B.raw(f"s_waitcnt vmcnt({16 + 32 - 8 * (g + 1)})")
+            B.raw(f"s_waitcnt vmcnt({32 - 8 * (g + 1)})")
             sg = Seg()
             for k in range(4 * g, 4 * g + 4):
                 for r in (k, k + 16):
-                    (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}",
-                                                          signed=True)
+                    dec(sg, sls7[r % len(sls7)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
             sched(B, sg)
             stage0_signed(B, tabs, dmap0, rows=range(4 * g, 4 * g + 4))
-        B.raw(*load_rows(ACC, S_OUT))
-        dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P, full_t=EXT_W1P and PBS_FULL_T)
-        if sol:
-            add_acc_sol(B, dmap)
-        else:
-            modswitch_acc(B, dmap)
-        B.raw(*store_rows(ACC, S_OUT))
-        return B
-    else:  # the out rows are only read by the final accumulate: issued last, waited for only by the MAC's waits
-        # (vmcnt waits for at most the count given, so the MAC's chunk waits over-cover them, which is safe)
-        B.raw(*load_rows(64, S_GL), *gload(0), *gload(1), *load_rows(ACC, S_OUT), "s_waitcnt vmcnt(48)")
-    sg = Seg()
-    sls = slots_at([8, 16, 24, 32, 40, 48, 56])
-    for r in range(32):
-        sl = sls[r % len(sls)]
-        xl, xh = f"v{64 + 2 * r}", f"v{65 + 2 * r}"
-        if cmux and sol:  # ct1 -= ct0 mod p (ntt64_pbs.rs:669-680)
-            al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
-            sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[0]}, {xl}, {al}", [xl, al], [xl, sl.c[0]])
-            sg.add(f"v_subb_co_u32_e64 {xh}, {sl.c[1]}, {xh}, {ah}, {sl.c[0]}", [xh, ah, sl.c[0]], [xh, sl.c[1]])
-            minus_eps(sg, sl.v[5], sl.c[1], pv(64 + 2 * r))
-        elif cmux:  # ct1 -= ct0 (ntt64_bnf_pbs.rs:683-705, wrapping)
-            al, ah = f"v{ACC + 2 * r}", f"v{ACC + 2 * r + 1}"
-            sg.add(f"v_sub_co_u32_e64 {xl}, {sl.c[1]}, {xl}, {al}", [xl, al], [xl, sl.c[1]])
-            sg.add(f"v_subb_co_u32_e64 {xh}, {JUNK}, {xh}, {ah}, {sl.c[1]}", [xh, ah, sl.c[1]], [xh, JUNK])
-    sched(B, sg)
-    if cmux:
-        B.raw(*store_rows(64, S_GL))
-    sg = Seg()
-    for r in range(32):
-        (decompose_sol if sol else decompose)(sg, sls[r % len(sls)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
-    sched(B, sg)
-    stage0_signed(B, tabs, [64 + 2 * r for r in range(32)])
-    dmap = fwd_mac_inv(B, tabs, [64 + 2 * r for r in range(32)], EXT_W1P, full_t=EXT_W1P and PBS_FULL_T)
-    if sol:
-        add_acc_sol(B, dmap)
-    else:
-        modswitch_acc(B, dmap)
-    B.raw(*store_rows(ACC, S_OUT))  # no final wait: the wave retires while its stores drain
+    dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P, full_t=False, ext=True)
+    # out += y, 16 rows at a time: rows 0..15 (y in v96..) through v8..v39, rows 16..31 (y in v64..) through v96..v127
+    assert dmap == [96 + 2 * r for r in range(16)] + [64 + 2 * r for r in range(16)], dmap
+    for h, base in ((0, 8), (1, 96)):
+        rows = list(range(16 * h, 16 * h + 16))
+        B.raw(*load_rows_sub(base, S_OUT, rows), "s_waitcnt vmcnt(0)")
+        (add_acc_sol if sol else modswitch_acc)(B, dmap, rows, base, sls3)
+        B.raw(*store_rows_sub(base, S_OUT, rows))  # no final wait: the wave retires while its stores drain
     return B
 
 
-def emit(name, body, sgprs=SGPR_CLOBBER):
-    clob = ([f'"v{i}"' for i in range(8, 256)] + [f'"s{i}"' for i in sgprs] + ['"scc"', '"memory"'] +
+def emit(name, body, sgprs=SGPR_CLOBBER, vgprs=256):
+    clob = ([f'"v{i}"' for i in range(8, vgprs)] + [f'"s{i}"' for i in sgprs] + ['"scc"', '"memory"'] +
             (['"vcc"'] if T.REGROUP_DPP_SELECT else []))
     return (f"// {name}: {body.nvalu} VALU, {len(body.lines)} lines\n"
             f"#define MI_PBS_BODY_{name.upper()}(...) asm volatile(\\\n" +
@@ -638,16 +715,17 @@ def main():
     print(f"#define MI_PBS_W1P {int(PBS_W1P)}  // blind rotation reads its key in the W1' order (tw_key_index)")
     print(f"#define MI_EXT_W1P {int(EXT_W1P)}  // external product / CMUX read their GGSW in the W1' order")
     print(f"#define MI_PBS_LDS_STRIDE {PBS_LDS_STRIDE}  // u64 per wave LDS buffer of the blind-rotation bodies")
-    print(f"#define MI_EXT_LDS_STRIDE {PBS_LDS_STRIDE if EXT_W1P else 2048}  // u64 per wave LDS buffer of the external-product bodies")
+    print(f"#define MI_EXT_LDS_STRIDE {EXT_LDS_STRIDE}  // u64 per wave LDS buffer of the external-product bodies")
+    print(f"#define MI_EXT_VGPRS {EXT_VGPRS}  // the external-product bodies use v0..v{EXT_VGPRS - 1} (3 waves per SIMD)")
     print(emit("bnf_l1", b))
     e, c = gen_ext(tabs, False), gen_ext(tabs, True)
-    print(emit("ext_bnf_l1", e))
-    print(emit("cmux_bnf_l1", c))
+    print(emit("ext_bnf_l1", e, vgprs=EXT_VGPRS))
+    print(emit("cmux_bnf_l1", c, vgprs=EXT_VGPRS))
     bs = gen_pbs(tabs, sol=True)
     es, cs = gen_ext(tabs, False, sol=True), gen_ext(tabs, True, sol=True)
     print(emit("sol_l1", bs, SGPR_CLOBBER_SOL))
-    print(emit("ext_sol_l1", es, SGPR_CLOBBER_SOL))
-    print(emit("cmux_sol_l1", cs, SGPR_CLOBBER_SOL))
+    print(emit("ext_sol_l1", es, SGPR_CLOBBER_SOL, EXT_VGPRS))
+    print(emit("cmux_sol_l1", cs, SGPR_CLOBBER_SOL, EXT_VGPRS))
     print(f"// pbs step {b.nvalu} VALU, ext {e.nvalu}, cmux {c.nvalu}; Solinas pbs step {bs.nvalu}, ext {es.nvalu}, "
           f"cmux {cs.nvalu}", file=sys.stderr)
 
