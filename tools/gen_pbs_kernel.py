@@ -551,7 +551,7 @@ def tw_key_index(pos):
     return 64 * (L >> 1) + 32 * (L & 1) + 2 * (R & 15) + (R >> 4)
 
 
-def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False, ext=False):
+def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False, ext=False, inv_kw=None):
     """Forward transform (its stage 0 already run), the MAC with the partner wave and the inverse; returns the output
     dmap (W0, canonical).  w1p: the MAC and the inverse's input stay in the forward's W1' layout (PBS_W1P).  ext: the
     ext-map MAC (mac_ext)."""
@@ -561,7 +561,8 @@ def fwd_mac_inv(B, tabs, dmap0, w1p, full_t=False, ext=False):
         (mac_ext if ext else mac)(B, dmap)
         assert dmap == ([64 + 2 * q for q in range(32)] if full_t else
                         [8 + 2 * q for q in range(16)] + [64 + 2 * q for q in range(16)]), dmap
-        return T.inv_core(B, tabs, dmap, ia, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64))
+        return T.inv_core(B, tabs, dmap, ia, w1pp=True, w1pp_regs=dict(w1p_in=True, pre_base=40, ybase=96, newhi=64),
+                          **(inv_kw or {}))
     dmap = T.fwd_core(B, tabs, dmap0, FWD_ADDR, first_stage=1)
     mac(B, dmap)
     return T.inv_core(B, tabs, dmap, INV_ADDR, w1pp=True, w1pp_regs=w1pp_regs(dmap))
@@ -685,12 +686,14 @@ def _gen_ext(tabs, cmux, sol):
                     dec(sg, sls7[r % len(sls7)], f"v{64 + 2 * r}", f"v{65 + 2 * r}", signed=True)
             sched(B, sg)
             stage0_signed(B, tabs, dmap0, rows=range(4 * g, 4 * g + 4))
-    dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P, full_t=False, ext=True)
-    # out += y, 16 rows at a time: rows 0..15 (y in v96..) through v8..v39, rows 16..31 (y in v64..) through v96..v127
+    # out += y, 16 rows at a time: rows 0..15 (y in v96..) through v8..v39, loaded while the inverse's G1 stages run
+    # (which keep to v40..v63 for their scratch), then rows 16..31 (y in v64..) through v96..v127
+    dmap = fwd_mac_inv(B, tabs, dmap0, EXT_W1P, full_t=False, ext=True,
+                       inv_kw=dict(g1_busy=range(8, 40), before_g1=load_rows_sub(8, S_OUT, range(16))))
     assert dmap == [96 + 2 * r for r in range(16)] + [64 + 2 * r for r in range(16)], dmap
     for h, base in ((0, 8), (1, 96)):
         rows = list(range(16 * h, 16 * h + 16))
-        B.raw(*load_rows_sub(base, S_OUT, rows), "s_waitcnt vmcnt(0)")
+        B.raw(*(load_rows_sub(base, S_OUT, rows) if h else []), "s_waitcnt vmcnt(0)")
         (add_acc_sol if sol else modswitch_acc)(B, dmap, rows, base, sls3)
         B.raw(*store_rows_sub(base, S_OUT, rows))  # no final wait: the wave retires while its stores drain
     return B

@@ -1668,8 +1668,10 @@ def inv_cyc_w1pp(B, dmap, ad, dst=None, pre_base=72, ybase=96, newhi=64, w1p_in=
     return t_w1pp_w0(B, dmap, ybase, newhi, ad, written=prog, reads_pending=prog)
 
 
-def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False, w1pp_regs=None):
-    """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  `prefetch`
+def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=False, w1pp_regs=None, g1_busy=(),
+             before_g1=()):
+    """Inverse transform of the W0 data in dmap; returns the output dmap (W0, canonical).  g1_busy / before_g1: registers
+    the G1 stages leave alone and lines emitted right before them (the external-product bodies' out-row loads).  `prefetch`
     (standalone kernel, see fwd_core): the caller has loaded the lane-pair table twiddles into
     v40..v43 with the data; the first untwist batch is loaded into v40..v55 after the lane-pair stage
     and stays there through the cyclic stages and T4 (the one register range free in both layouts)."""
@@ -1709,7 +1711,8 @@ def inv_core(B, tabs, dmap, ad=NTT_ADDR, prefetch=False, row_waits=None, w1pp=Fa
         prog = w1pp and getattr(ad, "full_t", False) and PROGRESSIVE_FULL_T  # the W1'' -> W0 reads are still landing
         twist_rows(B, dmap, ad, [regs[0], regs[16]], [MulSlot(0, SG0 + 6 * i, regs[32 + 12 * i:44 + 12 * i]) for i in range(2)],
                    contiguous=False, regs=regs, before_batch=(lambda bt: [UNTWIST_ROW_WAITS[bt]]) if prog else None)
-    fb = free_blocks_except(dmap)
+    B.raw(*before_g1)
+    fb = free_blocks_except(dmap, tuple(g1_busy))
     cf = [True] * 32  # untwist outputs are canonical
     for s in range(4, -1, -1):
         B.tag = f"G1 stage {s}"
