@@ -696,7 +696,7 @@ hipError_t launch_fftg_ext_product(int k, bool cmux, uint64_t* out, uint64_t* gl
 
 // Lanes, as launch_pbs_large (pbs_large.hip): a chunk of >= FFTG_LANE_MIN ciphertexts is split into
 // mi::pbs_lane_count(fftg_default_lanes(logn)) parts on the caller's stream and pooled side streams (mi::StreamFork), launches interleaved step
-// by step, so one part's memory-bound passes overlap another's transform rows.  MI_PBS_LANES=<n> (1: one lane, A/B).
+// by step, so one part's memory-bound passes overlap another's transform rows.
 static constexpr uint32_t FFTG_LANE_MIN = 64;
 // default lane count per N, from the one-box sweep of profiles/r4/session24/lane_sweep.txt (PBS/s at 1 / 2 / 3 / 4
 // lanes: 1_1 (N 512) 35.6 / 41.9 / 41.4 / 34.8 k, 3_3 (N 8192) 2.36 / 2.55 / 2.53 / 2.67 k, 4_4 (N 65536) 176 / 184 /

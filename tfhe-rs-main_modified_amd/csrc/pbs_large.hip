@@ -589,7 +589,7 @@ inline size_t chunk_for(const LargeShape& sh, size_t batch) {
 // each), the first on the caller's stream and the others on pooled side streams (mi::StreamFork), their launches
 // interleaved step by step.  Each ciphertext's blind rotation is independent, so the parts share nothing but the key,
 // and the GPU overlaps one part's memory-bound launches (the rotation + decomposition pass, the MAC, the accumulating
-// inverse pass) with another's issue-bound transform bodies.  MI_PBS_LANES=<n> in the environment (1: one lane, A/B).
+// inverse pass) with another's issue-bound transform bodies.
 static constexpr uint32_t PBS_LANE_MIN = 64;
 
 

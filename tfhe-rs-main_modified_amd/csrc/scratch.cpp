@@ -253,13 +253,7 @@ hipError_t StreamFork::join() {
   return first;
 }
 
-int pbs_lane_count(int dflt) {
-  static const int env = [] {
-    const char* v = getenv("MI_PBS_LANES");
-    return v ? atoi(v) : 0;
-  }();
-  return std::max(1, std::min(env > 0 ? env : dflt, 1 + StreamFork::MAX_SIDE));
-}
+int pbs_lane_count(int dflt) { return std::max(1, std::min(dflt, 1 + StreamFork::MAX_SIDE)); }
 
 size_t scratch_bytes(int device) {
   Pool& P = pool();

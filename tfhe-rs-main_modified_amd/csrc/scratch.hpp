@@ -48,8 +48,8 @@ class StreamFork {
   int device_ = 0, n_ = 0;
 };
 
-// lanes a batched blind rotation splits a chunk into: MI_PBS_LANES in the environment (1 ... 1 + MAX_SIDE), else the
-// caller's measured default for its shape
+// lanes a batched blind rotation splits a chunk into: the caller's measured default for its shape, clamped to
+// 1 ... 1 + MAX_SIDE (r6: no environment override; the lane sweeps of r4-r5 are in DESIGN.md section 4)
 int pbs_lane_count(int dflt);
 
 }  // namespace mi
