@@ -14,6 +14,10 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import tfhe_ntt_amd as eng  # noqa: E402
 
+if os.environ.get("PROBE_LIB"):  # A/B: another build of the library (loaded lazily, so this takes effect)
+    import tfhe_ntt_amd._lib as _L
+    _L.LIB_PATH = os.path.abspath(os.environ["PROBE_LIB"])
+
 fft = "--fft" in sys.argv
 names = [a for a in sys.argv[1:] if a != "--fft"] or list(bench.SHAPE_LEGS)
 for i, nm in enumerate(names):  # "N,k,n,base_log,level,batch" adds an ad-hoc shape
