@@ -106,6 +106,7 @@ int mi_multi_gpu_destroy(mi_multi_gpu* m) {
     DeviceGuard g(m->devices[i]);
     if (m->streams[i]) {
       (void)hipStreamSynchronize(m->streams[i]);
+      mi::scratch_stream_retired(m->streams[i]);
       (void)hipStreamDestroy(m->streams[i]);
     }
     if (i < m->events.size() && m->events[i]) (void)hipEventDestroy(m->events[i]);

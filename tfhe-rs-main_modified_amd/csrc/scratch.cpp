@@ -15,6 +15,7 @@ struct Block {
   size_t bytes = 0;
   int device = 0;
   hipEvent_t last_use = nullptr;  // recorded on the stream of the block's last user
+  hipStream_t stream = nullptr;   // that stream (scratch_stream_retired)
   bool recorded = false;
 };
 
@@ -79,15 +80,30 @@ bool fits_snugly(size_t block, size_t request) {
   return block / 4 <= request || block - request <= ((size_t)64 << 20);
 }
 
+// waits for the block's last user.  The event was recorded on the caller's stream, which the caller may have destroyed
+// since: on ROCm an event whose stream is gone can fail hipEventSynchronize / hipStreamWaitEvent (observed:
+// hipErrorCapturedEvent with no capture anywhere in the process).  The fallback is a device-wide wait, and the runtime's
+// sticky last error is cleared, so a later unrelated hipGetLastError (torch checks it after every launch) does not
+// report it.
+void wait_last_use(const Block& b) {
+  if (!b.recorded) return;
+  if (hipEventSynchronize(b.last_use) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipDeviceSynchronize();
+    (void)hipGetLastError();
+  }
+}
+
 // frees blocks that no longer have a pending user (their event has completed)
 void release(std::vector<Block>& blocks) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (Block& b : blocks) {
     (void)hipSetDevice(b.device);
-    if (b.recorded) (void)hipEventSynchronize(b.last_use);
+    wait_last_use(b);
     (void)hipEventDestroy(b.last_use);
     (void)hipFree(b.p);
+    (void)hipGetLastError();
   }
   (void)hipSetDevice(cur);
 }
@@ -106,12 +122,12 @@ bool take_idle(Pool& P, int dev, size_t bytes, bool snug, Block* out) {
   return true;
 }
 
-// hands a reused block to the caller: its stream waits for the block's last user
+// hands a reused block to the caller: its stream waits for the block's last user (host-side, if the event cannot be
+// waited on by the stream: see wait_last_use)
 hipError_t issue_reused(const Block& blk, void** out, hipStream_t s) {
-  hipError_t e;
-  if (blk.recorded && (e = hipStreamWaitEvent(s, blk.last_use, 0)) != hipSuccess) {
-    (void)scratch_free(blk.p, nullptr);
-    return e;
+  if (blk.recorded && hipStreamWaitEvent(s, blk.last_use, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    wait_last_use(blk);
   }
   *out = blk.p;
   return hipSuccess;
@@ -190,6 +206,7 @@ hipError_t scratch_free(void* p, hipStream_t s) {
   // the block is still owned by this caller: record before it becomes visible to others
   const hipError_t e = hipEventRecord(blk.last_use, s);
   blk.recorded = e == hipSuccess;
+  blk.stream = s;
   if (!blk.recorded) {  // cannot order the next user: retire the block after the device drains
     (void)hipDeviceSynchronize();
     std::lock_guard<std::mutex> lk(P.mu);
@@ -202,6 +219,16 @@ hipError_t scratch_free(void* p, hipStream_t s) {
   P.busy.erase(p);
   P.idle.push_back(blk);
   return hipSuccess;
+}
+
+void scratch_stream_retired(hipStream_t s) {
+  if (!s) return;  // the null stream is never destroyed
+  Pool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  for (Block& b : P.idle)
+    if (b.stream == s) b.recorded = false;  // the caller synchronized s: the block's last use has completed
+  for (auto& kv : P.busy)
+    if (kv.second.stream == s) kv.second.recorded = false;
 }
 
 size_t scratch_trim(int device) {

@@ -23,6 +23,9 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 hipError_t scratch_free(void* p, hipStream_t s);
 // frees every idle block of `device` (-1: all devices) after its last user retired; returns the bytes released
 size_t scratch_trim(int device);
+// the caller has synchronized `s` and is about to destroy it: blocks whose last user ran on `s` need no wait on the
+// event recorded there (an event whose stream is gone cannot be waited on reliably; see scratch.cpp wait_last_use)
+void scratch_stream_retired(hipStream_t s);
 // bytes held by the pool on `device` (idle + in use)
 size_t scratch_bytes(int device);
 

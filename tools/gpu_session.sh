@@ -24,7 +24,7 @@ for s in "$@"; do
            python3 tools/summarize_rocpd.py /tmp/mi_trace/run_kernel_trace.csv "$O/trace" \
              "$O/trace/bench_line_under_rocprof.json" > "$O/trace/summary.txt" 2>&1 || true ;;
     probe) step variant_probe 240 ./tools/variant_probe 8192 || exit 1; cp gpurun_out/variant_probe.txt "$O/" ;;
-    test=*) step pytest_sel 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu "${s#test=}"
+    test=*) step pytest_sel 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu ${s#test=}
             rc=$?; cp gpurun_out/pytest_sel.txt "$O/"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
