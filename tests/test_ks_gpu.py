@@ -43,6 +43,9 @@ def run_ks(engine, ksk, lwe, base_log, level):
     (20, 12, 21, 3, 17),        # 21-bit base: 3 bytes per digit
     (512, 300, 4, 4, 520),      # 3 row groups of 256 (last ragged) x 10 column groups of 32
     (48, 40, 4, 4, 300),        # odd number of k blocks (K = 192 -> 3), 2 row groups, padded columns
+    (50, 20, 6, 2, 33),         # r6 digit kernel at level 2 (one byte per digit), in_dim not a multiple of 32
+    (70, 11, 5, 1, 300),        # ... at level 1, 2 row groups
+    (24, 8, 3, 8, 9),           # ... at level 8 (native u64 output)
 ])
 def test_keyswitch_matches_oracle(engine, oracle, in_dim, out_dim, base_log, level, batch):
     g = H.rng(in_dim * 7 + out_dim + base_log)

@@ -1,34 +1,24 @@
-"""Run the PARAM_MESSAGE_2_CARRY_2 keyswitch (2048 -> 918, B 2^4, L 4) a few times on synthetic data, for
-rocprofv3 kernel-trace / PMC passes on the keyswitch kernels alone (bench.py runs every leg)."""
-import argparse
+#!/usr/bin/env python3
+"""Time bench.py's keyswitch leg alone (diagnostic): python tools/ks_probe.py [reps]; PROBE_PKG=<dir> loads another
+build of the package (A/B in one session)."""
+import json
 import os
 import sys
+import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "tfhe-rs-main_modified_amd"))
+# PROBE_PKG=<dir holding another tfhe_ntt_amd/ with its own .so>: A/B against another build in one session
+sys.path[:0] = [ROOT, os.environ.get("PROBE_PKG") or os.path.join(ROOT, "tfhe-rs-main_modified_amd")]
 
+import torch  # noqa: E402
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--reps", type=int, default=5)
-    args = ap.parse_args()
-    import torch
-    import tfhe_ntt_amd as eng
+import tfhe_ntt_amd as eng  # noqa: E402  (before bench, whose import puts the tree's package first on sys.path)
+import bench  # noqa: E402
 
-    KS = eng.lwe_keyswitch
-    dev = torch.device("cuda", 0)
-    ksk = torch.empty((2048, 4, 919), dtype=torch.int64, device=dev)
-    eng.fill_uniform(ksk, 0x74666865 + 40, 0)
-    key = KS.LweKeyswitchKey(ksk, 4, 4)
-    lwe = torch.empty((args.batch, 2049), dtype=torch.int64, device=dev)
-    eng.fill_uniform(lwe, 0x74666865 + 41, 0)
-    out = torch.empty((args.batch, 919), dtype=torch.int64, device=dev)
-    for _ in range(args.reps):
-        KS.keyswitch_lwe_ciphertext(key, lwe, out)
-    torch.cuda.synchronize()
-    print(f"ks_probe: {args.reps} x {args.batch} keyswitches done")
-
-
-if __name__ == "__main__":
-    main()
+dev = torch.device("cuda", 0)
+torch.cuda.set_stream(torch.cuda.Stream(device=dev))
+args = types.SimpleNamespace(pbs_batch=bench.PBS_BATCH)
+for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 1):
+    r = bench.bench_keyswitch(args, eng, torch, dev, 1, lambda: None, None)
+    print(json.dumps({"value": r["value"], "kernel_ms": r["kernel_ms"], "frac": r["roofline"]["frac"],
+                      "pkg": os.path.dirname(eng.__file__)}), flush=True)

@@ -7,16 +7,14 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "tfhe-rs-main_modified_amd")]
+# PROBE_PKG=<dir holding another tfhe_ntt_amd/ with its own .so>: A/B against another build in one session
+sys.path[:0] = [ROOT, os.environ.get("PROBE_PKG") or os.path.join(ROOT, "tfhe-rs-main_modified_amd")]
 
 import torch  # noqa: E402
 
+import tfhe_ntt_amd as eng  # noqa: E402  (before bench, whose import puts the tree's package first on sys.path)
 import bench  # noqa: E402
-import tfhe_ntt_amd as eng  # noqa: E402
 
-if os.environ.get("PROBE_LIB"):  # A/B: another build of the library (loaded lazily, so this takes effect)
-    import tfhe_ntt_amd._lib as _L
-    _L.LIB_PATH = os.path.abspath(os.environ["PROBE_LIB"])
 
 fft = "--fft" in sys.argv
 names = [a for a in sys.argv[1:] if a != "--fft"] or list(bench.SHAPE_LEGS)
