@@ -16,7 +16,9 @@
 //     [column group of GN tiles][k block][tile][plane][lane] x 16 B (one contiguous block per k step),
 //     zero-padded to whole column groups / 64-digit blocks;
 //   * ks_digits_kernel (per batch): decomposition of every mask element into int8 digits in A-fragment
-//     order [row group of GM tiles][k block][tile][lane] x 16 B (padded rows and digits are 0);
+//     order [row group of GM tiles][k block][tile][lane] x 16 B (padded rows and digits are 0); for one byte per
+//     digit at 1 / 2 / 4 / 8 levels, ks_digits_l_kernel (r6) builds each 16 KiB (row group, k block) in LDS from
+//     coalesced row reads;
 //   * ks_gemm_kernel: one 4-wave workgroup per CU computes a 256-row x 32-column block (x 8 planes):
 //     each k step's 16 + 16 KiB of fragments are copied global -> LDS by LDS-DMA
 //     (global_load_lds_dwordx4) into a 3-buffer ring two steps ahead of the MFMAs (counted vmcnt + raw
