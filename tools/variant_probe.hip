@@ -109,12 +109,15 @@ static void launch_w(bool fwd, u64* data, uint32_t batch, const u64* twist, hipS
     hipLaunchKernelGGL((probe_kernel<V, false, W>), dim3(grid), dim3(64 * W), 0, s, data, batch, twist);
 }
 
-// variants past the generated ones: bodies 0, 1 and 2 with 4 waves per workgroup (the library's inverse launch)
+// variants past the generated ones: bodies 0, 1 and 2 with 4 waves per workgroup (the library's inverse launch),
+// then body 1 with 2 and with 8
 static void launch_v(int v, bool fwd, u64* data, uint32_t batch, const u64* twist, hipStream_t s) {
   switch (v) {
     case MI_N_VARIANTS + 0: launch_w<0, 4>(fwd, data, batch, twist, s); return;
     case MI_N_VARIANTS + 1: launch_w<1, 4>(fwd, data, batch, twist, s); return;
     case MI_N_VARIANTS + 2: launch_w<2, 4>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 3: launch_w<1, 2>(fwd, data, batch, twist, s); return;  // r6: 2 and 8 waves per group
+    case MI_N_VARIANTS + 4: launch_w<1, 8>(fwd, data, batch, twist, s); return;
     default: break;
   }
   switch (v) {
@@ -127,7 +130,7 @@ static void launch_v(int v, bool fwd, u64* data, uint32_t batch, const u64* twis
 
 int main(int argc, char** argv) {
   const uint32_t batch = argc > 1 ? (uint32_t)atoi(argv[1]) : 8192;
-  const int nv = MI_N_VARIANTS + 3;
+  const int nv = MI_N_VARIANTS + 5;
   const size_t n = (size_t)batch * 2048;
   u64 *data, *twist, *ref;
   CK(hipMalloc(&data, n * 8));
@@ -147,7 +150,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(v == 0 ? h0.data() : h1.data(), data, n * 8, hipMemcpyDeviceToHost));
     static const int same[] = MI_SAME_MATH;
-    const bool cmp = v < MI_N_VARIANTS ? same[v] : same[v - MI_N_VARIANTS];  // extras: bodies 0, 1, 2 at 4 waves
+    const bool cmp = v < MI_N_VARIANTS ? same[v] : v < MI_N_VARIANTS + 3 ? same[v - MI_N_VARIANTS] : same[1];  // extras
     if (v && cmp && memcmp(h0.data(), h1.data(), n * 8) != 0) {
       fprintf(stderr, "variant %d differs from variant 0\n", v);
       return 2;
