@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes over one large-N PBS shape leg (default 3_3): bash tools/pmc_shape.sh <out-dir> [shape]
-# Each pass its own rocprofv3 process (no tracing domains); per-kernel means (VALU per wave, issue-busy share, HBM
+# (A two-lane batch, >= 64 ciphertexts, crashes rocprofv3 --pmc on the host; pass a one-lane ad-hoc shape such as
+# 8192,1,1077,15,2,48.)  Each pass its own rocprofv3 process (no tracing domains); per-kernel means (VALU per wave, issue-busy share, HBM
 # bytes: FETCH_SIZE KiB x 2 on gfx950, WRITE_SIZE KiB) come back in <out-dir>/summary.txt, durations from a
 # separate kernel trace.
 set -o pipefail
