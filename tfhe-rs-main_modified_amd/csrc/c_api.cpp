@@ -1402,7 +1402,7 @@ int mi_lwe_ksk32_create(const uint32_t* ksk, size_t in_dim, size_t out_dim, int 
     delete key;
     return fail(MI_ERR_INVALID_ARG, "bad device");
   }
-  if (hipMalloc(&key->frag, mi::ks_key_bytes(in_dim, out_dim, base_log, level)) != hipSuccess) {
+  if (hipMalloc(&key->frag, mi::ks32_key_bytes(in_dim, out_dim, base_log, level)) != hipSuccess) {
     delete key;
     return fail(MI_ERR_OOM, "keyswitch key allocation failed");
   }

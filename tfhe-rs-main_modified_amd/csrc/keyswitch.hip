@@ -97,26 +97,37 @@ __device__ __forceinline__ uint4 pack16(const int8_t (&b)[16]) {
 // side carries 8 planes, so tall blocks stage fewer bytes per MFMA.
 static constexpr int WAVE_R = 4, WAVE_C = 1;
 static constexpr int GM = 4 * WAVE_R;  // row tiles (of 16) per workgroup block
-static constexpr int GN = 2 * WAVE_C;  // column tiles (of 16) per workgroup block
-static constexpr int A_STEP = GM * 64;      // uint4 per k step of a row group
-static constexpr int B_STEP = GN * 8 * 64;  // uint4 per k step of a column group
-static constexpr int A_PIECES = GM / 4;      // 1 KiB LDS-DMA pieces per wave and k step
-static constexpr int B_PIECES = GN * 8 / 4;
+static constexpr int A_STEP = GM * 64;  // uint4 per k step of a row group
+static constexpr int A_PIECES = GM / 4;  // 1 KiB LDS-DMA pieces per wave and k step
+// B side, per key word type: the native u64 key needs all 8 byte planes of 2 column tiles per wave; the KS32 u32 key
+// (sums mod 2^32) only planes 0..3 (the signed-byte recoding of the low 4 bytes does not depend on the high ones), so
+// its waves cover 4 column tiles x 4 planes with the same 64 accumulators, 16 B fragments and LDS step (r6).
+template <bool K32>
+struct Geo {
+  static constexpr int GN = (K32 ? 4 : 2) * WAVE_C;  // column tiles (of 16) per workgroup block
+  static constexpr int NPL = K32 ? 4 : 8;            // byte planes
+  static constexpr int B_STEP = GN * NPL * 64;       // uint4 per k step of a column group
+  static constexpr int B_PIECES = GN * NPL / 4;
+};
+static_assert(Geo<false>::B_STEP == Geo<true>::B_STEP, "one LDS ring shape");
+static constexpr int B_STEP = Geo<false>::B_STEP, B_PIECES = Geo<false>::B_PIECES;
 static constexpr int PIECES = A_PIECES + B_PIECES;
 static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 measured no faster
 
-// frag[(((cg * KB + kb) * GN + ci) * 8 + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
+// frag[(((cg * KB + kb) * GN + ci) * NPL + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
 // column 16 (GN cg + ci) + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
 // (in_dim blocks of `level` LWEs) shifted left by 8 s.
-// W = u64 (native keyswitch) or uint32_t (KS32: the u32 key words zero-extended; only planes 0..3 matter mod 2^32)
+// W = u64 (native keyswitch) or uint32_t (KS32: the u32 key words zero-extended; planes 0..3 stored)
 template <typename W>
 __global__ __launch_bounds__(256) void ksk_prepare_kernel(uint4* __restrict__ frag, const W* __restrict__ ksk,
                                                           Shape s) {
-  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;  // CT is a multiple of GN
+  using G = Geo<sizeof(W) == 4>;
+  constexpr int GN = G::GN, NPL = G::NPL;
+  const uint64_t total = (uint64_t)s.CT * s.KB * NPL * 64;  // CT is a multiple of GN
   for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t lane = idx & 63, t = (idx >> 6) & 7, ci = (idx >> 9) % GN;
-    const uint64_t rest = idx / (512 * GN);
+    const uint32_t lane = idx & 63, t = (idx >> 6) % NPL, ci = (idx / (64 * NPL)) % GN;
+    const uint64_t rest = idx / (64 * NPL * GN);
     const uint32_t kb = rest % s.KB, cg = rest / s.KB;
     const uint32_t col = (cg * GN + ci) * 16 + (lane & 15);
     int8_t b[16];
@@ -245,6 +256,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   // NBUF stage buffers (A pieces, then B pieces) of 32 KiB: while step kb multiplies, step kb + 1 is
   // read into registers and steps kb + 2 .. kb + NBUF are in flight (deep enough to cover the L2 /
   // MALL latency at the per-CU byte rate one step of MFMAs needs)
+  constexpr int GN = Geo<OUT32>::GN, NPL = Geo<OUT32>::NPL, CW = GN / WAVE_C;  // CW column tiles per wave
   __shared__ uint4 lds[NBUF][A_STEP + B_STEP];
   uint32_t mg, cg;
   if (!ks_block(blockIdx.x, n_mg, s.CT / GN, mg, cg)) return;  // whole workgroup, before any barrier
@@ -268,17 +280,18 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
                                          &lds[buf][A_STEP + (B_PIECES * w + q - A_PIECES) * 64], 16, 0, 0);
     }
   };
-  i32x4 acc[4][2][8];
+  i32x4 acc[4][CW][NPL];
+  static_assert(CW * NPL == 16, "16 plane fragments per wave and k step");
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < CW; ++c)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[m][c][t] = i32x4{0, 0, 0, 0};
+      for (int t = 0; t < NPL; ++t) acc[m][c][t] = i32x4{0, 0, 0, 0};
   // this lane's fragment addresses in buffer 0 (buffer b adds b * BUF_BYTES)
   const uint32_t lds0 = (uint32_t)(uintptr_t)&lds[0][0];
   const uint32_t a_addr = lds0 + ((wr * 4) * 64 + lane) * 16;
-  const uint32_t b_addr = lds0 + (A_STEP + (wc * 2 * 8) * 64 + lane) * 16;
+  const uint32_t b_addr = lds0 + (A_STEP + (wc * CW * NPL) * 64 + lane) * 16;
   constexpr uint32_t BUF_BYTES = (A_STEP + B_STEP) * 16;
   // Fragment reads are inline asm: the compiler cannot tell the stage buffers apart and would drain
   // every LDS-DMA in flight (vmcnt(0)) before its own ds_reads; lgkm_wait retires them.
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
         : "=&v"(A[0]), "=&v"(A[1]), "=&v"(A[2]), "=&v"(A[3])
         : "v"(ao));
   };
-  auto rd_b = [&](uint32_t buf, int j, i32x4& Bj) {  // plane t of column tile c, j = 8 c + t
+  auto rd_b = [&](uint32_t buf, int j, i32x4& Bj) {  // plane t of column tile c, j = NPL c + t
     const uint32_t bo = b_addr + buf * BUF_BYTES + 1024 * j;
     asm volatile("ds_read_b128 %0, %1" : "=&v"(Bj) : "v"(bo));
   };
@@ -320,7 +333,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   for (int j = 0; j < 16; ++j) rd_b(0, j, Bf[j]);
   lgkm_wait(A, Bf);
   __builtin_amdgcn_s_barrier();
-  // Step kb: 16 groups of 4 MFMAs, group j on plane fragment Bf[j] (j = 8 c + t) and the 4 row tiles A.
+  // Step kb: 16 groups of 4 MFMAs, group j on plane fragment Bf[j] (j = NPL c + t) and the 4 row tiles A.
   // Behind group j the wave refills Bf[j] with step kb + 1's fragment (just freed), reads step kb + 1's
   // A into NA behind group 0, and issues a quarter of step kb + NBUF's LDS-DMA into the buffer step kb
   // occupied behind groups 1, 3, 5, 7 (an MFMA leaves half its cycles to other issue).  Step kb + 2's
@@ -330,7 +343,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
     const uint32_t nbuf = (buf + 1) % NBUF, src = kb + NBUF < last ? kb + NBUF : last;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int c = j >> 3, t = j & 7;
+      const int c = j / NPL, t = j % NPL;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {  // accumulators pinned to AGPRs ("+a"): fragments keep the VGPRs
         if (j == 0 && m == 0)  // A was just copied by VALU: 2 wait states before an MFMA reads it
@@ -356,8 +369,8 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   // the compiler does not know the asm above holds MFMAs: 12 wait states before it reads their results
   asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const uint32_t col = (cg * GN + wc * 2 + c) * 16 + (lane & 15);
+  for (int c = 0; c < CW; ++c) {
+    const uint32_t col = (cg * GN + wc * CW + c) * 16 + (lane & 15);
     if (col >= s.out_size) continue;
     const bool is_body = col == s.out_size - 1;
 #pragma unroll
@@ -368,7 +381,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
         if (row >= batch) continue;
         u64 v = 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) v += (u64)(int64_t)acc[m][c][t][r] << (8 * t);
+        for (int t = 0; t < NPL; ++t) v += (u64)(int64_t)acc[m][c][t][r] << (8 * t);
         u64 base = is_body ? lwe_in[(uint64_t)row * (s.in_dim + 1) + s.in_dim] : 0;
         if constexpr (OUT32) {
           if (is_body) base = closest_representable(base, s.body_log) >> 32;
@@ -445,7 +458,9 @@ __global__ __launch_bounds__(256) void lwe_ms_kernel(u64* __restrict__ out, cons
 
 int ks_digit_bytes_per_term(int base_log) { return (base_log + 1 + 7) / 8; }
 
-static ks::Shape ks_shape(size_t in_dim, size_t out_dim, int base_log, int level) {
+// k32: the KS32 key geometry (ks::Geo<true>)
+static ks::Shape ks_shape(size_t in_dim, size_t out_dim, int base_log, int level, bool k32 = false) {
+  const uint32_t gn = k32 ? ks::Geo<true>::GN : ks::Geo<false>::GN;
   ks::Shape s;
   s.in_dim = (uint32_t)in_dim;
   s.out_size = (uint32_t)(out_dim + 1);
@@ -454,14 +469,19 @@ static ks::Shape ks_shape(size_t in_dim, size_t out_dim, int base_log, int level
   s.nd = (uint32_t)ks_digit_bytes_per_term(base_log);
   s.K = (uint32_t)(in_dim * (size_t)level * s.nd);
   s.KB = (s.K + 63) / 64;
-  s.CT = (s.out_size + 16 * ks::GN - 1) / (16 * ks::GN) * ks::GN;  // whole column groups
+  s.CT = (s.out_size + 16 * gn - 1) / (16 * gn) * gn;  // whole column groups
   s.body_log = 64;
   return s;
 }
 
 size_t ks_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level) {
   const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
-  return (size_t)s.CT * s.KB * 8 * 64 * 16;
+  return (size_t)s.CT * s.KB * ks::Geo<false>::NPL * 64 * 16;
+}
+
+size_t ks32_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level) {
+  const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level, true);
+  return (size_t)s.CT * s.KB * ks::Geo<true>::NPL * 64 * 16;
 }
 
 size_t ks_digit_bytes(size_t in_dim, int base_log, int level, size_t batch) {
@@ -473,7 +493,7 @@ size_t ks_digit_bytes(size_t in_dim, int base_log, int level, size_t batch) {
 hipError_t launch_ksk_prepare(void* frag, const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level,
                               hipStream_t st) {
   const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
-  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;
+  const uint64_t total = (uint64_t)s.CT * s.KB * ks::Geo<false>::NPL * 64;
   const unsigned grid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
   hipLaunchKernelGGL(ks::ksk_prepare_kernel<uint64_t>, dim3(grid), dim3(256), 0, st, (uint4*)frag, ksk, s);
   return hipGetLastError();
@@ -481,8 +501,8 @@ hipError_t launch_ksk_prepare(void* frag, const uint64_t* ksk, size_t in_dim, si
 
 hipError_t launch_ksk32_prepare(void* frag, const uint32_t* ksk, size_t in_dim, size_t out_dim, int base_log,
                                 int level, hipStream_t st) {
-  const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
-  const uint64_t total = (uint64_t)s.CT * s.KB * 8 * 64;
+  const ks::Shape s = ks_shape(in_dim, out_dim, base_log, level, true);
+  const uint64_t total = (uint64_t)s.CT * s.KB * ks::Geo<true>::NPL * 64;
   const unsigned grid = (unsigned)((total + 255) / 256 < 65535 * 4 ? (total + 255) / 256 : 65535 * 4);
   hipLaunchKernelGGL(ks::ksk_prepare_kernel<uint32_t>, dim3(grid), dim3(256), 0, st, (uint4*)frag, ksk, s);
   return hipGetLastError();
@@ -510,7 +530,7 @@ hipError_t launch_lwe_ms64(uint64_t* out, const uint64_t* in, size_t dim, size_t
 static hipError_t keyswitch_launch(void* out, const uint64_t* lwe_in, const void* frag, void* digits, size_t batch,
                                    size_t in_dim, size_t out_dim, int base_log, int level, int out_log, hipStream_t st) {
   if (batch == 0) return hipSuccess;
-  ks::Shape s = ks_shape(in_dim, out_dim, base_log, level);
+  ks::Shape s = ks_shape(in_dim, out_dim, base_log, level, out_log != 0);
   if (out_log) s.body_log = (uint32_t)out_log;
   const uint32_t rows = (uint32_t)((batch + 16 * ks::GM - 1) / (16 * ks::GM) * 16 * ks::GM);
   const uint64_t total = (uint64_t)rows * s.KB * 4;
@@ -526,7 +546,7 @@ static hipError_t keyswitch_launch(void* out, const uint64_t* lwe_in, const void
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t n_mg = rows / (16 * ks::GM), n_cg = s.CT / ks::GN;
+  const uint32_t n_mg = rows / (16 * ks::GM), n_cg = s.CT / (out_log ? ks::Geo<true>::GN : ks::Geo<false>::GN);
   const uint32_t tiles = (n_mg + 7) / 8 * 8 * n_cg;
   const unsigned grid = 8 * ((tiles + 7) / 8);
   if (out_log)

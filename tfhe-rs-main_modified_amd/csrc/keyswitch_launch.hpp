@@ -9,6 +9,7 @@ namespace mi {
 
 // keyswitch.hip — native-modulus LWE keyswitch on the int8 matrix cores.
 size_t ks_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level);
+size_t ks32_key_bytes(size_t in_dim, size_t out_dim, int base_log, int level);  // the 4-plane KS32 layout
 int ks_digit_bytes_per_term(int base_log);  // signed bytes per decomposition digit
 size_t ks_digit_bytes(size_t in_dim, int base_log, int level, size_t batch);
 hipError_t launch_ksk_prepare(void* frag, const uint64_t* ksk, size_t in_dim, size_t out_dim, int base_log, int level,

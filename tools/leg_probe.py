@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time one of bench.py's legs alone (diagnostic; the numbers the bench reports come from bench.py itself):
-  python tools/leg_probe.py <keyswitch|ext_product|pbs|pbs_solinas|bsk_conversion> [reps]
+  python tools/leg_probe.py <keyswitch|ks32_pbs|ext_product|pbs|pbs_solinas|bsk_conversion> [reps]
 PROBE_PKG=<dir holding another tfhe_ntt_amd/ with its own .so> runs another build of the package (A/B in one session)."""
 import json
 import os
@@ -28,4 +28,4 @@ for _ in range(reps):
     else:
         r = fn(args, eng, torch, dev, 1, lambda: None, None)
     print(json.dumps({"leg": leg, "value": r["value"], "kernel_ms": r.get("kernel_ms"),
-                      "pkg": os.path.dirname(eng.__file__)}), flush=True)
+                      "sub": r.get("keyswitch_and_switch"), "pkg": os.path.dirname(eng.__file__)}), flush=True)
