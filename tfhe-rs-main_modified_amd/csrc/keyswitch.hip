@@ -19,12 +19,12 @@
 //     order [row group of GM tiles][k block][tile][lane] x 16 B (padded rows and digits are 0); for one byte per
 //     digit at 1 / 2 / 4 / 8 levels, ks_digits_l_kernel (r6) builds each 16 KiB (row group, k block) in LDS from
 //     coalesced row reads;
-//   * ks_gemm_kernel: one 4-wave workgroup per CU computes a 256-row x 32-column block (x 8 planes):
+//   * ks_gemm_kernel: one 8-wave workgroup per CU computes a 256-row x 32-column block (x 8 planes):
 //     each k step's 16 + 16 KiB of fragments are copied global -> LDS by LDS-DMA
 //     (global_load_lds_dwordx4) into a 3-buffer ring two steps ahead of the MFMAs (counted vmcnt + raw
 //     s_barrier, so the copies stay in flight across barriers); fragment reads are inline-asm
-//     ds_read_b128 so the compiler does not drain the ring before them.  Each wave owns 4 row tiles x 2
-//     column tiles x 8 planes = 64 accumulators of 16x16 i32 (256 AGPRs, one wave per SIMD).  Blocks
+//     ds_read_b128 so the compiler does not drain the ring before them.  Each wave owns 4 row tiles x 1
+//     column tile x 8 planes = 32 accumulators of 16x16 i32 (128 AGPRs, two waves per SIMD).  Blocks
 //     are mapped XCD-aware: the workgroups one XCD runs together cover 8 row groups x 4 column groups,
 //     so the fragments they share are re-read from that XCD's L2.
 // Fragment maps (gfx950): lane l holds row/column (l & 15) of the tile and the 16 consecutive k of
@@ -92,27 +92,33 @@ __device__ __forceinline__ uint4 pack16(const int8_t (&b)[16]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Workgroup block = WAVE_R x WAVE_C waves, each owning 4 row tiles x 2 column tiles (x 8 planes).
-// 4 x 1 (256 rows x 32 columns) moves 32 KiB per k step for 256 MFMAs, 2 x 2 (128 x 64) 40 KiB: the B
-// side carries 8 planes, so tall blocks stage fewer bytes per MFMA.
-static constexpr int WAVE_R = 4, WAVE_C = 1;
+// Workgroup block = 256 rows x 32 columns (x 8 planes): 32 KiB per k step for 256 MFMAs (a 128 x 64 block moves
+// 40 KiB: the B side carries 8 planes, so tall blocks stage fewer bytes per MFMA).  r6: the block is split over
+// WAVE_R x WAVE_C = 8 waves, two per SIMD, each owning 4 row tiles x 8 plane fragments (32 accumulators, 128
+// AGPRs): an LDS-DMA piece stalls its wave's issue for 100+ cycles among MFMAs and ds_reads (MI355X_MICROARCH.md,
+// 'LDS-DMA piece issue cost'), and with one wave per SIMD those stalls were the kernel's time (MFMA busy ~0.5);
+// the second wave issues its MFMAs through them.
+static constexpr int WAVE_R = 4, WAVE_C = 2, NW = WAVE_R * WAVE_C;
+static constexpr int NFR = 8;          // plane fragments (column tiles x planes) per wave and k step
 static constexpr int GM = 4 * WAVE_R;  // row tiles (of 16) per workgroup block
 static constexpr int A_STEP = GM * 64;  // uint4 per k step of a row group
-static constexpr int A_PIECES = GM / 4;  // 1 KiB LDS-DMA pieces per wave and k step
+static constexpr int A_PIECES = GM / NW;  // 1 KiB LDS-DMA pieces per wave and k step
 // B side, per key word type: the native u64 key needs all 8 byte planes of 2 column tiles per wave; the KS32 u32 key
 // (sums mod 2^32) only planes 0..3 (the signed-byte recoding of the low 4 bytes does not depend on the high ones), so
-// its waves cover 4 column tiles x 4 planes with the same 64 accumulators, 16 B fragments and LDS step (r6).
+// its workgroups cover 4 column tiles x 4 planes with the same accumulators, 16 B fragments and LDS step (r6).
 template <bool K32>
 struct Geo {
-  static constexpr int GN = (K32 ? 4 : 2) * WAVE_C;  // column tiles (of 16) per workgroup block
-  static constexpr int NPL = K32 ? 4 : 8;            // byte planes
-  static constexpr int B_STEP = GN * NPL * 64;       // uint4 per k step of a column group
-  static constexpr int B_PIECES = GN * NPL / 4;
+  static constexpr int GN = K32 ? 4 : 2;        // column tiles (of 16) per workgroup block
+  static constexpr int NPL = K32 ? 4 : 8;       // byte planes
+  static constexpr int CW = GN / WAVE_C;        // column tiles per wave
+  static constexpr int B_STEP = GN * NPL * 64;  // uint4 per k step of a column group
+  static constexpr int B_PIECES = GN * NPL / NW;
+  static_assert(CW * NPL == NFR, "NFR plane fragments per wave");
 };
 static_assert(Geo<false>::B_STEP == Geo<true>::B_STEP, "one LDS ring shape");
 static constexpr int B_STEP = Geo<false>::B_STEP, B_PIECES = Geo<false>::B_PIECES;
 static constexpr int PIECES = A_PIECES + B_PIECES;
-static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 measured no faster
+static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 and 5 measured no faster (r6 s17)
 
 // frag[(((cg * KB + kb) * GN + ci) * NPL + t) * 64 + lane] = plane t of GEMM rows k = 64 kb + 16 (lane >> 4) + j,
 // column 16 (GN cg + ci) + (lane & 15); GEMM row k = (i * level + li) * nd + s holds KSK row i * level + li
@@ -249,14 +255,14 @@ __device__ __forceinline__ u64 closest_representable(u64 x, uint32_t bits) {
 // OUT32: keyswitch_lwe_ciphertext_with_scalar_change (lwe_keyswitch.rs:331-447): the body is the input body rounded
 // to the output modulus' 2^body_log and scaled down by 2^32, the sums wrap mod 2^32, and u32 words are stored
 template <bool OUT32>
-__global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_v, const u64* __restrict__ lwe_in,
+__global__ __launch_bounds__(64 * NW, 1) void ks_gemm_kernel(void* __restrict__ out_v, const u64* __restrict__ lwe_in,
                                                          const uint4* __restrict__ afrag,
                                                          const uint4* __restrict__ bfrag, uint32_t batch,
                                                          uint32_t n_mg, Shape s) {
   // NBUF stage buffers (A pieces, then B pieces) of 32 KiB: while step kb multiplies, step kb + 1 is
   // read into registers and steps kb + 2 .. kb + NBUF are in flight (deep enough to cover the L2 /
   // MALL latency at the per-CU byte rate one step of MFMAs needs)
-  constexpr int GN = Geo<OUT32>::GN, NPL = Geo<OUT32>::NPL, CW = GN / WAVE_C;  // CW column tiles per wave
+  constexpr int GN = Geo<OUT32>::GN, NPL = Geo<OUT32>::NPL, CW = Geo<OUT32>::CW;  // CW column tiles per wave
   __shared__ uint4 lds[NBUF][A_STEP + B_STEP];
   uint32_t mg, cg;
   if (!ks_block(blockIdx.x, n_mg, s.CT / GN, mg, cg)) return;  // whole workgroup, before any barrier
@@ -281,7 +287,6 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
     }
   };
   i32x4 acc[4][CW][NPL];
-  static_assert(CW * NPL == 16, "16 plane fragments per wave and k step");
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -307,11 +312,11 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
     const uint32_t bo = b_addr + buf * BUF_BYTES + 1024 * j;
     asm volatile("ds_read_b128 %0, %1" : "=&v"(Bj) : "v"(bo));
   };
-  auto lgkm_wait = [&](i32x4(&A)[4], i32x4(&Bf)[16]) {
+  static_assert(NFR == 8, "lgkm_wait names 8 plane fragments");
+  auto lgkm_wait = [&](i32x4(&A)[4], i32x4(&Bf)[NFR]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
                  : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(Bf[0]), "+v"(Bf[1]), "+v"(Bf[2]),
-                   "+v"(Bf[3]), "+v"(Bf[4]), "+v"(Bf[5]), "+v"(Bf[6]), "+v"(Bf[7]), "+v"(Bf[8]), "+v"(Bf[9]),
-                   "+v"(Bf[10]), "+v"(Bf[11]), "+v"(Bf[12]), "+v"(Bf[13]), "+v"(Bf[14]), "+v"(Bf[15]));
+                   "+v"(Bf[3]), "+v"(Bf[4]), "+v"(Bf[5]), "+v"(Bf[6]), "+v"(Bf[7]));
   };
   // prologue: steps 0..2 in flight; steps 0 and 1 landed; step 0's fragments in (A, Bf); a barrier so
   // that nobody's step-NBUF DMA overwrites buffer 0 before every wave has read it
@@ -327,13 +332,13 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * PIECES) : "memory");  // steps 0 and 1 landed
   __builtin_amdgcn_s_barrier();
-  i32x4 A[4], NA[4], Bf[16];
+  i32x4 A[4], NA[4], Bf[NFR];
   rd_a(0, A);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) rd_b(0, j, Bf[j]);
+  for (int j = 0; j < NFR; ++j) rd_b(0, j, Bf[j]);
   lgkm_wait(A, Bf);
   __builtin_amdgcn_s_barrier();
-  // Step kb: 16 groups of 4 MFMAs, group j on plane fragment Bf[j] (j = NPL c + t) and the 4 row tiles A.
+  // Step kb: NFR groups of 4 MFMAs, group j on plane fragment Bf[j] (j = NPL c + t) and the 4 row tiles A.
   // Behind group j the wave refills Bf[j] with step kb + 1's fragment (just freed), reads step kb + 1's
   // A into NA behind group 0, and issues a quarter of step kb + NBUF's LDS-DMA into the buffer step kb
   // occupied behind groups 1, 3, 5, 7 (an MFMA leaves half its cycles to other issue).  Step kb + 2's
@@ -342,7 +347,7 @@ __global__ __launch_bounds__(256, 1) void ks_gemm_kernel(void* __restrict__ out_
   for (uint32_t kb = 0; kb < s.KB; ++kb) {
     const uint32_t nbuf = (buf + 1) % NBUF, src = kb + NBUF < last ? kb + NBUF : last;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < NFR; ++j) {
       const int c = j / NPL, t = j % NPL;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {  // accumulators pinned to AGPRs ("+a"): fragments keep the VGPRs
@@ -550,10 +555,10 @@ static hipError_t keyswitch_launch(void* out, const uint64_t* lwe_in, const void
   const uint32_t tiles = (n_mg + 7) / 8 * 8 * n_cg;
   const unsigned grid = 8 * ((tiles + 7) / 8);
   if (out_log)
-    hipLaunchKernelGGL(ks::ks_gemm_kernel<true>, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
+    hipLaunchKernelGGL(ks::ks_gemm_kernel<true>, dim3(grid), dim3(64 * ks::NW), 0, st, out, lwe_in, (const uint4*)digits,
                        (const uint4*)frag, (uint32_t)batch, n_mg, s);
   else
-    hipLaunchKernelGGL(ks::ks_gemm_kernel<false>, dim3(grid), dim3(256), 0, st, out, lwe_in, (const uint4*)digits,
+    hipLaunchKernelGGL(ks::ks_gemm_kernel<false>, dim3(grid), dim3(64 * ks::NW), 0, st, out, lwe_in, (const uint4*)digits,
                        (const uint4*)frag, (uint32_t)batch, n_mg, s);
   return hipGetLastError();
 }
