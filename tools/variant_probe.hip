@@ -29,13 +29,27 @@ static constexpr int WAVE_LDS2 = 1088;
       [t1w] "v"(t1w), [t1r] "v"(t1r), [t4w] "v"(t4w), [t4r] "v"(t4r), [lwo] "v"(lwo), [t1x] "v"(t1x),        \
       [t1y] "v"(t1y)
 
-template <int V, bool FWD, int W = 4>
+// STAG > 0 (r6 stagger probe): the first generation's waves start in four slots of 1,024 (wave index >> 10), slot s
+// sleeping s x STAG x 64 cycles before its row loads, so the first slot's rows arrive at the full HBM rate instead
+// of every resident wave's rows arriving together
+template <int V, bool FWD, int W = 4, int STAG = 0>
 __global__ __launch_bounds__(64 * W) void probe_kernel(u64* __restrict__ data, uint32_t batch, const u64* __restrict__ twist) {
   __shared__ u64 lds[W * WAVE_LDS2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t poly = blockIdx.x * W + wv;
   if (poly >= batch) return;
+  if constexpr (STAG > 0) {
+    const uint32_t slot = poly < 4096 ? poly >> 10 : 0;
+    for (uint32_t k = 0; k < slot; ++k) {
+      if constexpr (STAG > 127) {
+        __builtin_amdgcn_s_sleep(127);
+        __builtin_amdgcn_s_sleep(STAG - 127);
+      } else {
+        __builtin_amdgcn_s_sleep(STAG);
+      }
+    }
+  }
   u64* p = data + (uint64_t)poly * 2048;
   const uint32_t S = (uint32_t)(uintptr_t)(lds + wv * WAVE_LDS2);
   constexpr int W1X[] = MI_VARIANT_W1X;
@@ -100,24 +114,24 @@ static void launch(bool fwd, u64* data, uint32_t batch, const u64* twist, hipStr
     hipLaunchKernelGGL((probe_kernel<V, false, 1>), dim3(batch), dim3(64), 0, s, data, batch, twist);
 }
 
-template <int V, int W>
-static void launch_w(bool fwd, u64* data, uint32_t batch, const u64* twist, hipStream_t s) {
-  const unsigned grid = (batch + W - 1) / W;
+// the library's launch form (forward: one wave per workgroup, inverse: four) of body V with a first-generation stagger
+template <int V, int STAG>
+static void launch_lib(bool fwd, u64* data, uint32_t batch, const u64* twist, hipStream_t s) {
   if (fwd)
-    hipLaunchKernelGGL((probe_kernel<V, true, W>), dim3(grid), dim3(64 * W), 0, s, data, batch, twist);
+    hipLaunchKernelGGL((probe_kernel<V, true, 1, STAG>), dim3(batch), dim3(64), 0, s, data, batch, twist);
   else
-    hipLaunchKernelGGL((probe_kernel<V, false, W>), dim3(grid), dim3(64 * W), 0, s, data, batch, twist);
+    hipLaunchKernelGGL((probe_kernel<V, false, 4, STAG>), dim3((batch + 3) / 4), dim3(256), 0, s, data, batch, twist);
 }
 
-// variants past the generated ones: bodies 0, 1 and 2 with 4 waves per workgroup (the library's inverse launch),
-// then body 1 with 2 and with 8
+// variants past the generated ones: body 1 (the library's) in the library's launch form, plain (control) and with a
+// first-generation stagger of 25 / 50 / 100 / 200 x 64 cycles per slot (r6)
 static void launch_v(int v, bool fwd, u64* data, uint32_t batch, const u64* twist, hipStream_t s) {
   switch (v) {
-    case MI_N_VARIANTS + 0: launch_w<0, 4>(fwd, data, batch, twist, s); return;
-    case MI_N_VARIANTS + 1: launch_w<1, 4>(fwd, data, batch, twist, s); return;
-    case MI_N_VARIANTS + 2: launch_w<2, 4>(fwd, data, batch, twist, s); return;
-    case MI_N_VARIANTS + 3: launch_w<1, 2>(fwd, data, batch, twist, s); return;  // r6: 2 and 8 waves per group
-    case MI_N_VARIANTS + 4: launch_w<1, 8>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 0: launch_lib<1, 0>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 1: launch_lib<1, 25>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 2: launch_lib<1, 50>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 3: launch_lib<1, 100>(fwd, data, batch, twist, s); return;
+    case MI_N_VARIANTS + 4: launch_lib<1, 200>(fwd, data, batch, twist, s); return;
     default: break;
   }
   switch (v) {
@@ -150,7 +164,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(v == 0 ? h0.data() : h1.data(), data, n * 8, hipMemcpyDeviceToHost));
     static const int same[] = MI_SAME_MATH;
-    const bool cmp = v < MI_N_VARIANTS ? same[v] : v < MI_N_VARIANTS + 3 ? same[v - MI_N_VARIANTS] : same[1];  // extras
+    const bool cmp = v < MI_N_VARIANTS ? same[v] : same[1];  // extras: body 1
     if (v && cmp && memcmp(h0.data(), h1.data(), n * 8) != 0) {
       fprintf(stderr, "variant %d differs from variant 0\n", v);
       return 2;
