@@ -7,10 +7,13 @@ out=$1; leg=$2; match=$3
 mkdir -p "$out"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 raw=/tmp/mi_pmc_leg; rm -rf $raw; mkdir -p $raw
+# PMC_SETS (optional): other counter sets, ';'-separated (each within one pass's per-block limits)
+sets=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+      "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE"
+      "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE")
+[ -n "$PMC_SETS" ] && IFS=';' read -r -a sets <<< "$PMC_SETS"
 i=0
-for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
-           "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE" \
-           "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do
+for set in "${sets[@]}"; do
   i=$((i+1))
   echo "=== pass $i $(date +%T)"
   timeout -k 10 180 rocprofv3 --pmc $set --output-format csv -d $raw/p$i -o run -- python3 tools/leg_probe.py "$leg" 1 \
