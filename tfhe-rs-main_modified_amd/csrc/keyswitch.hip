@@ -193,39 +193,49 @@ __global__ __launch_bounds__(256) void ks_digits_kernel(uint4* __restrict__ afra
 }
 
 // r6: the common digit shapes (one signed byte per term, nd = 1, and a level count that divides 16: 1, 2, 4, 8), one
-// workgroup per (row group mg, k block kb) = a 16 KiB block of afrag.  ks_digits_kernel's lanes each read 4
-// coefficients of 16 different rows per load (16 KiB-strided); here the workgroup reads its 256 rows x 64 / LEVEL
-// coefficients with 16 consecutive lanes on consecutive coefficients of one row (128-byte segments), decomposes
-// each coefficient into its LEVEL digits (unrolled), places them in the fragment order in LDS (one LEVEL-byte write),
-// and stores the block with coalesced 16-byte stores.  Same bytes as ks_digits_kernel.
+// workgroup per (row group mg, KBW consecutive k blocks) = KBW 16 KiB blocks of afrag.  ks_digits_kernel's lanes each
+// read 4 coefficients of 16 different rows per load (16 KiB-strided); here the workgroup reads its 256 rows x 16
+// coefficients (KBW = 1 block of 64 / LEVEL coefficients at LEVEL <= 4, two blocks of 8 at LEVEL 8) with 16
+// consecutive lanes on consecutive coefficients of one row (whole 128-byte lines: at LEVEL 8 one block's 64-byte half
+// line left the other half to another workgroup, often on another XCD), decomposes each coefficient into its LEVEL
+// digits (unrolled), places them in the fragment order in LDS (one LEVEL-byte write), and stores the blocks with
+// coalesced 16-byte stores.  Same bytes as ks_digits_kernel.
 template <int LEVEL>
 __global__ __launch_bounds__(256) void ks_digits_l_kernel(uint4* __restrict__ afrag, const u64* __restrict__ lwe_in,
                                                           uint32_t batch, uint32_t rows, Shape s) {
   static_assert(16 % LEVEL == 0, "a coefficient's digits stay inside one 16-byte fragment");
-  constexpr int CPB = 64 / LEVEL;  // coefficients per k block
+  constexpr int CPB = 64 / LEVEL;                // coefficients per k block
+  constexpr int KBW = LEVEL > 4 ? LEVEL / 4 : 1;  // k blocks per workgroup: 16 coefficients (128 B) per row
+  constexpr int CPW = CPB * KBW;
   using W = std::conditional_t<LEVEL == 1, uint8_t,
                                std::conditional_t<LEVEL == 2, uint16_t, std::conditional_t<LEVEL == 4, uint32_t, u64>>>;
-  __shared__ uint4 blk[GM * 64];  // 16 KiB: the (mg, kb) block in storage order
-  const uint32_t kb = blockIdx.x % s.KB, mg = blockIdx.x / s.KB;
+  __shared__ uint4 blk[KBW * GM * 64];  // KBW x 16 KiB: the (mg, kb) blocks in storage order
+  const uint32_t nkw = (s.KB + KBW - 1) / KBW;
+  const uint32_t kb0 = (blockIdx.x % nkw) * KBW, mg = blockIdx.x / nkw;
   const uint32_t t = threadIdx.x;
   const int bl = (int)s.base_log;
   uint8_t* bytes = reinterpret_cast<uint8_t*>(blk);
 #pragma unroll 4
-  for (uint32_t q = 0; q < (GM * 16 * CPB) / 256; ++q) {
-    const uint32_t pidx = q * 256 + t, R = pidx / CPB, c = pidx % CPB;  // row in the group, coefficient in the block
-    const uint32_t row = mg * GM * 16 + R, i = kb * CPB + c;
+  for (uint32_t q = 0; q < (GM * 16 * CPW) / 256; ++q) {
+    const uint32_t pidx = q * 256 + t, R = pidx / CPW, cw = pidx % CPW;  // row in the group, coefficient in the span
+    const uint32_t kbi = cw / CPB, c = cw % CPB;
+    const uint32_t row = mg * GM * 16 + R, i = kb0 * CPB + cw;
     const u64 x = (row < batch && i < s.in_dim) ? lwe_in[(uint64_t)row * (s.in_dim + 1) + i] : 0;
     u64 state = decomp_init(x, bl, LEVEL);  // 0 decomposes to 0 at every level (padding rows / columns)
     W w = 0;
 #pragma unroll
     for (int l = 0; l < LEVEL; ++l) w |= (W)(uint8_t)(int8_t)decompose_one(bl, state) << (8 * l);
     const uint32_t kk = LEVEL * c, lane = (kk >> 4) * 16 + (R & 15);
-    *reinterpret_cast<W*>(bytes + ((R >> 4) * 64 + lane) * 16 + (kk & 15)) = w;
+    *reinterpret_cast<W*>(bytes + ((kbi * GM + (R >> 4)) * 64 + lane) * 16 + (kk & 15)) = w;
   }
   __syncthreads();
-  uint4* dst = afrag + ((uint64_t)mg * s.KB + kb) * (GM * 64);
 #pragma unroll
-  for (uint32_t q = 0; q < GM * 64 / 256; ++q) dst[q * 256 + t] = blk[q * 256 + t];
+  for (int kbi = 0; kbi < KBW; ++kbi) {
+    if (kb0 + kbi >= s.KB) break;  // uniform: a ragged last span
+    uint4* dst = afrag + ((uint64_t)mg * s.KB + kb0 + kbi) * (GM * 64);
+#pragma unroll
+    for (uint32_t q = 0; q < GM * 64 / 256; ++q) dst[q * 256 + t] = blk[kbi * GM * 64 + q * 256 + t];
+  }
 }
 
 // Block t of the launch order -> (row group, column group): XCD x (workgroups x, x + 8, ... are dispatched
@@ -543,7 +553,9 @@ static hipError_t keyswitch_launch(void* out, const uint64_t* lwe_in, const void
   if (s.nd == 1 && (level == 1 || level == 2 || level == 4 || level == 8)) {
     auto kern = level == 1 ? ks::ks_digits_l_kernel<1> : level == 2 ? ks::ks_digits_l_kernel<2>
                 : level == 4 ? ks::ks_digits_l_kernel<4> : ks::ks_digits_l_kernel<8>;
-    const unsigned blocks = (unsigned)(rows / (16 * ks::GM) * s.KB);  // one workgroup per 16 KiB (mg, kb) block
+    const uint32_t kbw = level > 4 ? (uint32_t)level / 4 : 1;  // the kernel's KBW
+    // one workgroup per row group and span of kbw k blocks (16 KiB each)
+    const unsigned blocks = (unsigned)(rows / (16 * ks::GM) * ((s.KB + kbw - 1) / kbw));
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, (uint4*)digits, lwe_in, (uint32_t)batch, rows, s);
   } else {
     hipLaunchKernelGGL(ks::ks_digits_kernel, dim3(dgrid), dim3(256), 0, st, (uint4*)digits, lwe_in, (uint32_t)batch,
