@@ -115,7 +115,8 @@ struct Geo {
   static constexpr int B_PIECES = GN * NPL / NW;
   static_assert(CW * NPL == NFR, "NFR plane fragments per wave");
 };
-static_assert(Geo<false>::B_STEP == Geo<true>::B_STEP, "one LDS ring shape");
+static_assert(Geo<false>::B_STEP == Geo<true>::B_STEP && Geo<false>::B_PIECES == Geo<true>::B_PIECES,
+              "one LDS ring shape and DMA split for both key types");
 static constexpr int B_STEP = Geo<false>::B_STEP, B_PIECES = Geo<false>::B_PIECES;
 static constexpr int PIECES = A_PIECES + B_PIECES;
 static constexpr uint32_t NBUF = 3;  // LDS stage buffers (NBUF x 32 KiB); 4 and 5 measured no faster (r6 s17)
