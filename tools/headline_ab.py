@@ -45,7 +45,7 @@ def child(pkg):
     d20 = loop(20)
     ss = loop(int(2.0 / 115e-6))
     print(json.dumps({"pkg": os.path.basename(pkg.rstrip("/")), "driver20_us": d20, "steady_us": ss,
-                      "frac20": BATCH * 2 * N * 8 * 2 / (d20 * 1e-6) / 8e12}), flush=True)
+                      "frac20": BATCH * N * 8 * 2 / (d20 * 1e-6) / 8e12}), flush=True)
 
 
 def main():
