@@ -253,3 +253,22 @@ def test_lwe_modulus_switch_u64_reference_kat(engine):
     out = dev(np.zeros((1, 3), np.uint64))
     KS.lwe_ciphertext_centered_binary_modulus_switch(dev(np.array([[1, 1, 0]], np.uint64)), out, 12)
     assert host(out).tolist() == [[0, 0, 4095]]
+
+
+def test_view_empty_batch(engine):
+    """A zero-row batch is a no-op for the six view operations and the u64 switch (the reference's per-polynomial
+    loops run zero times): no launch, no error, the operands untouched."""
+    import torch
+    view = engine.ntt64.Ntt64(P, 2048).as_view()
+    a = torch.zeros((0, 2048), dtype=torch.int64, device="cuda")
+    b = torch.zeros((0, 2048), dtype=torch.int64, device="cuda")
+    view.forward(a, b)
+    view.forward_normalized(a, b)
+    view.forward_from_power_of_two_modulus(64, a, b)
+    view.forward_from_decomp(a, b)
+    view.add_backward(a, b)
+    view.add_backward_on_power_of_two_modulus(21, a, b)
+    lwe = torch.zeros((0, 919), dtype=torch.int64, device="cuda")
+    engine.lwe_keyswitch.lwe_ciphertext_modulus_switch(lwe, torch.zeros_like(lwe), 12, centered=True)
+    torch.cuda.synchronize()
+    assert a.numel() == 0 and b.numel() == 0
