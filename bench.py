@@ -72,7 +72,7 @@ def parse():
 LEG_SECONDS = 0.3  # every non-headline leg times at least this much GPU work (no --steps-scaled legs)
 # order of the legs in the JSON line (not the order they run in): the driver keeps only the tail of stdout, so the
 # config-3 / config-4 legs come last, followed only by the compact legs_summary
-LEG_ORDER = ("pbs_shapes", "pbs_shapes_fft", "keyswitch", "ks_pbs", "ks32_pbs", "ks_pbs_fft", "ext_product_fft",
+LEG_ORDER = ("plans", "pbs_shapes", "pbs_shapes_fft", "keyswitch", "ks_pbs", "ks32_pbs", "ks_pbs_fft", "ext_product_fft",
              "bsk_conversion",
              "pbs_fft", "ext_product", "pbs_solinas", "pbs")
 
@@ -699,6 +699,82 @@ def cpu_baseline_bsk(seconds: float):
                       f"({'AVX-512' if O.have_avx512() else 'scalar'} transforms), 1 thread"}
 
 
+# the other plans of SURVEY.md 8 a13 / f3: the largest primes = 1 mod 2^16 below 2^62 and 2^64
+# (largest_prime_in_arithmetic_progression64, prime.rs:130-; the GPU tests' p62 / p64) and a prime32 NTT prime
+P62, P64G, P30 = 0x3FFFFFFFFFFF0001, 0xFFFFFFFFFFE40001, 1062862849
+
+
+def bench_plans(args, eng, torch, dev, world, barrier, dist):
+    """Rates of the other SURVEY.md 8 rows at config 2's shape (N = 2048, inputs resident), each over >= 0.3 s of GPU
+    work with the HBM fraction of its algorithmic bytes: a7 the core_crypto Ntt64View pair forward_from_decomp +
+    add_backward_on_power_of_two_modulus(64) (ntt64.rs:221-266, conversions fused into the twisted bodies), a4
+    mul_accumulate (prime64.rs:1182-1222), a13 fwd + inv over generic 62- / 64-bit primes (Montgomery window kernels)
+    and prime32 (prime32.rs:632-1025), f3 the native64 CRT negacyclic product (native64.rs:929-1160)."""
+    B = args.batch
+    out = {"metric": "other plans and the Ntt64View layer at N = 2048 (SURVEY.md 8 a4 / a7 / a13 / f3)"}
+
+    def leg(name, run, units, unit, nbytes, workload):
+        K, el, ms = timed_leg(run, torch, barrier, dist, dev)
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"value": world * units * K / el, "unit": unit, "ms_per_step": el / K * 1e3, "kernel_ms": ms,
+                     "steps": K, "config": {"workload": workload, "batch_per_gpu": units},
+                     "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": nbytes}}
+
+    poly = N * 8
+    view = eng.ntt64.Ntt64(SOLINAS_P, N, dev.index).as_view()
+    dec = torch.empty((B, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(dec, SEED + 80, 1 << 23)
+    dec -= 1 << 22  # signed digits in [-2^22, 2^22)
+    ntt, std = torch.empty_like(dec), torch.empty_like(dec)
+    eng.fill_uniform(std, SEED + 81, 0)
+
+    def view_step():
+        view.forward_from_decomp(ntt, dec)
+        view.add_backward_on_power_of_two_modulus(64, std, ntt)
+
+    leg("ntt64_view", view_step, B, "fwd+add_backward pairs/s", B * poly * 6,
+        "Ntt64View forward_from_decomp then add_backward_on_power_of_two_modulus(64), Solinas N=2048")
+    del dec, ntt, std
+    plan = eng.Plan.try_new(N, SOLINAS_P, device=dev.index)
+    acc, a, b = (torch.empty((B, N), dtype=torch.int64, device=dev) for _ in range(3))
+    for i, t in enumerate((acc, a, b)):
+        eng.fill_uniform(t, SEED + 82 + i, SOLINAS_P)
+    leg("mul_accumulate", lambda: plan.mul_accumulate(acc, a, b), B, "polys/s", B * poly * 4,
+        "Plan::mul_accumulate acc += a b mod p, Solinas N=2048")
+    del acc, a, b
+    for name, p in (("prime64_p62", P62), ("prime64_p64", P64G)):
+        gp = eng.Plan.try_new(N, p, device=dev.index)
+        buf = torch.empty((B, N), dtype=torch.int64, device=dev)
+        eng.fill_uniform(buf, SEED + 85, p)
+
+        def pair(gp=gp, buf=buf):
+            gp.fwd(buf)
+            gp.inv(buf)
+
+        leg(name, pair, B, "fwd+inv NTT pairs/s", B * poly * 4, f"prime64 Plan fwd then inv, N=2048, p={p:#x}")
+        del buf
+    p32 = eng.prime32.Plan.try_new(N, P30, device=dev.index)
+    b32 = torch.empty((B, N), dtype=torch.int64, device=dev)
+    eng.fill_uniform(b32, SEED + 86, P30)
+    b32 = b32.to(torch.int32)
+
+    def pair32():
+        p32.fwd(b32)
+        p32.inv(b32)
+
+    leg("prime32", pair32, B, "fwd+inv NTT pairs/s", B * N * 4 * 4, f"prime32 Plan fwd then inv, N=2048, p={P30}")
+    del b32
+    nb = B // 8
+    nplan = eng.native64.Plan32.try_new(N, dev.index)
+    prod, lhs, rhs = (torch.empty((nb, N), dtype=torch.int64, device=dev) for _ in range(3))
+    eng.fill_uniform(lhs, SEED + 87, 0)
+    eng.fill_uniform(rhs, SEED + 88, 0)
+    leg("native64_polymul", lambda: nplan.negacyclic_polymul(prod, lhs, rhs), nb, "products/s", nb * poly * 3,
+        "native64::Plan32 negacyclic_polymul mod 2^64 (CRT over 32-bit primes), N=2048")
+    return out
+
+
 KS_IN, KS_BASE_LOG, KS_LEVEL = 2048, 4, 4  # PARAM_MESSAGE_2_CARRY_2 keyswitch (ks_pbs.rs:38-39): k*N -> n
 I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: i8 MFMA = 2x the dense bf16 rate (~2.5 PF)
 
@@ -1117,6 +1193,7 @@ def main():
         legs["ks_pbs_fft"] = bench_ks_pbs_fft(args, eng, torch, dev, world, barrier, dist)
         legs["ext_product_fft"] = bench_ext_product_fft(args, eng, torch, dev, world, barrier, dist)
         legs["bsk_conversion"] = bench_bsk_conversion(args, eng, torch, dev, world, barrier, dist)
+        legs["plans"] = bench_plans(args, eng, torch, dev, world, barrier, dist)
         # last before the headline: the external product, an integer-VALU load like the transform's, so the headline
         # always follows the same kind of work (the held clock depends on what ran just before)
         legs["ext_product"] = bench_ext_product(args, eng, torch, dev, world, barrier, dist)

@@ -81,7 +81,7 @@ def test_compact_line_fits_driver_tail():
                             "sample": "s" * 250},
            "host_path": {"blob": "b" * 20000}, "default_stream": {"blob": "b" * 5000}}
     for i, name in enumerate(bench.LEG_ORDER):
-        out[name] = _stub_leg(i, nested=name.startswith("pbs_shapes"))
+        out[name] = _stub_leg(i, nested=name.startswith("pbs_shapes") or name == "plans")
     # config 5 at world 8: the sharded legs nested under pbs / pbs_fft reach the summary
     for name in ("pbs", "pbs_fft"):
         out[name]["sharded"] = dict(_stub_leg(90), scaling="strong", value_with_scatter_gather=2.5e5,
