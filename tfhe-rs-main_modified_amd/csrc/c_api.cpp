@@ -138,6 +138,22 @@ static int plan_create(size_t n, uint64_t p, int device, mi_ntt64_plan** out_pla
     (void)hipFree(plan->d_inv_twid);
     return hip_fail(e, "twiddle upload");
   }
+  if (!plan->goldilocks && p < ((u64)1 << 32)) {  // the Shoup32 transform tables (mi_arith.hpp Shoup32)
+    std::vector<u64> t32(2 * n);
+    for (size_t k = 0; k < n; ++k) {
+      t32[k] = plan->twid[k] | ((u64)(((u128)plan->twid[k] << 32) / p) << 32);
+      t32[n + k] = plan->inv_twid[k] | ((u64)(((u128)plan->inv_twid[k] << 32) / p) << 32);
+    }
+    e = hipMalloc(&plan->d_tw32, 2 * n * sizeof(u64));
+    if (e == hipSuccess) e = hipMemcpy(plan->d_tw32, t32.data(), 2 * n * sizeof(u64), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (plan->d_tw32) (void)hipFree(plan->d_tw32);
+      (void)hipFree(plan->d_twid);
+      (void)hipFree(plan->d_inv_twid);
+      return hip_fail(e, "twiddle upload");
+    }
+    plan->d_itw32 = plan->d_tw32 + n;
+  }
   if (plan->goldilocks && n == 2048) {
     // The twisted factorisation needs the reference's first five stages to use power-of-two
     // twiddles (the Solinas root tower, psi^64 = 8); check it against the tables it was built from.
@@ -280,6 +296,7 @@ int mi_ntt64_plan_destroy(mi_ntt64_plan* plan) {
     if (plan->d_inv_twid) (void)hipFree(plan->d_inv_twid);
     if (plan->d_twist_f) (void)hipFree(plan->d_twist_f);  // d_twist_i points into the same allocation
     if (plan->d_split) (void)hipFree(plan->d_split);
+    if (plan->d_tw32) (void)hipFree(plan->d_tw32);  // d_itw32 points into the same allocation
   }
   delete plan;
   return MI_OK;
@@ -354,7 +371,8 @@ static int check_batch(const mi_ntt64_plan* plan, const void* buf, size_t batch,
 }
 
 // Kernel routing: the twisted shift-twiddle kernel for the Solinas N = 2048 plan, the split transform (top passes +
-// that kernel on 2048-blocks) for Solinas 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN, else the register-window kernels.  One kernel per plan shape; nothing in the environment changes it.
+// that kernel on 2048-blocks) for Solinas 2^12 <= N <= 2^MI_SPLIT_MAX_LOGN, else the register-window kernels (Shoup32
+// arithmetic for p < 2^32, Montgomery above).  One kernel per plan shape; nothing in the environment changes it.
 static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t* buf, size_t batch, size_t stride,
                                    hipStream_t s) {
   if (plan->twisted)
@@ -362,6 +380,9 @@ static hipError_t launch_transform(bool fwd, const mi_ntt64_plan* plan, uint64_t
   if (plan->d_split)
     return mi::launch_ntt_split(fwd, plan->logn, buf, batch, stride, fwd ? plan->d_twid : plan->d_inv_twid,
                                 plan->split_tables(), s);
+  if (plan->d_tw32)
+    return mi::launch_ntt_shoup32(fwd, plan->logn, (uint32_t)plan->p, buf, nullptr, batch, stride,
+                                  fwd ? plan->d_tw32 : plan->d_itw32, s);
   return mi::launch_ntt(fwd, plan->logn, plan->goldilocks, plan->mp, buf, batch, stride,
                         fwd ? plan->d_twid : plan->d_inv_twid, s);
 }
@@ -1109,8 +1130,8 @@ static int run_ntt32(bool fwd, const mi_ntt32_plan* plan, uint32_t* buf, size_t 
   int st = check_batch(q, buf, batch, stride);
   if (st != MI_OK || batch == 0) return st;
   DeviceGuard g(q->device);
-  hipError_t e = mi::launch_ntt_u32(fwd, q->logn, q->mp, buf, batch, stride, fwd ? q->d_twid : q->d_inv_twid,
-                                    (hipStream_t)stream);
+  hipError_t e = mi::launch_ntt_shoup32(fwd, q->logn, (uint32_t)q->p, nullptr, buf, batch, stride,
+                                        fwd ? q->d_tw32 : q->d_itw32, (hipStream_t)stream);
   return e == hipSuccess ? MI_OK : hip_fail(e, fwd ? "fwd launch" : "inv launch");
 }
 

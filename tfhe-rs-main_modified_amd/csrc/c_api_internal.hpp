@@ -31,6 +31,9 @@ struct mi_ntt64_plan {
   u64 c_normalize = 0, c_man = 0, c_macc = 0;  // device constants of the pointwise ops
   u64* d_twid = nullptr;
   u64* d_inv_twid = nullptr;
+  // p < 2^32 (not Solinas): the transforms' Shoup32 tables, w | floor(w 2^32 / p) << 32, forward then inverse (2 N)
+  u64* d_tw32 = nullptr;
+  u64* d_itw32 = nullptr;
   // twisted N = 2048 Solinas transform (ntt64_tw.hip): rho_i^j and rho_i^-j, 64 i + j
   u64* d_twist_f = nullptr;
   u64* d_twist_i = nullptr;

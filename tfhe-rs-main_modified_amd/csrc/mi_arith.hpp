@@ -134,4 +134,28 @@ struct Montgomery {
   }
 };
 
+// Odd modulus p < 2^32 (r6: prime32 plans and the CRT primes of the native plans).  A twiddle table entry packs w in
+// its low half and Shoup's quotient w' = floor(w 2^32 / p) in its high half: x w mod p = x w - floor(x w' / 2^32) p,
+// which lies in [0, 2p), then one conditional subtraction (v_mul_hi_u32 + two v_mad_u64_u32 instead of Montgomery's
+// two 64 x 64 products).  Values live in the low 32 bits of u64 registers, canonical, so the results are the same
+// residues as the Montgomery form's (bit-exact).
+struct Shoup32 {
+  uint32_t p;
+  __device__ __forceinline__ u64 add(u64 a, u64 b) const {
+    const uint32_t x = (uint32_t)a, y = (uint32_t)b, neg_y = p - y;
+    return x >= neg_y ? x - neg_y : x + y;
+  }
+  __device__ __forceinline__ u64 sub(u64 a, u64 b) const {
+    const uint32_t x = (uint32_t)a, y = (uint32_t)b;
+    return x >= y ? x - y : x + (p - y);
+  }
+  // x < 2^32, wv = w | w' << 32 with w < p
+  __device__ __forceinline__ u64 mul(u64 a, u64 wv) const {
+    const uint32_t x = (uint32_t)a, w = (uint32_t)wv, wq = (uint32_t)(wv >> 32);
+    const uint32_t q = __umulhi(x, wq);
+    const u64 r = (u64)x * w - (u64)q * p;
+    return r >= p ? r - p : r;
+  }
+};
+
 }  // namespace mi

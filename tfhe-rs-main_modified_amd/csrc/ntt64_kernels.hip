@@ -418,10 +418,13 @@ hipError_t launch_ntt(bool fwd, int logn, bool goldilocks, const MontParams& mp,
   return fwd ? dispatch<true>(logn, data, batch, stride, tw, m, s) : dispatch<false>(logn, data, batch, stride, tw, m, s);
 }
 
-hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* data, size_t batch, size_t stride,
-                          const uint64_t* tw, hipStream_t s) {
-  Montgomery m{mp.p, mp.pinv, mp.r2};
-  return fwd ? dispatch<true>(logn, data, batch, stride, tw, m, s) : dispatch<false>(logn, data, batch, stride, tw, m, s);
+// p < 2^32 (Shoup32 tables, c_api.cpp plan_create): u64 buffers (data64) or u32 buffers (data32, prime32 plans)
+hipError_t launch_ntt_shoup32(bool fwd, int logn, uint32_t p, u64* data64, uint32_t* data32, size_t batch,
+                              size_t stride, const uint64_t* tw, hipStream_t s) {
+  const Shoup32 m{p};
+  if (data32)
+    return fwd ? dispatch<true>(logn, data32, batch, stride, tw, m, s) : dispatch<false>(logn, data32, batch, stride, tw, m, s);
+  return fwd ? dispatch<true>(logn, data64, batch, stride, tw, m, s) : dispatch<false>(logn, data64, batch, stride, tw, m, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -18,9 +18,10 @@ struct MontParams {
 hipError_t launch_ntt(bool fwd, int logn, bool goldilocks, const MontParams& mp, uint64_t* data,
                       size_t batch, size_t stride, const uint64_t* tw, hipStream_t s);
 
-// prime32 plans (u32 buffers, generic Montgomery arithmetic)
-hipError_t launch_ntt_u32(bool fwd, int logn, const MontParams& mp, uint32_t* data, size_t batch, size_t stride,
-                          const uint64_t* tw, hipStream_t s);
+// p < 2^32 plans (Shoup32 tables): u64 buffers (data64) or the prime32 plans' u32 buffers (data32); prime32 pointwise ops
+// (u32 buffers, Montgomery constants)
+hipError_t launch_ntt_shoup32(bool fwd, int logn, uint32_t p, uint64_t* data64, uint32_t* data32, size_t batch,
+                              size_t stride, const uint64_t* tw, hipStream_t s);
 hipError_t launch_pointwise_u32(int op, const MontParams& mp, uint32_t* out, const uint32_t* a, const uint32_t* b,
                                 size_t n, size_t batch, size_t stride, uint64_t c, hipStream_t s);
 

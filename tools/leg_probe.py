@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time one of bench.py's legs alone (diagnostic; the numbers the bench reports come from bench.py itself):
-  python tools/leg_probe.py <keyswitch|ks32_pbs|ext_product|pbs|pbs_solinas|bsk_conversion> [reps]
+  python tools/leg_probe.py <keyswitch|ks32_pbs|ext_product|pbs|pbs_solinas|bsk_conversion|plans> [reps]
 PROBE_PKG=<dir holding another tfhe_ntt_amd/ with its own .so> runs another build of the package (A/B in one session)."""
 import json
 import os
@@ -27,5 +27,12 @@ for _ in range(reps):
         r = fn(args, eng, torch, dev, 0, 1, lambda: None, None)
     else:
         r = fn(args, eng, torch, dev, 1, lambda: None, None)
+    if "value" not in r:  # a group of legs (plans): one line per member
+        for k, v in r.items():
+            if isinstance(v, dict) and "value" in v:
+                print(json.dumps({"leg": f"{leg}.{k}", "value": v["value"], "unit": v.get("unit"),
+                                  "kernel_ms": v.get("kernel_ms"), "frac": (v.get("roofline") or {}).get("frac"),
+                                  "pkg": os.path.dirname(eng.__file__)}), flush=True)
+        continue
     print(json.dumps({"leg": leg, "value": r["value"], "kernel_ms": r.get("kernel_ms"),
                       "sub": r.get("keyswitch_and_switch"), "pkg": os.path.dirname(eng.__file__)}), flush=True)
