@@ -171,6 +171,11 @@ def test_pointwise_ops(engine, oracle, name):
     tf = dev(full); v = tf[:, :n]
     plan.mul_accumulate(v, dev(np.concatenate([a, a[:, :1]], 1))[:, :n], dev(np.concatenate([b, b[:, :1]], 1))[:, :n])
     assert np.array_equal(host(tf)[:, :n], ora.mul_accumulate(c, a, b))
+    # even stride > N -> the 16-byte path with the per-row offset (the contiguous batch above takes the flat path)
+    full2 = np.concatenate([c, np.zeros((batch, 2), np.uint64)], axis=1)
+    tf2 = dev(full2); v2 = tf2[:, :n]
+    plan.mul_accumulate(v2, dev(np.concatenate([a, a[:, :2]], 1))[:, :n], dev(np.concatenate([b, b[:, :2]], 1))[:, :n])
+    assert np.array_equal(host(tf2)[:, :n], ora.mul_accumulate(c, a, b)) and (host(tf2)[:, n:] == 0).all()
 
 
 def test_polymul_through_ntt(engine, oracle):

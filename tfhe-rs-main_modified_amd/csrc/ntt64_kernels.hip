@@ -441,8 +441,9 @@ __device__ __forceinline__ u64 pw_one(u64 o, u64 a, u64 b, u64 c, const Mod& mod
   return mod.add(o, prod);
 }
 
-// VW = values per lane per iteration (2 -> 16-byte accesses, needs even stride + 16-B alignment)
-template <int OP, int VW, class Mod, class IO = u64>
+// VW = values per lane per iteration (2 -> 16-byte accesses, needs even stride + 16-B alignment); CONTIG: stride == n,
+// the batch is one flat array (no per-element row division)
+template <int OP, int VW, class Mod, class IO = u64, bool CONTIG = false>
 __global__ __launch_bounds__(256) void pointwise_kernel(IO* __restrict__ out, const IO* __restrict__ a,
                                                         const IO* __restrict__ b, uint32_t n, uint32_t batch,
                                                         uint64_t stride, u64 c, Mod mod) {
@@ -450,8 +451,13 @@ __global__ __launch_bounds__(256) void pointwise_kernel(IO* __restrict__ out, co
   const uint64_t total = per_poly * batch;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t poly = i / per_poly;
-    const uint64_t off = poly * stride + VW * (i - poly * per_poly);
+    uint64_t off;
+    if constexpr (CONTIG) {
+      off = VW * i;
+    } else {
+      const uint64_t poly = i / per_poly;
+      off = poly * stride + VW * (i - poly * per_poly);
+    }
     if constexpr (VW == 2) {
       const ulonglong2 ov = *reinterpret_cast<const ulonglong2*>(out + off);
       ulonglong2 av = make_ulonglong2(0, 0), bv = make_ulonglong2(0, 0);
@@ -476,7 +482,10 @@ static hipError_t launch_pw(u64* out, const u64* a, const u64* b, size_t n, size
   uint64_t blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) return hipSuccess;
-  if (vec)
+  if (vec && stride == n)
+    hipLaunchKernelGGL((pointwise_kernel<OP, 2, Mod, u64, true>), dim3((unsigned)blocks), dim3(256), 0, s, out, a, b,
+                       (uint32_t)n, (uint32_t)batch, (uint64_t)stride, c, mod);
+  else if (vec)
     hipLaunchKernelGGL((pointwise_kernel<OP, 2, Mod>), dim3((unsigned)blocks), dim3(256), 0, s, out, a, b,
                        (uint32_t)n, (uint32_t)batch, (uint64_t)stride, c, mod);
   else
