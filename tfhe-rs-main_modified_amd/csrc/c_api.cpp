@@ -1244,6 +1244,16 @@ int mi_native_plan_create(int kind, size_t n, int device, mi_native_plan** out_p
   }
   c.m_lo = (u64)prefix;
   c.m_hi = (u64)(prefix >> 64);
+  for (int k = 0; k < nk.k; ++k) {  // the device's Montgomery constants (native_crt.hip)
+    const u64 p = c.p[k];
+    u64 inv = p;  // Newton: p * inv == 1 mod 2^64
+    for (int it = 0; it < 6; ++it) inv *= 2 - p * inv;
+    c.pinv[k] = (u64)0 - inv;
+    c.r1[k] = (u64)(((u128)1 << 64) % p);
+    c.r2[k] = mi::host::mul_mod(c.r1[k], c.r1[k], p);
+    c.inv_prefix_m[k] = mont_form(c.inv_prefix[k], p);
+    for (int j = 0; j < nk.k; ++j) c.pjk_m[j][k] = mont_form(c.p[j] % p, p);
+  }
   *out_plan = plan;
   return MI_OK;
 }

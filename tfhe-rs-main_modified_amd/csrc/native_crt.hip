@@ -15,7 +15,14 @@
 namespace mi {
 namespace crt {
 
-__device__ __forceinline__ u64 mulmod(u64 a, u64 b, u64 p) { return (u64)(((unsigned __int128)a * b) % p); }
+// the Montgomery form of prime k (REDC(a b) for any a < 2^64 and b < p_k is canonical: a b < R p_k)
+__device__ __forceinline__ Montgomery mont(const CrtConst& c, int k) { return Montgomery{c.p[k], c.pinv[k], c.r2[k]}; }
+
+// x mod p for x < 3p (the CRT primes of one plan lie within a factor of two of each other)
+__device__ __forceinline__ u64 fold3(u64 x, u64 p) {
+  x = x >= p ? x - p : x;
+  return x >= p ? x - p : x;
+}
 
 // one coefficient of a width-bit word array (u128 = two little-endian u64 words)
 __device__ __forceinline__ unsigned __int128 load_value(const void* in, size_t i, int width) {
@@ -32,7 +39,13 @@ __global__ __launch_bounds__(256) void residue_kernel(u64* __restrict__ planes, 
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
     unsigned __int128 v = load_value(in, i, width);
     if (binary) v = c.prime_bits == 32 ? (unsigned __int128)(uint32_t)v : (unsigned __int128)(u64)v;
-    for (int k = 0; k < c.k; ++k) planes[(uint64_t)k * count + i] = (u64)(v % c.p[k]);
+    const u64 lo = (u64)v, hi = (u64)(v >> 64);
+    for (int k = 0; k < c.k; ++k) {
+      const Montgomery m = mont(c, k);
+      u64 r = m.mul(lo, c.r1[k]);                       // REDC(lo (R mod p)) = lo mod p
+      if (width == 128) r = m.add(r, m.mul(hi, c.r2[k]));  // + REDC(hi R^2) = hi 2^64 mod p
+      planes[(uint64_t)k * count + i] = r;
+    }
   }
 }
 
@@ -46,11 +59,13 @@ __global__ __launch_bounds__(256) void reconstruct_kernel(void* __restrict__ out
         v[0] = r;
         continue;
       }
-      // s = sum_{j<k} v_j prod_{l<j} p_l  mod p_k (Horner from the top digit)
-      u64 s = v[k - 1] % c.p[k];
-      for (int j = k - 2; j >= 0; --j) s = (mulmod(s, c.p[j] % c.p[k], c.p[k]) + v[j]) % c.p[k];
-      const u64 d = r >= s ? r - s : r + c.p[k] - s;
-      v[k] = mulmod(d, c.inv_prefix[k], c.p[k]);
+      // s = sum_{j<k} v_j prod_{l<j} p_l  mod p_k (Horner from the top digit), in Montgomery products by constants
+      const Montgomery m = mont(c, k);
+      const u64 pk = c.p[k];
+      u64 s = fold3(v[k - 1], pk);
+      for (int j = k - 2; j >= 0; --j) s = m.add(m.mul(s, c.pjk_m[j][k]), fold3(v[j], pk));
+      const u64 d = r >= s ? r - s : r + pk - s;
+      v[k] = m.mul(d, c.inv_prefix_m[k]);
     }
     unsigned __int128 acc = 0;  // sum v_k * prod_{l<k} p_l  mod 2^128
     for (int k = 0; k < c.k; ++k) {

@@ -97,6 +97,10 @@ struct CrtConst {
   int k = 0, prime_bits = 32;
   uint64_t p[MI_CRT_MAX] = {}, inv_prefix[MI_CRT_MAX] = {}, prefix_lo[MI_CRT_MAX] = {}, prefix_hi[MI_CRT_MAX] = {};
   uint64_t m_lo = 0, m_hi = 0;
+  // Montgomery constants per prime (R = 2^64; r6: the residue split and the Garner steps without 128-bit division):
+  // pinv = -p^-1 mod R, r1 = R mod p, r2 = R^2 mod p, inv_prefix_m = inv_prefix R mod p, pjk_m[j][k] = (p_j mod p_k) R mod p_k
+  uint64_t pinv[MI_CRT_MAX] = {}, r1[MI_CRT_MAX] = {}, r2[MI_CRT_MAX] = {}, inv_prefix_m[MI_CRT_MAX] = {};
+  uint64_t pjk_m[MI_CRT_MAX][MI_CRT_MAX] = {};
 };
 hipError_t launch_crt_residues(uint64_t* planes, const void* in, size_t count, int width, int binary,
                                const CrtConst& c, hipStream_t s);
