@@ -37,6 +37,7 @@ def test_prime32_plan_parity(engine, oracle, n):
         g = np.random.default_rng(p % 1000 + n)
         x = g.integers(0, p, size=(5, n), dtype=np.uint64).astype(np.uint32)
         x[0, :3] = [0, p - 1, 1]
+        x[1] = p - 1  # a whole row at the top of the range (the Shoup32 sums and products near 2^32 at lo31)
         t = dev(x, np.int32)
         plan.fwd(t)
         want = np.stack([ref.fwd(r.astype(np.uint64)) for r in x])
